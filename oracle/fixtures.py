@@ -1,0 +1,45 @@
+"""Deterministic inputs shared by the fixture generator and the tests.
+
+TEST INFRASTRUCTURE ONLY (see oracle/unet_oracle.py header).
+
+Synthetic batch definition (SURVEY.md §8d "Synthetic inputs"):
+* x ~ U[0,1) float32 (N,C,H,W) -- the range of ToTensor (utils/dataset.py:96)
+* target ~ Bernoulli(0.4) int64 (N,Ho,Wo) -- mean foreground of man_seg000
+* weight map = 10 + 1/freq(class) per image -- what scripts/preprocess_data.py
+  actually produces (its line 47 leaves d1 = d2 = 0, so w = w_c + w0*exp(0) ...
+  reduces to a per-class constant).
+"""
+from __future__ import annotations
+
+import zlib
+
+import numpy as np
+
+from . import unet_oracle as O
+
+
+def make_inputs(seed: int, n: int, c: int, h: int, w: int | None = None):
+    w = h if w is None else w
+    ho, wo = O.output_size(h), O.output_size(w)
+    x = O.hash_uniform(seed, 1000, n * c * h * w).astype(np.float32).reshape(n, c, h, w)
+    tgt = (O.hash_uniform(seed, 1001, n * ho * wo) < 0.4).astype(np.int64).reshape(n, ho, wo)
+    wmap = class_weight_map(tgt)
+    return x, tgt, wmap
+
+
+def class_weight_map(tgt: np.ndarray) -> np.ndarray:
+    """10 + 1/freq(class), per image (float32)."""
+    out = np.empty(tgt.shape, np.float32)
+    for i in range(tgt.shape[0]):
+        t = tgt[i]
+        f1 = max(t.mean(), 1e-6)
+        f0 = max(1.0 - t.mean(), 1e-6)
+        out[i] = np.where(t > 0, 10.0 + 1.0 / f1, 10.0 + 1.0 / f0)
+    return out
+
+
+def sample_indices(name: str, size: int, k: int = 32) -> np.ndarray:
+    """Fixed per-parameter sample positions for gradient digests."""
+    s = zlib.crc32(name.encode())
+    u = O.hash_uniform(s, 77, k)
+    return np.unique((u * size).astype(np.int64).clip(0, size - 1))
