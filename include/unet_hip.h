@@ -1,0 +1,165 @@
+/*
+ * unet_hip.h -- C-ABI of libunet_hip.so, the MI355X (gfx950) implementation of
+ * the valid-convolution U-Net training / inference hot path of
+ * SaurabhIndi/unet-segmentation (reference snapshot 2025-07-25).
+ *
+ * The reference has no FFI: its boundary is the nn.Module API
+ *   models/unet_model.py:66   UNet(n_channels, n_classes, bilinear=False)
+ *   models/unet_model.py:105  UNet.forward(x) -> logits (N, n_classes, H-184, W-184)
+ *   utils/losses.py:29        WeightedCrossEntropyLoss.forward(inputs, targets, weight_maps)
+ *   scripts/train.py:97,131   optim.SGD(lr=1e-4, momentum=0.99).step()
+ * These entry points are what a Python (ctypes) binding of that boundary calls;
+ * unet-segmentation_amd/unet_amd/_lib.py is that binding.
+ *
+ * Conventions
+ *  - Every pointer is a DEVICE pointer unless the name says host_.  Buffers are
+ *    owned by the caller (PyTorch caching allocator); the library never
+ *    allocates device memory.
+ *  - Activations are NHWC float32 ("_nhwc"); the network input x and the
+ *    logits use the reference's NCHW layout.
+ *  - Parameter tables are host arrays of device pointers in the reference
+ *    state_dict order (136 entries incl. BN buffers; 82 gradient entries in
+ *    named_parameters order).  Shapes are PyTorch's (Conv2d OIHW,
+ *    ConvTranspose2d IOHW).
+ *  - stream is a hipStream_t (torch.cuda.current_stream().cuda_stream).
+ *  - Return 0 on success, a negative errno-style code on bad arguments
+ *    (-EINVAL) or a HIP launch failure (-EIO); never throws across the ABI.
+ *    unet_last_error() returns a static message for the last failure.
+ */
+#ifndef UNET_HIP_H
+#define UNET_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef void* unet_stream_t; /* hipStream_t */
+
+const char* unet_version(void);
+const char* unet_last_error(void);
+
+/* ------------------------------------------------------------------------
+ * Whole-network plan: one plan per (N, C, H, W, n_classes).  Replaces the
+ * body of UNet.forward (models/unet_model.py:105-146) and autograd's backward
+ * through it.
+ * ---------------------------------------------------------------------- */
+typedef struct unet_plan unet_plan;
+
+/* Create a plan; returns NULL (and sets unet_last_error) for sizes the valid
+ * U-Net cannot take (models/unet_model.py:189: out = in - 184 for clean sizes). */
+unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes);
+void unet_plan_destroy(unet_plan* p);
+/* Output spatial size and the workspace the caller must provide. */
+int unet_plan_out_hw(const unet_plan* p, int* out_h, int* out_w);
+size_t unet_plan_workspace_bytes(const unet_plan* p);
+int unet_plan_num_params(const unet_plan* p);  /* 136 (state_dict entries) */
+int unet_plan_num_grads(const unet_plan* p);   /* 82 */
+
+/* Forward.  train=1: BatchNorm uses batch statistics and updates the running
+ * buffers in place (momentum 0.1, unbiased var, num_batches_tracked += 1);
+ * train=0: running statistics (scripts/predict.py:70 model.eval()).
+ * host_params[136]: device pointers of the state_dict tensors.
+ * x_nchw: (N, C, H, W) float32 contiguous.  logits_nchw: (N, K, Ho, Wo).
+ * workspace: unet_plan_workspace_bytes() bytes, 256-B aligned; it holds the
+ * activations the backward needs, so keep it alive until unet_plan_backward. */
+int unet_plan_forward(unet_plan* p, void* const* host_params, const float* x_nchw,
+                      float* logits_nchw, void* workspace, int train, unet_stream_t stream);
+
+/* Backward of the whole network for dlogits (N, K, Ho, Wo).  Writes (does not
+ * accumulate) the 82 parameter gradients to host_grads[].  Segments let a
+ * data-parallel caller all-reduce finished gradients while the rest runs:
+ * segment s in [seg_begin, seg_end) of unet_plan_num_segments(); the full
+ * backward is (0, num_segments).  unet_plan_segment_grads() lists, for a
+ * segment, which gradient entries are final after it.  x_nchw is the forward
+ * input (inc.c0's weight gradient reads it). */
+int unet_plan_num_segments(const unet_plan* p);
+int unet_plan_segment_grads(const unet_plan* p, int seg, int* first_grad, int* n_grads);
+int unet_plan_backward(unet_plan* p, void* const* host_params, void* const* host_grads,
+                       const float* x_nchw, const float* dlogits_nchw, void* workspace,
+                       int seg_begin, int seg_end, unet_stream_t stream);
+
+/* Optional per-kernel timing of the next forward/backward: the plan records a
+ * hipEvent pair around each launch (class ids below).  unet_plan_timing()
+ * returns accumulated milliseconds and algorithmic FLOP/bytes per class. */
+enum {
+  UNET_KC_CONV_FWD = 0, UNET_KC_CONV_DGRAD = 1, UNET_KC_CONV_WGRAD = 2,
+  UNET_KC_STAGE1 = 3,   /* inc.c0 fwd + its BN/ReLU passes (memory-bound) */
+  UNET_KC_ELEMWISE = 4, /* BN / pool / head / repack passes */
+  UNET_KC_COUNT = 5
+};
+int unet_plan_set_timing(unet_plan* p, int enable);
+int unet_plan_timing(const unet_plan* p, double* ms, double* flops, double* bytes, int* launches);
+
+/* ------------------------------------------------------------------------
+ * Loss: WeightedCrossEntropyLoss (utils/losses.py:29-57) fused fwd+bwd.
+ * logits (N, K, H, W) contiguous; targets int64 and weights float32 are read
+ * through element strides (the caller's center-cropped views,
+ * scripts/train.py:118-126, need no copy).  Writes loss (1 float) and
+ * dlogits = w*(softmax - onehot)/(N*H*W) * grad_scale.  ws: 64*8 bytes. */
+int unet_wce_fwd_bwd(const float* logits, const int64_t* targets, const float* weights,
+                     int n, int k, int h, int w,
+                     const int64_t* t_strides /*host, 3*/, const int64_t* w_strides /*host, 3*/,
+                     float* loss_out, float* dlogits, float grad_scale, void* ws,
+                     unet_stream_t stream);
+/* dlogits *= g[0] (the upstream scalar gradient, device), in place. */
+int unet_scale_by_device_scalar(float* x, size_t n, const float* g, unet_stream_t stream);
+
+/* SGD with momentum (torch.optim.SGD, dampening 0, no weight decay), flat,
+ * on the gradient g*grad_scale (grad_scale = 1/world after a SUM all-reduce):
+ * first_step: buf = g; else buf = momentum*buf + g;  p -= lr*buf.
+ * p, g, buf 16-byte aligned.  scripts/train.py:97,131. */
+int unet_sgd_momentum(float* p, const float* g, float* buf, size_t n, float lr, float momentum,
+                      float grad_scale, int first_step, unet_stream_t stream);
+
+/* Binary IoU of two uint8 masks (utils/metrics.py:6-37), counts on device:
+ * out[0] = |pred>0 & gt>0|, out[1] = |pred>0 | gt>0| (uint64). */
+int unet_iou_counts(const uint8_t* pred, const uint8_t* gt, size_t n, unsigned long long* out,
+                    unet_stream_t stream);
+/* mask = (logit1 > logit0) * 255 (scripts/predict.py:85-92), logits NCHW K=2. */
+int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int w,
+                          unet_stream_t stream);
+
+/* ------------------------------------------------------------------------
+ * Per-op entry points (used by the op-level parity tests and by tools).
+ * Shapes: x (N,H,W,Ci) NHWC; W OIHW as in PyTorch; outputs NHWC.
+ * ---------------------------------------------------------------------- */
+/* y = conv3x3_valid(x) + b; optional BN+ReLU transform of x on load
+ * (x_scale/x_shift per Ci channel, NULL = identity).  ws >= unet_conv_ws_bytes(). */
+int unet_conv3x3_fwd(const float* x, int n, int h, int w, int ci, const float* wt_oihw,
+                     const float* bias, int co, const float* x_scale, const float* x_shift,
+                     float* y, void* ws, unet_stream_t stream);
+/* dx = full-correlation(dy, W) (input gradient).  dy (N,H-2,W-2,Co). */
+int unet_conv3x3_dgrad(const float* dy, int n, int h, int w, int ci, const float* wt_oihw,
+                       int co, float* dx, void* ws, unet_stream_t stream);
+/* dW (OIHW) = sum over pixels of x (x) dy;  db = sum dy. */
+int unet_conv3x3_wgrad(const float* x, const float* dy, int n, int h, int w, int ci, int co,
+                       float* dw_oihw, float* db, void* ws, unet_stream_t stream);
+size_t unet_conv_ws_bytes(int n, int h, int w, int ci, int co);
+/* ConvTranspose2d(k=2, s=2): y (N,2H,2W,Co) = convT(x) + b;  W (Ci,Co,2,2). */
+int unet_convT2_fwd(const float* x, int n, int h, int w, int ci, const float* wt, const float* bias,
+                    int co, float* y, void* ws, unet_stream_t stream);
+/* ConvTranspose2d backward: dx, dW (IOHW), db.  ws >= unet_conv_ws_bytes(n,h,w,ci,co). */
+int unet_convT2_bwd(const float* x, const float* dy, int n, int h, int w, int ci, const float* wt,
+                    int co, float* dx, float* dw, float* db, void* ws, unet_stream_t stream);
+/* MaxPool2d(2) floor mode, first max wins; argmax index 0..3 per output. */
+int unet_maxpool2_fwd(const float* x, int n, int h, int w, int c, float* y, uint8_t* arg,
+                      unet_stream_t stream);
+int unet_maxpool2_bwd(const float* dy, const uint8_t* arg, int n, int h, int w, int c, float* dx,
+                      unet_stream_t stream);
+/* BatchNorm2d train forward over (N,H,W) per channel (+ running-stat update)
+ * and backward; y = (x-mean)*invstd*gamma + beta. */
+int unet_bn_train_fwd(const float* x, int n, int h, int w, int c, const float* gamma,
+                      const float* beta, float* running_mean, float* running_var, float* y,
+                      float* save_mean, float* save_invstd, void* ws, unet_stream_t stream);
+int unet_bn_train_bwd(const float* x, const float* dy, int n, int h, int w, int c,
+                      const float* gamma, const float* save_mean, const float* save_invstd,
+                      float* dx, float* dgamma, float* dbeta, void* ws, unet_stream_t stream);
+size_t unet_bn_ws_bytes(int c);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* UNET_HIP_H */

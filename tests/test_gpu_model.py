@@ -1,0 +1,206 @@
+"""Whole-network parity on the GPU: the drop-in UNet / WeightedCrossEntropyLoss
+(through libunet_hip.so) vs the CPU oracle (float64) and vs the golden
+fixtures produced by the reference itself (tests/golden/make_golden.py).
+
+Tolerances (from the measured fp32 noise floor):
+  logits <= 1e-3 abs; loss <= 1e-4 rel; argmax masks exact where the oracle
+  margin |l1-l0| > 1e-3; parameter grads rel-L2 <= 1e-2 per tensor except the
+  22 BN-cancelled biases (abs <= 1e-3 * max|grad of their weight|).
+"""
+import os
+
+import numpy as np
+import pytest
+
+from oracle import unet_oracle as O
+from oracle import fixtures as F
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+G = os.path.join(os.path.dirname(__file__), "golden")
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _need_gpu():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+
+
+def make_model(params, n_channels=1, n_classes=2):
+    from unet_amd import UNet
+    m = UNet(n_channels, n_classes)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    return m.cuda()
+
+
+def grads_of(m):
+    return {n: p.grad.detach().double().cpu().numpy() for n, p in m.named_parameters()}
+
+
+def check_grads(gpu, ref, tol=1e-2):
+    worst = 0.0
+    for name, g in gpu.items():
+        r = np.asarray(ref[name], np.float64)
+        if O.bn_cancelled(name):
+            wname = name.replace(".bias", ".weight")
+            scale = np.abs(ref[wname]).max()
+            assert np.abs(g).max() <= 1e-3 * scale, name
+            continue
+        e = np.linalg.norm(g - r) / max(np.linalg.norm(r), 1e-30)
+        worst = max(worst, e)
+        assert e <= tol, (name, e)
+    return worst
+
+
+@pytest.mark.parametrize("n,h,seed", [(2, 188, 11), (2, 204, 12), (1, 220, 13)])
+def test_train_step_vs_oracle(n, h, seed):
+    from unet_amd import WeightedCrossEntropyLoss
+    params = O.hash_init(1, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
+    net = O.UNetOracle(params)
+    rl, cache, nb = net.forward(x)
+    rloss, rdl = O.weighted_ce(rl, tgt, wmap)
+    rg = net.backward(rdl, cache)
+
+    m = make_model(params)
+    m.train()
+    xd = torch.from_numpy(x).cuda()
+    logits = m(xd)
+    loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+    loss.backward()
+    torch.cuda.synchronize()
+    lg = logits.detach().double().cpu().numpy()
+    assert np.abs(lg - rl).max() <= 1e-3
+    assert abs(loss.item() - rloss) <= 1e-4 * abs(rloss)
+    worst = check_grads(grads_of(m), rg)
+    print(f"worst grad rel-L2 {worst:.2e}, max logit err {np.abs(lg - rl).max():.2e}")
+    sd = m.state_dict()
+    for k, v in nb.items():
+        if "running" in k:
+            np.testing.assert_allclose(sd[k].cpu().numpy(), v, rtol=1e-4, atol=1e-5, err_msg=k)
+        elif "num_batches" in k:
+            assert int(sd[k]) == int(v)
+    # eval forward with the updated running stats (scripts/predict.py:70)
+    p2 = dict(params)
+    p2.update(nb)
+    le, _, _ = O.UNetOracle(p2).forward(x, train=False)
+    m.eval()
+    with torch.no_grad():
+        ge = m(xd).double().cpu().numpy()
+    assert np.abs(ge - le).max() <= 1e-3
+
+
+@pytest.mark.parametrize("tag", ["n2_188", "n2_204"])
+def test_vs_reference_fixture(tag):
+    z = np.load(os.path.join(G, f"model_{tag}.npz"), allow_pickle=False)
+    from unet_amd import WeightedCrossEntropyLoss
+    seed, n, h, c = int(z["x_seed"]), int(z["n"]), int(z["h"]), int(z["c"])
+    params = O.hash_init(c, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, c, h)
+    m = make_model(params, c)
+    logits = m(torch.from_numpy(x).cuda())
+    loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+    loss.backward()
+    lg = logits.detach().double().cpu().numpy()
+    assert np.abs(lg - z["logits"]).max() <= 1e-3
+    assert abs(loss.item() - float(z["loss"])) <= 1e-4 * abs(float(z["loss"]))
+    margin = np.abs(z["logits"][:, 1] - z["logits"][:, 0])
+    sure = margin > 1e-3
+    np.testing.assert_array_equal((lg[:, 1] > lg[:, 0])[sure], (z["logits"][:, 1] > z["logits"][:, 0])[sure])
+    for name, p in m.named_parameters():
+        g = p.grad.detach().double().cpu().numpy().ravel()
+        ref_norm = float(z[f"gnorm/{name}"])
+        if O.bn_cancelled(name):
+            wn = float(z[f"gnorm/{name.replace('.bias', '.weight')}"])
+            assert np.abs(g).max() <= 1e-3 * wn, name
+            continue
+        assert abs(np.linalg.norm(g) - ref_norm) <= 1e-2 * ref_norm, name
+        idx = z[f"gidx/{name}"]
+        np.testing.assert_allclose(g[idx], z[f"gval/{name}"], atol=2e-2 * np.abs(z[f"gval/{name}"]).max() + 1e-7,
+                                   err_msg=name)
+
+
+@pytest.mark.parametrize("tag", ["n1_512", "n1_c3_572"])
+def test_full_size_forward_vs_reference_fixture(tag):
+    """512x512x1 (configs[0]/[1] tile) and 3-ch 572x572 (configs[4]) forward."""
+    from unet_amd import WeightedCrossEntropyLoss
+    z = np.load(os.path.join(G, f"fwd_{tag}.npz"), allow_pickle=False)
+    seed, n, h, c = int(z["x_seed"]), int(z["n"]), int(z["h"]), int(z["c"])
+    params = O.hash_init(c, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, c, h)
+    m = make_model(params, c)
+    with torch.no_grad():
+        logits = m(torch.from_numpy(x).cuda())
+        loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+    lg = logits.double().cpu().numpy()
+    assert lg.shape[-1] == O.output_size(h)
+    assert np.abs(lg[:, :, ::7, ::5] - z["logits_sample"]).max() <= 1e-3
+    assert abs(loss.item() - float(z["loss"])) <= 1e-4 * abs(float(z["loss"]))
+    mask = lg[:, 1] > lg[:, 0]
+    sure = z["margin"] > 1e-3
+    np.testing.assert_array_equal(mask[sure], z["mask"].astype(bool)[sure])
+    print(f"{tag}: {int((~sure).sum())} low-margin pixels of {sure.size}")
+
+
+def test_hela_real_frames_masks_and_iou():
+    """Real DIC-C2DH-HeLa frames (01, 01_ST/SEG): eval-mode masks and IoU
+    (utils/metrics.py:6-37) vs the reference run on the same weights."""
+    z = np.load(os.path.join(G, "hela_real.npz"), allow_pickle=False)
+    params = O.hash_init(1, 2, seed=int(z["seed"]), bn_random=True)
+    for k in z.files:
+        if k.startswith("buf/"):
+            params[k[4:]] = z[k].astype(np.float32)
+    m = make_model(params)
+    m.eval()
+    x = (z["images"].astype(np.float32)[:, None] / 255.0) * 2.0 - 1.0
+    with torch.no_grad():
+        logits = m(torch.from_numpy(x).cuda())
+    from unet_amd import _lib
+    import ctypes
+    lib = _lib.load()
+    mask = torch.empty((x.shape[0], 324, 324), dtype=torch.uint8, device="cuda")
+    _lib.check(lib.unet_mask_from_logits(logits.data_ptr(), mask.data_ptr(), x.shape[0], 324, 324,
+                                         _lib.stream_of()), "mask")
+    mk = mask.cpu().numpy()
+    sure = z["margin"] > 1e-3
+    np.testing.assert_array_equal(mk[sure], z["masks"][sure])
+    oy = (512 - 324) // 2
+    gt = z["segs"][:, oy:oy + 324, oy:oy + 324]
+    ious = []
+    for i in range(len(mk)):
+        g = torch.from_numpy(gt[i].astype(np.uint8).clip(0, 1) * 255).cuda()
+        cnt = torch.zeros(2, dtype=torch.int64, device="cuda")
+        _lib.check(lib.unet_iou_counts(mask[i].data_ptr(), g.data_ptr(), g.numel(), cnt.data_ptr(),
+                                       _lib.stream_of()), "iou")
+        c = cnt.cpu().numpy()
+        ious.append(c[0] / c[1])
+    np.testing.assert_allclose(ious, z["ious"], atol=1e-3)
+
+
+def test_sgd_trajectory_vs_reference_fixture():
+    """scripts/train.py loop shape: zero_grad, forward, loss, backward,
+    optim.SGD(momentum=0.99).step() -- three steps against the reference."""
+    from unet_amd import WeightedCrossEntropyLoss
+    z = np.load(os.path.join(G, "model_n2_188.npz"), allow_pickle=False)
+    seed, n, h = int(z["x_seed"]), int(z["n"]), int(z["h"])
+    params = O.hash_init(1, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
+    m = make_model(params)
+    xd, td, wd = (torch.from_numpy(a).cuda() for a in (x, tgt, wmap))
+    crit = WeightedCrossEntropyLoss()
+    with torch.no_grad():
+        m(xd)  # the fixture's model had one earlier train-mode forward
+    opt = torch.optim.SGD(m.parameters(), lr=float(z["sgd_lr"]), momentum=0.99)
+    losses = []
+    for _ in range(len(z["sgd_losses"])):
+        opt.zero_grad()
+        lo = crit(m(xd), td, wd)
+        lo.backward()
+        opt.step()
+        losses.append(lo.item())
+    np.testing.assert_allclose(losses, z["sgd_losses"], rtol=1e-3)
+    m.eval()
+    with torch.no_grad():
+        le = m(xd).double().cpu().numpy()
+    ref = z["logits_after_sgd_eval"]
+    assert np.abs(le - ref).max() <= 1e-3 * max(1.0, np.abs(ref).max())

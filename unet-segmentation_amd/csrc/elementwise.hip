@@ -1,0 +1,916 @@
+// Memory-bound kernels of the U-Net hot path (gfx950): the first conv (Ci<=4,
+// HBM-bound), BatchNorm finalize/apply passes, 2x2 max-pool with argmax, the
+// 1x1 head, the fused weighted cross-entropy, SGD-momentum and weight repacks.
+// All NHWC activations are touched as float4 (16 B per lane) so every wave
+// instruction moves 1 KiB of contiguous bytes where the layout allows it.
+#include "unet_internal.h"
+
+namespace unet {
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
+static inline int grid_cap(long long work, int per_block, int cap = 4096) {
+  long long g = (work + per_block - 1) / per_block;
+  if (g < 1) g = 1;
+  return (int)(g < cap ? g : cap);
+}
+
+// Per-channel reduction of (a, b) pairs accumulated by threads that own channel
+// group tid % CG (4 channels each).  One fp64 atomic per channel per block.
+__device__ void reduce_pairs_to_global(const float (&a)[4], const float (&b)[4], int CG, int C,
+                                       double* dst /* [C][2] of this group */) {
+  __shared__ float red[256][9];
+  const int tid = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) { red[tid][k] = a[k]; red[tid][4 + k] = b[k]; }
+  __syncthreads();
+  if (tid < CG) {
+    float sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+    for (int r = tid; r < 256; r += CG) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { sa[k] += red[r][k]; sb[k] += red[r][4 + k]; }
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      atomicAdd(dst + (size_t)(tid * 4 + k) * 2 + 0, (double)sa[k]);
+      atomicAdd(dst + (size_t)(tid * 4 + k) * 2 + 1, (double)sb[k]);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// inc.c0 forward (models/unet_model.py:11 with in_channels = n_channels <= 4):
+// direct 3x3 valid conv from the NCHW network input, 64 output channels NHWC,
+// + conv bias, + BatchNorm batch statistics (sum, sumsq) of the output.
+// Block = one output row segment of 64 pixels; thread = (channel, pixel phase).
+// ---------------------------------------------------------------------------
+template <int CI>
+__global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict__ x, int h, int w,
+                                                        const float* __restrict__ wt,
+                                                        const float* __restrict__ bias, float* __restrict__ y,
+                                                        double* __restrict__ stats) {
+  const int ho = h - 2, wo = w - 2;
+  const int x0 = blockIdx.x * 64, row = blockIdx.y, n = blockIdx.z;
+  __shared__ float tile[CI][3][66];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < CI * 3 * 66; i += 256) {
+    const int ci = i / 198, rem = i - ci * 198, r = rem / 66, cx = rem - r * 66;
+    const int gx = min(x0 + cx, w - 1);
+    tile[ci][r][cx] = x[((size_t)(n * CI + ci) * h + row + r) * w + gx];
+  }
+  const int c = tid & 63, q = tid >> 6;
+  float wr[CI * 9];
+#pragma unroll
+  for (int k = 0; k < CI * 9; ++k) wr[k] = wt[c * CI * 9 + k];
+  const float b = bias[c];
+  __syncthreads();
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll 4
+  for (int j = 0; j < 16; ++j) {
+    const int px = q + 4 * j;
+    const int gx = x0 + px;
+    float acc = b;
+#pragma unroll
+    for (int ci = 0; ci < CI; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) acc = fmaf(tile[ci][ky][px + kx], wr[(ci * 3 + ky) * 3 + kx], acc);
+    if (gx < wo) {
+      y[((size_t)(n * ho + row) * wo + gx) * 64 + c] = acc;
+      s1 += acc;
+      s2 += acc * acc;
+    }
+  }
+  __shared__ float red[4][2][64];
+  red[q][0][c] = s1;
+  red[q][1][c] = s2;
+  __syncthreads();
+  if (tid < 64) {
+    const float a = red[0][0][tid] + red[1][0][tid] + red[2][0][tid] + red[3][0][tid];
+    const float bb = red[0][1][tid] + red[1][1][tid] + red[2][1][tid] + red[3][1][tid];
+    const int grp = (blockIdx.x + blockIdx.y * gridDim.x) % kStatGroups;
+    atomicAdd(stats + ((size_t)grp * 64 + tid) * 2 + 0, (double)a);
+    atomicAdd(stats + ((size_t)grp * 64 + tid) * 2 + 1, (double)bb);
+  }
+}
+
+// inc.c0 weight gradient: dW[co][ci][ky][kx] = sum_p dY[p][co] * x[ci][p+(ky,kx)].
+// Grid-stride over (image, row, 64-pixel segment); per-thread register sums,
+// one fp32 atomic per weight per workgroup.
+template <int CI>
+__global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restrict__ x, int nimg, int h, int w,
+                                                          Src dy, float* __restrict__ dw) {
+  const int ho = h - 2, wo = w - 2;
+  const int nseg = (wo + 63) / 64;
+  const long long items = (long long)nimg * ho * nseg;
+  __shared__ float tile[CI][3][66];
+  const int tid = threadIdx.x, c = tid & 63, q = tid >> 6;
+  float acc[CI * 9];
+#pragma unroll
+  for (int k = 0; k < CI * 9; ++k) acc[k] = 0.f;
+  for (long long it = blockIdx.x; it < items; it += gridDim.x) {
+    const int seg = (int)(it % nseg);
+    const long long t2 = it / nseg;
+    const int row = (int)(t2 % ho), n = (int)(t2 / ho);
+    const int x0 = seg * 64;
+    __syncthreads();
+    for (int i = tid; i < CI * 3 * 66; i += 256) {
+      const int ci = i / 198, rem = i - ci * 198, r = rem / 66, cx = rem - r * 66;
+      const int gx = min(x0 + cx, w - 1);
+      tile[ci][r][cx] = x[((size_t)(n * CI + ci) * h + row + r) * w + gx];
+    }
+    __syncthreads();
+    for (int j = 0; j < 16; ++j) {
+      const int px = q + 4 * j;
+      const int gx = x0 + px;
+      if (gx >= wo) break;
+      const float g = dy.ptr[((size_t)(n * dy.H + row + dy.oy) * dy.W + gx + dy.ox) * dy.C + c];
+#pragma unroll
+      for (int ci = 0; ci < CI; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) acc[(ci * 3 + ky) * 3 + kx] = fmaf(g, tile[ci][ky][px + kx], acc[(ci * 3 + ky) * 3 + kx]);
+    }
+  }
+  __shared__ float red[4][CI * 9][64];
+#pragma unroll
+  for (int k = 0; k < CI * 9; ++k) red[q][k][c] = acc[k];
+  __syncthreads();
+  for (int i = tid; i < CI * 9 * 64; i += 256) {
+    const int k = i / 64, cc = i - k * 64;
+    const float v = red[0][k][cc] + red[1][k][cc] + red[2][k][cc] + red[3][k][cc];
+    atomicAdd(dw + (size_t)cc * CI * 9 + k, v);
+  }
+}
+
+hipError_t launch_conv_first_fwd(const float* x, int n, int ci, int h, int w, const float* wt,
+                                 const float* bias, int co, float* y, double* stats, hipStream_t s) {
+  if (co != 64 || ci < 1 || ci > 4 || h < 3 || w < 3) return hipErrorInvalidValue;
+  dim3 grid(cdiv(w - 2, 64), h - 2, n);
+  switch (ci) {
+    case 1: hipLaunchKernelGGL(k_conv_first_fwd<1>, grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+    case 2: hipLaunchKernelGGL(k_conv_first_fwd<2>, grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+    case 3: hipLaunchKernelGGL(k_conv_first_fwd<3>, grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+    default: hipLaunchKernelGGL(k_conv_first_fwd<4>, grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, const Src& dy, int co,
+                                   float* dw, hipStream_t s) {
+  if (co != 64 || ci < 1 || ci > 4) return hipErrorInvalidValue;
+  const long long items = (long long)n * (h - 2) * cdiv(w - 2, 64);
+  const int grid = (int)(items < 1024 ? items : 1024);
+  switch (ci) {
+    case 1: hipLaunchKernelGGL(k_conv_first_wgrad<1>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, dw); break;
+    case 2: hipLaunchKernelGGL(k_conv_first_wgrad<2>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, dw); break;
+    case 3: hipLaunchKernelGGL(k_conv_first_wgrad<3>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, dw); break;
+    default: hipLaunchKernelGGL(k_conv_first_wgrad<4>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, dw); break;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// BatchNorm2d (train) finalize: grouped fp64 (sum, sumsq) -> batch mean, biased
+// variance, invstd; consumer transform scale = gamma*invstd, shift = beta -
+// mean*scale; running stats: momentum 0.1, unbiased variance; nbt += 1.
+// ---------------------------------------------------------------------------
+__global__ void k_bn_finalize(const double* __restrict__ st, int C, double count, const float* gamma,
+                              const float* beta, float* rmean, float* rvar, int64_t* nbt, float* mean,
+                              float* invstd, float* scale, float* shift, float mom, float eps) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c == 0 && nbt) *nbt += 1;
+  if (c >= C) return;
+  double s1 = 0, s2 = 0;
+  for (int g = 0; g < kStatGroups; ++g) {
+    s1 += st[((size_t)g * C + c) * 2 + 0];
+    s2 += st[((size_t)g * C + c) * 2 + 1];
+  }
+  const double mu = s1 / count;
+  double var = s2 / count - mu * mu;
+  if (var < 0) var = 0;
+  const double is = 1.0 / sqrt(var + (double)eps);
+  const double sc = (double)gamma[c] * is;
+  mean[c] = (float)mu;
+  invstd[c] = (float)is;
+  scale[c] = (float)sc;
+  shift[c] = (float)((double)beta[c] - mu * sc);
+  if (rmean) rmean[c] = (float)((1.0 - mom) * rmean[c] + mom * mu);
+  if (rvar) rvar[c] = (float)((1.0 - mom) * rvar[c] + mom * var * count / (count > 1 ? count - 1 : 1));
+}
+
+__global__ void k_bn_eval_prepare(int C, const float* gamma, const float* beta, const float* rm,
+                                  const float* rv, float* scale, float* shift, float eps) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  const double is = 1.0 / sqrt((double)rv[c] + (double)eps);
+  const double sc = (double)gamma[c] * is;
+  scale[c] = (float)sc;
+  shift[c] = (float)((double)beta[c] - (double)rm[c] * sc);
+}
+
+// BN backward finalize.  With B1 = sum dz', B2 = sum dz'*xhat (dz' = dL/dz after
+// the ReLU mask):  dbeta = B1, dgamma = B2 and
+//   dY = gamma*invstd*(dz' - B1/M - xhat*B2/M)
+//      = k0*dz' + k1*(y - mean) + k2,  k0 = g*is, k1 = -g*is^2*B2/M, k2 = -g*is*B1/M.
+// The conv bias that precedes the BN gets sum_p dY = k0*B1 + k2*M (+ k1*0),
+// which is zero up to rounding (BN-cancelled biases).
+__global__ void k_bnb_finalize(const double* __restrict__ st, int C, double M, const float* gamma,
+                               const float* mean, const float* invstd, float* dgamma, float* dbeta,
+                               float* dbias, float* coef) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double b1 = 0, b2 = 0;
+  for (int g = 0; g < kStatGroups; ++g) {
+    b1 += st[((size_t)g * C + c) * 2 + 0];
+    b2 += st[((size_t)g * C + c) * 2 + 1];
+  }
+  const double gi = (double)gamma[c] * (double)invstd[c];
+  const double k0 = gi, k1 = -gi * (double)invstd[c] * b2 / M, k2 = -gi * b1 / M;
+  if (dgamma) dgamma[c] = (float)b2;
+  if (dbeta) dbeta[c] = (float)b1;
+  if (dbias) dbias[c] = (float)(k0 * b1 + k2 * M);
+  coef[c] = (float)k0;
+  coef[C + c] = (float)k1;
+  coef[2 * C + c] = (float)k2;
+  coef[3 * C + c] = mean[c];
+}
+
+// dYpad[n][y+pad][x+pad][c] = k0*dz + k1*(y - mean) + k2 ; border written as 0.
+__global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restrict__ yr,
+                            const float* __restrict__ coef, int n, int h, int w, int C,
+                            float* __restrict__ dyp, int pad) {
+  const int C4 = C / 4;
+  const int hp = h + 2 * pad, wp = w + 2 * pad;
+  const long long total = (long long)n * hp * wp * C4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    long long p = i / C4;
+    const int xp = (int)(p % wp);
+    p /= wp;
+    const int yp = (int)(p % hp);
+    const int nn = (int)(p / hp);
+    const int yy = yp - pad, xx = xp - pad;
+    float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (yy >= 0 && yy < h && xx >= 0 && xx < w) {
+      const size_t src = (((size_t)nn * h + yy) * w + xx) * C + c4 * 4;
+      const float4 d = ld4(dz + src), yv = ld4(yr + src);
+      const float4 k0 = ld4(coef + c4 * 4), k1 = ld4(coef + C + c4 * 4), k2 = ld4(coef + 2 * C + c4 * 4),
+                   mu = ld4(coef + 3 * C + c4 * 4);
+      out.x = fmaf(k0.x, d.x, fmaf(k1.x, yv.x - mu.x, k2.x));
+      out.y = fmaf(k0.y, d.y, fmaf(k1.y, yv.y - mu.y, k2.y));
+      out.z = fmaf(k0.z, d.z, fmaf(k1.z, yv.z - mu.z, k2.z));
+      out.w = fmaf(k0.w, d.w, fmaf(k1.w, yv.w - mu.w, k2.w));
+    }
+    st4(dyp + i * 4, out);
+  }
+}
+
+hipError_t launch_bn_finalize(const double* stats, int c, double count, const float* gamma, const float* beta,
+                              float* rmean, float* rvar, int64_t* nbt, float* mean, float* invstd, float* scale,
+                              float* shift, float momentum, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(c, 256)), dim3(256), 0, s, stats, c, count, gamma, beta, rmean, rvar,
+                     nbt, mean, invstd, scale, shift, momentum, eps);
+  return hipGetLastError();
+}
+hipError_t launch_bn_eval_prepare(int c, const float* gamma, const float* beta, const float* rmean, const float* rvar,
+                                  float* scale, float* shift, float eps, hipStream_t s) {
+  hipLaunchKernelGGL(k_bn_eval_prepare, dim3(cdiv(c, 256)), dim3(256), 0, s, c, gamma, beta, rmean, rvar, scale, shift,
+                     eps);
+  return hipGetLastError();
+}
+hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const float* gamma, const float* mean,
+                               const float* invstd, float* dgamma, float* dbeta, float* dbias, float* coef,
+                               hipStream_t s) {
+  hipLaunchKernelGGL(k_bnb_finalize, dim3(cdiv(c, 256)), dim3(256), 0, s, bstats, c, count, gamma, mean, invstd,
+                     dgamma, dbeta, dbias, coef);
+  return hipGetLastError();
+}
+hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h, int w, int c,
+                            float* dypad, int pad, hipStream_t s) {
+  if (c % 4) return hipErrorInvalidValue;
+  const long long work = (long long)n * (h + 2 * pad) * (w + 2 * pad) * (c / 4);
+  hipLaunchKernelGGL(k_bnb_apply, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad,
+                     pad);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// MaxPool2d(2) forward (models/unet_model.py:28) of relu(bn(y)): floor mode,
+// scan order (0,0),(0,1),(1,0),(1,1) with strict '>' so the FIRST max wins.
+// ---------------------------------------------------------------------------
+__global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y, uint8_t* __restrict__ arg) {
+  const int C = s.C, C4 = C / 4, ho = h / 2, wo = w / 2;
+  const long long total = (long long)n * ho * wo * C4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c4 = (int)(i % C4);
+    long long p = i / C4;
+    const int xo = (int)(p % wo);
+    p /= wo;
+    const int yo = (int)(p % ho);
+    const int nn = (int)(p / ho);
+    float4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int yy = 2 * yo + (k >> 1), xx = 2 * xo + (k & 1);
+      float4 t = ld4(s.ptr + ((size_t)(nn * s.H + yy + s.oy) * s.W + xx + s.ox) * C + c4 * 4);
+      if (s.scale) {
+        const float4 a = ld4(s.scale + c4 * 4), b = ld4(s.shift + c4 * 4);
+        t.x = fmaxf(fmaf(t.x, a.x, b.x), 0.f);
+        t.y = fmaxf(fmaf(t.y, a.y, b.y), 0.f);
+        t.z = fmaxf(fmaf(t.z, a.z, b.z), 0.f);
+        t.w = fmaxf(fmaf(t.w, a.w, b.w), 0.f);
+      }
+      v[k] = t;
+    }
+    float4 best = v[0];
+    uchar4 a = make_uchar4(0, 0, 0, 0);
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      if (v[k].x > best.x) { best.x = v[k].x; a.x = k; }
+      if (v[k].y > best.y) { best.y = v[k].y; a.y = k; }
+      if (v[k].z > best.z) { best.z = v[k].z; a.z = k; }
+      if (v[k].w > best.w) { best.w = v[k].w; a.w = k; }
+    }
+    st4(y + i * 4, best);
+    *reinterpret_cast<uchar4*>(arg + i * 4) = a;
+  }
+}
+
+hipError_t launch_maxpool_fwd(const Src& s, int n, int h, int w, float* y, uint8_t* arg, hipStream_t st) {
+  if (s.C % 4) return hipErrorInvalidValue;
+  const long long work = (long long)n * (h / 2) * (w / 2) * (s.C / 4);
+  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, st, s, n, h, w, y, arg);
+  return hipGetLastError();
+}
+
+// Maxpool backward fused with the skip-gradient add (the encoder output feeds
+// both the pool and the center-cropped concat, models/unet_model.py:107,130-142),
+// the ReLU mask and the BN-backward statistics of that layer.
+__global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restrict__ dpool,
+                                                           const uint8_t* __restrict__ arg,
+                                                           const float* __restrict__ dskip, int soy, int sox,
+                                                           int sh, int sw, const float* __restrict__ yr,
+                                                           const float* scale, const float* shift,
+                                                           const float* mean, const float* invstd, int n, int h,
+                                                           int w, int C, float* __restrict__ dz,
+                                                           double* __restrict__ bstats) {
+  const int C4 = C / 4;            // channel groups; C4 divides 256 (C <= 1024, power of 2)
+  const int tid = threadIdx.x;
+  const int cg = tid % C4;
+  const int ppb = 256 / C4;        // pixels per block iteration
+  const int ho = h / 2, wo = w / 2;
+  const long long pixels = (long long)n * h * w;
+  float sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+  const int c = cg * 4;
+  float4 sc = make_float4(0, 0, 0, 0), sf = sc, mu = sc, is = sc;
+  if (scale) { sc = ld4(scale + c); sf = ld4(shift + c); mu = ld4(mean + c); is = ld4(invstd + c); }
+  for (long long p = (long long)blockIdx.x * ppb + tid / C4; p < pixels; p += (long long)gridDim.x * ppb) {
+    const int xx = (int)(p % w);
+    const long long t = p / w;
+    const int yy = (int)(t % h);
+    const int nn = (int)(t / h);
+    float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int yo = yy >> 1, xo = xx >> 1;
+    if (yo < ho && xo < wo) {
+      const size_t pi = (((size_t)nn * ho + yo) * wo + xo) * C + c;
+      const uchar4 a = *reinterpret_cast<const uchar4*>(arg + pi);
+      const float4 g = ld4(dpool + pi);
+      const int k = (yy & 1) * 2 + (xx & 1);
+      d.x = (a.x == k) ? g.x : 0.f;
+      d.y = (a.y == k) ? g.y : 0.f;
+      d.z = (a.z == k) ? g.z : 0.f;
+      d.w = (a.w == k) ? g.w : 0.f;
+    }
+    if (dskip && yy >= soy && yy < soy + sh && xx >= sox && xx < sox + sw) {
+      const float4 g = ld4(dskip + (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c);
+      d.x += g.x; d.y += g.y; d.z += g.z; d.w += g.w;
+    }
+    const size_t oi = (size_t)p * C + c;
+    if (scale) {
+      const float4 yv = ld4(yr + oi);
+      d.x = (fmaf(yv.x, sc.x, sf.x) > 0.f) ? d.x : 0.f;
+      d.y = (fmaf(yv.y, sc.y, sf.y) > 0.f) ? d.y : 0.f;
+      d.z = (fmaf(yv.z, sc.z, sf.z) > 0.f) ? d.z : 0.f;
+      d.w = (fmaf(yv.w, sc.w, sf.w) > 0.f) ? d.w : 0.f;
+      sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
+      sb[0] += d.x * (yv.x - mu.x) * is.x;
+      sb[1] += d.y * (yv.y - mu.y) * is.y;
+      sb[2] += d.z * (yv.z - mu.z) * is.z;
+      sb[3] += d.w * (yv.w - mu.w) * is.w;
+    }
+    st4(dz + oi, d);
+  }
+  if (bstats) reduce_pairs_to_global(sa, sb, C4, C, bstats + (size_t)(blockIdx.x % kStatGroups) * C * 2);
+}
+
+hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, const float* dskip, int soy, int sox,
+                                    int sh, int sw, const float* y, const float* scale, const float* shift,
+                                    const float* mean, const float* invstd, int n, int h, int w, int c, float* dz,
+                                    double* bstats, hipStream_t s) {
+  if (c % 4 || (256 % (c / 4)) != 0) return hipErrorInvalidValue;
+  const long long pixels = (long long)n * h * w;
+  const int ppb = 256 / (c / 4);
+  hipLaunchKernelGGL(k_maxpool_bwd_fused, dim3(grid_cap(pixels, ppb * 4, 4096)), dim3(256), 0, s, dpool, arg, dskip,
+                     soy, sox, sh, sw, y, scale, shift, mean, invstd, n, h, w, c, dz, bstats);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// OutConv 1x1 head (models/unet_model.py:56-63): logits[n][k][y][x] =
+// b[k] + sum_c W[k][c] * relu(bn(y))[c].  16 lanes per pixel (C = 64).
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void k_head_fwd(Src s, int n, int h, int w, const float* __restrict__ wt,
+                                                  const float* __restrict__ bias, float* __restrict__ logits) {
+  const int tid = threadIdx.x, sub = tid & 15;
+  const long long pixels = (long long)n * h * w;
+  const int c = sub * 4;
+  float4 wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wk[k] = ld4(wt + k * 64 + c);
+  float4 sc = make_float4(1, 1, 1, 1), sf = make_float4(0, 0, 0, 0);
+  if (s.scale) { sc = ld4(s.scale + c); sf = ld4(s.shift + c); }
+  for (long long p = (long long)blockIdx.x * 16 + (tid >> 4); p < pixels; p += (long long)gridDim.x * 16) {
+    const int xx = (int)(p % w);
+    const long long t = p / w;
+    const int yy = (int)(t % h);
+    const int nn = (int)(t / h);
+    float4 v = ld4(s.ptr + ((size_t)(nn * s.H + yy + s.oy) * s.W + xx + s.ox) * 64 + c);
+    if (s.scale) {
+      v.x = fmaxf(fmaf(v.x, sc.x, sf.x), 0.f);
+      v.y = fmaxf(fmaf(v.y, sc.y, sf.y), 0.f);
+      v.z = fmaxf(fmaf(v.z, sc.z, sf.z), 0.f);
+      v.w = fmaxf(fmaf(v.w, sc.w, sf.w), 0.f);
+    }
+    float acc[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      acc[k] = v.x * wk[k].x + v.y * wk[k].y + v.z * wk[k].z + v.w * wk[k].w;
+#pragma unroll
+      for (int o = 8; o >= 1; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
+    }
+    if (sub < K) {
+      float val = acc[0];
+#pragma unroll
+      for (int k = 1; k < K; ++k)
+        if (sub == k) val = acc[k];
+      logits[(((size_t)nn * K + sub) * h + yy) * w + xx] = val + bias[sub];
+    }
+  }
+}
+
+// head backward: dz = W^T dl masked by ReLU'(bn(y)) (+ BN-bwd stats), dW, db.
+template <int K>
+__global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict__ dl, int n, int h, int w,
+                                                  const float* __restrict__ wt, const float* __restrict__ mean,
+                                                  const float* __restrict__ invstd, float* __restrict__ dz,
+                                                  double* __restrict__ bstats, double* __restrict__ acc_out) {
+  const int tid = threadIdx.x, sub = tid & 15;
+  const long long pixels = (long long)n * h * w;
+  const int c = sub * 4;
+  float4 wk[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) wk[k] = ld4(wt + k * 64 + c);
+  const float4 sc = ld4(s.scale + c), sf = ld4(s.shift + c), mu = ld4(mean + c), is = ld4(invstd + c);
+  float dwa[K][4], dba[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    dba[k] = 0.f;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) dwa[k][j] = 0.f;
+  }
+  float sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+  const long long hw = (long long)h * w;
+  for (long long p = (long long)blockIdx.x * 16 + (tid >> 4); p < pixels; p += (long long)gridDim.x * 16) {
+    const int nn = (int)(p / hw);
+    const long long r = p - nn * hw;
+    const size_t ii = ((size_t)(nn * s.H + (int)(r / w) + s.oy) * s.W + (int)(r % w) + s.ox) * 64 + c;
+    const float4 yv = ld4(s.ptr + ii);
+    float g[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) g[k] = dl[((size_t)nn * K + k) * hw + r];
+    const float zx = fmaf(yv.x, sc.x, sf.x), zy = fmaf(yv.y, sc.y, sf.y), zz = fmaf(yv.z, sc.z, sf.z),
+                zw = fmaf(yv.w, sc.w, sf.w);
+    float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      d.x = fmaf(wk[k].x, g[k], d.x);
+      d.y = fmaf(wk[k].y, g[k], d.y);
+      d.z = fmaf(wk[k].z, g[k], d.z);
+      d.w = fmaf(wk[k].w, g[k], d.w);
+      dwa[k][0] += g[k] * fmaxf(zx, 0.f);
+      dwa[k][1] += g[k] * fmaxf(zy, 0.f);
+      dwa[k][2] += g[k] * fmaxf(zz, 0.f);
+      dwa[k][3] += g[k] * fmaxf(zw, 0.f);
+      dba[k] += g[k];
+    }
+    d.x = zx > 0.f ? d.x : 0.f;
+    d.y = zy > 0.f ? d.y : 0.f;
+    d.z = zz > 0.f ? d.z : 0.f;
+    d.w = zw > 0.f ? d.w : 0.f;
+    sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
+    sb[0] += d.x * (yv.x - mu.x) * is.x;
+    sb[1] += d.y * (yv.y - mu.y) * is.y;
+    sb[2] += d.z * (yv.z - mu.z) * is.z;
+    sb[3] += d.w * (yv.w - mu.w) * is.w;
+    st4(dz + (size_t)p * 64 + c, d);
+  }
+  reduce_pairs_to_global(sa, sb, 16, 64, bstats + (size_t)(blockIdx.x % kStatGroups) * 64 * 2);
+  __syncthreads();
+  __shared__ float red[256][4];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) red[tid][j] = dwa[k][j];
+    __syncthreads();
+    if (tid < 16) {
+      float t[4] = {0, 0, 0, 0};
+      for (int rr = tid; rr < 256; rr += 16)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] += red[rr][j];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) atomicAdd(acc_out + k * 64 + tid * 4 + j, (double)t[j]);
+    }
+    __syncthreads();
+    red[tid][0] = (sub == 0) ? dba[k] : 0.f;
+    __syncthreads();
+    if (tid == 0) {
+      float t = 0.f;
+      for (int rr = 0; rr < 256; rr += 16) t += red[rr][0];
+      atomicAdd(acc_out + K * 64 + k, (double)t);
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void k_d2f(const double* __restrict__ a, int n, float* __restrict__ o) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) o[i] = (float)a[i];
+}
+
+hipError_t launch_head_fwd(const Src& s, int n, int h, int w, int c, const float* wt, const float* bias, int k,
+                           float* logits, hipStream_t st) {
+  if (c != 64) return hipErrorInvalidValue;
+  const long long pixels = (long long)n * h * w;
+  dim3 grid(grid_cap(pixels, 16 * 4, 8192));
+  switch (k) {
+    case 1: hipLaunchKernelGGL(k_head_fwd<1>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits); break;
+    case 2: hipLaunchKernelGGL(k_head_fwd<2>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits); break;
+    case 3: hipLaunchKernelGGL(k_head_fwd<3>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits); break;
+    case 4: hipLaunchKernelGGL(k_head_fwd<4>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, int c, const float* wt, int k,
+                           const float* yraw, const float* mean, const float* invstd, float* dz, double* bstats,
+                           float* dw, float* db, double* acc, hipStream_t st) {
+  (void)yraw;
+  if (c != 64) return hipErrorInvalidValue;
+  const long long pixels = (long long)n * h * w;
+  dim3 grid(grid_cap(pixels, 16 * 8, 2048));
+  hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
+  switch (k) {
+    case 1: hipLaunchKernelGGL(k_head_bwd<1>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
+    case 2: hipLaunchKernelGGL(k_head_bwd<2>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
+    case 3: hipLaunchKernelGGL(k_head_bwd<3>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
+    case 4: hipLaunchKernelGGL(k_head_bwd<4>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
+    default: return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(k_d2f, dim3(cdiv(k * 64, 256)), dim3(256), 0, st, acc, k * 64, dw);
+  hipLaunchKernelGGL(k_d2f, dim3(1), dim3(64), 0, st, acc + k * 64, k, db);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// WeightedCrossEntropyLoss (utils/losses.py:29-57), forward and backward fused:
+// loss = mean(w * (logsumexp(l) - l[t]));  dl = w*(softmax - onehot)/count.
+// targets/weights through element strides (the caller's cropped views).
+// ---------------------------------------------------------------------------
+template <int K>
+__global__ __launch_bounds__(256) void k_wce(const float* __restrict__ lg, const int64_t* __restrict__ t,
+                                             const float* __restrict__ wm, int n, int h, int w, int64_t ts0,
+                                             int64_t ts1, int64_t ts2, int64_t ws0, int64_t ws1, int64_t ws2,
+                                             float* __restrict__ dl, float gscale, double* __restrict__ acc) {
+  const long long hw = (long long)h * w, total = (long long)n * hw;
+  const double inv = 1.0 / (double)total;
+  float local = 0.f;
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < total;
+       p += (long long)gridDim.x * blockDim.x) {
+    const int nn = (int)(p / hw);
+    const long long r = p - nn * hw;
+    const int yy = (int)(r / w), xx = (int)(r % w);
+    float l[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) l[k] = lg[((size_t)nn * K + k) * hw + r];
+    const int64_t tg = t[nn * ts0 + yy * ts1 + xx * ts2];
+    const float wt = wm[nn * ws0 + yy * ws1 + xx * ws2];
+    float mx = l[0];
+#pragma unroll
+    for (int k = 1; k < K; ++k) mx = fmaxf(mx, l[k]);
+    float se = 0.f, e[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) { e[k] = __expf(l[k] - mx); se += e[k]; }
+    const float lse = mx + __logf(se);
+    const bool valid = (tg >= 0 && tg < K);   // ignore_index (-100) -> 0 loss, 0 grad
+    float lt = 0.f;
+#pragma unroll
+    for (int k = 0; k < K; ++k)
+      if (k == tg) lt = l[k];
+    if (valid) local += wt * (lse - lt);
+    const float sc = valid ? (float)((double)wt * inv) * gscale : 0.f;
+    const float rs = 1.f / se;
+#pragma unroll
+    for (int k = 0; k < K; ++k) dl[((size_t)nn * K + k) * hw + r] = sc * (e[k] * rs - (k == tg ? 1.f : 0.f));
+  }
+  for (int o = 32; o >= 1; o >>= 1) local += __shfl_xor(local, o);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(acc, (double)(red[0] + red[1] + red[2] + red[3]));
+}
+
+__global__ void k_wce_final(const double* acc, double count, float* loss) { *loss = (float)(acc[0] / count); }
+
+hipError_t launch_wce(const float* logits, const int64_t* t, const float* wm, int n, int k, int h, int w,
+                      const int64_t* ts, const int64_t* wsd, float* loss, float* dlogits, float gscale, double* acc,
+                      hipStream_t s) {
+  const long long total = (long long)n * h * w;
+  dim3 grid(grid_cap(total, 256 * 4, 2048));
+  hipMemsetAsync(acc, 0, sizeof(double), s);
+  switch (k) {
+    case 1: hipLaunchKernelGGL(k_wce<1>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
+    case 2: hipLaunchKernelGGL(k_wce<2>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
+    case 3: hipLaunchKernelGGL(k_wce<3>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
+    case 4: hipLaunchKernelGGL(k_wce<4>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
+    default: return hipErrorInvalidValue;
+  }
+  hipLaunchKernelGGL(k_wce_final, dim3(1), dim3(1), 0, s, acc, (double)total, loss);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// torch.optim.SGD(momentum, dampening=0, nesterov=False, weight_decay=0) step.
+// ---------------------------------------------------------------------------
+__global__ void k_sgd(float* __restrict__ p, const float* __restrict__ g, float* __restrict__ b, size_t n, float lr,
+                      float mom, float gs, int first) {
+  const size_t n4 = n / 4;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
+    float4 gv = ld4(g + 4 * i), pv = ld4(p + 4 * i), bv;
+    gv.x *= gs; gv.y *= gs; gv.z *= gs; gv.w *= gs;
+    if (first) {
+      bv = gv;
+    } else {
+      bv = ld4(b + 4 * i);
+      bv.x = fmaf(mom, bv.x, gv.x);
+      bv.y = fmaf(mom, bv.y, gv.y);
+      bv.z = fmaf(mom, bv.z, gv.z);
+      bv.w = fmaf(mom, bv.w, gv.w);
+    }
+    pv.x = fmaf(-lr, bv.x, pv.x);
+    pv.y = fmaf(-lr, bv.y, pv.y);
+    pv.z = fmaf(-lr, bv.z, pv.z);
+    pv.w = fmaf(-lr, bv.w, pv.w);
+    st4(b + 4 * i, bv);
+    st4(p + 4 * i, pv);
+  }
+  if (blockIdx.x == 0 && threadIdx.x < (n & 3)) {
+    const size_t i = n4 * 4 + threadIdx.x;
+    const float bv = first ? g[i] * gs : fmaf(mom, b[i], g[i] * gs);
+    b[i] = bv;
+    p[i] = fmaf(-lr, bv, p[i]);
+  }
+}
+
+hipError_t launch_sgd(float* p, const float* g, float* buf, size_t n, float lr, float mom, float gs, int first,
+                      hipStream_t s) {
+  if ((reinterpret_cast<uintptr_t>(p) | reinterpret_cast<uintptr_t>(g) | reinterpret_cast<uintptr_t>(buf)) & 15)
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_sgd, dim3(grid_cap((long long)(n / 4 + 1), 256, 4096)), dim3(256), 0, s, p, g, buf, n, lr, mom,
+                     gs, first);
+  return hipGetLastError();
+}
+
+__global__ void k_scale_dev(float* x, size_t n, const float* g) {
+  const float s = *g;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) x[i] *= s;
+}
+hipError_t launch_scale_by_dev(float* x, size_t n, const float* g, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale_dev, dim3(grid_cap((long long)n, 256, 4096)), dim3(256), 0, s, x, n, g);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Weight repacks (per step; weights change every optimizer step).
+//   conv fwd  B[co][t*Ci+ci]  = W[co][ci][t]
+//   conv dgrad B[ci][t'*Co+co] = W[co][ci][T-1-t']   (flipped, transposed)
+//   convT fwd  B[ab*Co+co][ci] = W[ci][co][ab]
+//   convT dgrad B[ci][ab*Co+co] = W[ci][co][ab]
+// ---------------------------------------------------------------------------
+__global__ void k_permute_last2(const float* __restrict__ in, int A, int B, int C, float* __restrict__ out) {
+  const long long total = (long long)A * B * C;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    // i indexes out[a][c][b]
+    const int b = (int)(i % B);
+    const long long t = i / B;
+    const int c = (int)(t % C);
+    const long long a = t / C;
+    out[i] = in[(a * B + b) * C + c];
+  }
+}
+
+// out[r2(s)][r] = in[r][s] for a [R][S] matrix with S = T*Cb, s = t*Cb + cb,
+// r2 = cb*T + (flip ? T-1-t : t).  32x32 tiles through LDS.
+__global__ void k_transpose_taps(const float* __restrict__ in, int R, int T, int Cb, int flip,
+                                 float* __restrict__ out) {
+  __shared__ float tile[32][33];
+  const int S = T * Cb;
+  const int s0 = blockIdx.x * 32, r0 = blockIdx.y * 32;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 256 threads: 8 rows per pass
+  for (int k = ty; k < 32; k += 8) {
+    const int r = r0 + k, s = s0 + tx;
+    tile[k][tx] = (r < R && s < S) ? in[(size_t)r * S + s] : 0.f;
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int s = s0 + k, r = r0 + tx;
+    if (s < S && r < R) {
+      const int t = s / Cb, cb = s - t * Cb;
+      const int r2 = cb * T + (flip ? T - 1 - t : t);
+      out[(size_t)r2 * R + r] = tile[tx][k];
+    }
+  }
+}
+
+hipError_t launch_permute_last2(const float* in, int A, int B, int C, float* out, hipStream_t s) {
+  const long long total = (long long)A * B * C;
+  hipLaunchKernelGGL(k_permute_last2, dim3(grid_cap(total, 256, 8192)), dim3(256), 0, s, in, A, B, C, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_conv(const float* w, int co, int ci, int kh, int kw, float* wf, float* wd, hipStream_t s) {
+  const int T = kh * kw;
+  hipError_t e = launch_permute_last2(w, co, ci, T, wf, s);  // [co][T][ci]
+  if (e != hipSuccess || !wd) return e;
+  // wf viewed as [co][T*ci]: out row = ci*T + (T-1-t), col = co
+  dim3 grid(cdiv((long long)T * ci, 32), cdiv(co, 32));
+  hipLaunchKernelGGL(k_transpose_taps, grid, dim3(256), 0, s, wf, co, T, ci, 1, wd);
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_convT(const float* w, int ci, int co, float* wf, float* wd, hipStream_t s) {
+  // wd[ci][ab][co] = W[ci][co][ab]
+  hipError_t e = launch_permute_last2(w, ci, co, 4, wd, s);
+  if (e != hipSuccess) return e;
+  // wf[ab*co + c][ci] = wd[ci][ab*co + c]: plain transpose (T=1)
+  dim3 grid(cdiv(4LL * co, 32), cdiv(ci, 32));
+  hipLaunchKernelGGL(k_transpose_taps, grid, dim3(256), 0, s, wd, ci, 1, 4 * co, 0, wf);
+  return hipGetLastError();
+}
+
+__global__ void k_fill(float* p, size_t n, float v) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+hipError_t launch_fill(float* p, size_t n, float v, hipStream_t s) {
+  hipLaunchKernelGGL(k_fill, dim3(grid_cap((long long)n, 256, 1024)), dim3(256), 0, s, p, n, v);
+  return hipGetLastError();
+}
+// out[c] = sum_g st[g][c][0]  (first member of grouped (a, b) pairs)
+__global__ void k_pair_sum(const double* __restrict__ st, int G, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0;
+  for (int g = 0; g < G; ++g) s += st[((size_t)g * C + c) * 2];
+  out[c] = (float)s;
+}
+hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_pair_sum, dim3(cdiv(c, 256)), dim3(256), 0, s, st, g, c, out);
+  return hipGetLastError();
+}
+
+__global__ void k_colsum(const double* __restrict__ g, int G, int C, float* __restrict__ out) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  double s = 0;
+  for (int i = 0; i < G; ++i) s += g[(size_t)i * C + c];
+  out[c] = (float)s;
+}
+hipError_t launch_colsum(const double* groups, int g, int c, float* out, hipStream_t s) {
+  hipLaunchKernelGGL(k_colsum, dim3(cdiv(c, 256)), dim3(256), 0, s, groups, g, c, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// predict.py:85-92 mask and metrics.py:6-37 IoU counts.
+// ---------------------------------------------------------------------------
+__global__ void k_mask(const float* __restrict__ lg, uint8_t* __restrict__ m, int n, long long hw) {
+  const long long total = n * hw;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const long long nn = i / hw, r = i - nn * hw;
+    m[i] = (lg[(nn * 2 + 1) * hw + r] > lg[(nn * 2) * hw + r]) ? 255 : 0;
+  }
+}
+hipError_t launch_mask(const float* logits, uint8_t* mask, int n, int h, int w, hipStream_t s) {
+  hipLaunchKernelGGL(k_mask, dim3(grid_cap((long long)n * h * w, 256, 4096)), dim3(256), 0, s, logits, mask, n,
+                     (long long)h * w);
+  return hipGetLastError();
+}
+__global__ void k_iou(const uint8_t* __restrict__ a, const uint8_t* __restrict__ b, size_t n,
+                      unsigned long long* out) {
+  unsigned long long inter = 0, uni = 0;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const bool p = a[i] > 0, g = b[i] > 0;
+    inter += (p && g);
+    uni += (p || g);
+  }
+  for (int o = 32; o >= 1; o >>= 1) {
+    inter += __shfl_xor(inter, o);
+    uni += __shfl_xor(uni, o);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(out, inter);
+    atomicAdd(out + 1, uni);
+  }
+}
+hipError_t launch_iou(const uint8_t* a, const uint8_t* b, size_t n, unsigned long long* out, hipStream_t s) {
+  hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), s);
+  hipLaunchKernelGGL(k_iou, dim3(grid_cap((long long)n, 256, 1024)), dim3(256), 0, s, a, b, n, out);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Generic per-channel helpers for the per-op BatchNorm API.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_channel_stats(const float* __restrict__ x, long long pixels, int C,
+                                                       double* __restrict__ st) {
+  const int C4 = C / 4, tid = threadIdx.x, cg = tid % C4, ppb = 256 / C4;
+  float sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+  for (long long p = (long long)blockIdx.x * ppb + tid / C4; p < pixels; p += (long long)gridDim.x * ppb) {
+    const float4 v = ld4(x + p * C + cg * 4);
+    sa[0] += v.x; sa[1] += v.y; sa[2] += v.z; sa[3] += v.w;
+    sb[0] += v.x * v.x; sb[1] += v.y * v.y; sb[2] += v.z * v.z; sb[3] += v.w * v.w;
+  }
+  reduce_pairs_to_global(sa, sb, C4, C, st + (size_t)(blockIdx.x % kStatGroups) * C * 2);
+}
+__global__ __launch_bounds__(256) void k_bn_bwd_stats(const float* __restrict__ dy, const float* __restrict__ x,
+                                                      const float* mean, const float* invstd, long long pixels,
+                                                      int C, double* __restrict__ st) {
+  const int C4 = C / 4, tid = threadIdx.x, cg = tid % C4, ppb = 256 / C4;
+  const float4 mu = ld4(mean + cg * 4), is = ld4(invstd + cg * 4);
+  float sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+  for (long long p = (long long)blockIdx.x * ppb + tid / C4; p < pixels; p += (long long)gridDim.x * ppb) {
+    const float4 d = ld4(dy + p * C + cg * 4), v = ld4(x + p * C + cg * 4);
+    sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
+    sb[0] += d.x * (v.x - mu.x) * is.x;
+    sb[1] += d.y * (v.y - mu.y) * is.y;
+    sb[2] += d.z * (v.z - mu.z) * is.z;
+    sb[3] += d.w * (v.w - mu.w) * is.w;
+  }
+  reduce_pairs_to_global(sa, sb, C4, C, st + (size_t)(blockIdx.x % kStatGroups) * C * 2);
+}
+__global__ void k_affine_relu(const float* __restrict__ x, long long total4, int C, const float* sc, const float* sh,
+                              int relu, float* __restrict__ y) {
+  const int C4 = C / 4;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total4;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % C4) * 4;
+    float4 v = ld4(x + i * 4);
+    const float4 a = ld4(sc + c), b = ld4(sh + c);
+    v.x = fmaf(v.x, a.x, b.x); v.y = fmaf(v.y, a.y, b.y); v.z = fmaf(v.z, a.z, b.z); v.w = fmaf(v.w, a.w, b.w);
+    if (relu) { v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f); }
+    st4(y + i * 4, v);
+  }
+}
+
+hipError_t launch_channel_stats(const float* x, size_t pixels, int c, double* stats, hipStream_t s) {
+  if (c % 4 || 256 % (c / 4)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_channel_stats, dim3(grid_cap((long long)pixels, 256 / (c / 4) * 4, 2048)), dim3(256), 0, s, x,
+                     (long long)pixels, c, stats);
+  return hipGetLastError();
+}
+hipError_t launch_bn_bwd_stats(const float* dy, const float* x, const float* mean, const float* invstd, size_t pixels,
+                               int c, double* bstats, hipStream_t s) {
+  if (c % 4 || 256 % (c / 4)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(k_bn_bwd_stats, dim3(grid_cap((long long)pixels, 256 / (c / 4) * 4, 2048)), dim3(256), 0, s, dy,
+                     x, mean, invstd, (long long)pixels, c, bstats);
+  return hipGetLastError();
+}
+hipError_t launch_affine_relu(const float* x, size_t pixels, int c, const float* scale, const float* shift, int relu,
+                              float* y, hipStream_t s) {
+  if (c % 4) return hipErrorInvalidValue;
+  const long long t4 = (long long)pixels * (c / 4);
+  hipLaunchKernelGGL(k_affine_relu, dim3(grid_cap(t4, 256, 8192)), dim3(256), 0, s, x, t4, c, scale, shift, relu, y);
+  return hipGetLastError();
+}
+
+}  // namespace unet

@@ -1,0 +1,415 @@
+// Implicit-GEMM convolution kernels for gfx950 (MI355X), fp32 in / fp32 accumulate
+// on the matrix cores (v_mfma_f32_32x32x2_f32: exact f32 fma chain, 64 FLOP/clk/SIMD).
+//
+// One kernel family serves every dense op of the U-Net hot path
+// (models/unet_model.py): 3x3 valid conv forward (nn.Conv2d, :11/:15), its input
+// gradient (full correlation with the flipped kernel over a zero-padded dY), the
+// ConvTranspose2d k2s2 forward (:45, a GEMM + pixel-shuffle store) and its input
+// gradient (a 4-tap stride-2 gather).  The weight gradient of all of them is the
+// second kernel (k_wgrad): a pixel-reduction GEMM split over workgroups.
+//
+// Operand staging: A rows are pixels gathered from NHWC tensors (16 channels =
+// 64 contiguous bytes per row per K-step), with the consumer-side BatchNorm+ReLU
+// transform and the skip/upsample channel concat folded into the gather.
+// LDS tiles are [rows][16+4] floats (80-B row stride: ds_read_b128 conflict-free),
+// double buffered, register-prefetched one K-step ahead (one barrier per step).
+#include "unet_internal.h"
+
+namespace unet {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ float4 affine_relu4(float4 v, const float* sc, const float* sh, int c) {
+  float4 a = ld4(sc + c), b = ld4(sh + c);
+  v.x = fmaxf(fmaf(v.x, a.x, b.x), 0.f);
+  v.y = fmaxf(fmaf(v.y, a.y, b.y), 0.f);
+  v.z = fmaxf(fmaf(v.z, a.z, b.z), 0.f);
+  v.w = fmaxf(fmaf(v.w, a.w, b.w), 0.f);
+  return v;
+}
+
+__device__ __forceinline__ float comp(const float4& a, const float4& b, int s) {
+  switch (s) {
+    case 0: return a.x; case 1: return a.y; case 2: return a.z; case 3: return a.w;
+    case 4: return b.x; case 5: return b.y; case 6: return b.z; default: return b.w;
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_igemm: C[m][n] = sum_k A[m][k] * B[n][k];  A gathered, B packed [N][K].
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
+  constexpr int BK = 16, LDK = BK + 4;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  constexpr int AV = BM / 64, BV = BN / 64;   // float4 loads per thread per K-step
+  static_assert(WM * WN == 4, "4 waves");
+  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const Gather& g = args.a;
+  const int M = args.M, K = args.K;
+  const int col4 = tid & 3;
+
+  // Per staged A row: pixel base in each source grid (before the tap offset).
+  int rb0[AV], rb1[AV];
+  const int HWg = g.Hg * g.Wg;
+#pragma unroll
+  for (int q = 0; q < AV; ++q) {
+    int m = m0 + (tid >> 2) + 64 * q;
+    m = m < M ? m : M - 1;
+    int n = m / HWg, r = m - n * HWg;
+    int y = r / g.Wg, x = r - y * g.Wg;
+    y *= g.stride; x *= g.stride;
+    rb0[q] = (n * g.s[0].H + y + g.s[0].oy) * g.s[0].W + x + g.s[0].ox;
+    rb1[q] = (n * g.s[1].H + y + g.s[1].oy) * g.s[1].W + x + g.s[1].ox;
+  }
+  const float* bptr[BV];
+#pragma unroll
+  for (int q = 0; q < BV; ++q) bptr[q] = args.b + (size_t)(n0 + (tid >> 2) + 64 * q) * K + col4 * 4;
+
+  float4 ra[AV], rb[BV];
+  auto load_regs = [&](int k0) {
+    const int tap = k0 / g.Cg;
+    const int c0 = k0 - tap * g.Cg;
+    const int ty = tap / g.taps_w, tx = tap - ty * g.taps_w;
+    const bool second = c0 >= g.c_split;
+    const Src& s = second ? g.s[1] : g.s[0];
+    const int c = (second ? c0 - g.c_split : c0) + col4 * 4;
+    const int toff = ty * s.W + tx;
+#pragma unroll
+    for (int q = 0; q < AV; ++q) {
+      const int pix = (second ? rb1[q] : rb0[q]) + toff;
+      ra[q] = ld4(s.ptr + (size_t)pix * s.C + c);
+    }
+    if (s.scale) {
+#pragma unroll
+      for (int q = 0; q < AV; ++q) ra[q] = affine_relu4(ra[q], s.scale, s.shift, c);
+    }
+#pragma unroll
+    for (int q = 0; q < BV; ++q) rb[q] = ld4(bptr[q] + k0);
+  };
+  auto store_lds = [&](int buf) {
+    float* As = lds + buf * (BM + BN) * LDK;
+    float* Bs = As + BM * LDK;
+#pragma unroll
+    for (int q = 0; q < AV; ++q) st4(As + ((tid >> 2) + 64 * q) * LDK + col4 * 4, ra[q]);
+#pragma unroll
+    for (int q = 0; q < BV; ++q) st4(Bs + ((tid >> 2) + 64 * q) * LDK + col4 * 4, rb[q]);
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int h = lane >> 5, li = lane & 31;
+  const int nk = K / BK;
+  load_regs(0);
+  store_lds(0);
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    if (kc + 1 < nk) load_regs((kc + 1) * BK);
+    const float* As = lds + cur * (BM + BN) * LDK;
+    const float* Bs = As + BM * LDK;
+    float4 a0[TM], a1[TM], b0[TN], b1[TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* p = As + (wm * TM * 32 + i * 32 + li) * LDK + h * 8;
+      a0[i] = ld4(p);
+      a1[i] = ld4(p + 4);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* p = Bs + (wn * TN * 32 + j * 32 + li) * LDK + h * 8;
+      b0[j] = ld4(p);
+      b1[j] = ld4(p + 4);
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(a0[i], a1[i], s), comp(b0[j], b1[j], s),
+                                                           acc[i][j], 0, 0, 0);
+    if (kc + 1 < nk) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ------------------------------ epilogue ---------------------------------
+  const Epilogue& e = args.e;
+  const int N = args.N;
+  // column statistics accumulated per lane (one column per lane per tile j)
+  float s1[TN], s2[TN], t1[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; t1[j] = 0.f; }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * TN * 32 + j * 32 + li;
+    const float bias = e.bias ? e.bias[e.shuffle_co ? col % e.shuffle_co : col] : 0.f;
+    const bool second = col >= e.n_split;
+    const Dst& d = second ? e.d[1] : e.d[0];
+    const int dcol = second ? col - e.n_split : col;
+    float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
+    const bool bwd_mask = (e.yref != nullptr) && !second;
+    if (bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int m = m0 + row;
+        if (m >= M) continue;
+        float v = acc[i][j][r] + bias;
+        size_t idx;
+        if (e.shuffle_co) {
+          const int ab = dcol / e.shuffle_co, co = dcol - ab * e.shuffle_co;
+          const int n = m / HWg, rr = m - n * HWg;
+          const int y = rr / g.Wg, x = rr - y * g.Wg;
+          idx = ((size_t)(n * d.H + 2 * y + (ab >> 1) + d.oy) * d.W + 2 * x + (ab & 1) + d.ox) * d.C + co;
+        } else if (d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg) {
+          idx = (size_t)m * d.C + dcol;
+        } else {
+          const int n = m / HWg, rr = m - n * HWg;
+          const int y = rr / g.Wg, x = rr - y * g.Wg;
+          idx = ((size_t)(n * d.H + y + d.oy) * d.W + x + d.ox) * d.C + dcol;
+        }
+        if (bwd_mask) {
+          const float yv = e.yref[idx];
+          v = (fmaf(yv, bsc, bsh) > 0.f) ? v : 0.f;
+          s1[j] += v;
+          s2[j] += v * ((yv - bmu) * bis);
+        } else if (e.stats) {
+          s1[j] += v;
+          s2[j] += v * v;
+        } else if (second && e.colsum1) {
+          t1[j] += v;
+        }
+        d.ptr[idx] = v;
+      }
+    }
+  }
+  const bool want_stats = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
+  if (!want_stats) return;
+  // reduce lanes l and l+32 (same column), then the WM waves sharing columns
+  __shared__ float red[4][3][BN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    s1[j] += __shfl_xor(s1[j], 32);
+    s2[j] += __shfl_xor(s2[j], 32);
+    t1[j] += __shfl_xor(t1[j], 32);
+  }
+  __syncthreads();
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int lc = wn * TN * 32 + j * 32 + li;
+      red[wm][0][lc] = s1[j];
+      red[wm][1][lc] = s2[j];
+      red[wm][2][lc] = t1[j];
+    }
+  }
+  __syncthreads();
+  const int grp = blockIdx.x % kStatGroups;
+  const int nsplit = min(e.n_split, N);
+  for (int lc = tid; lc < BN; lc += 256) {
+    float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) { a += red[w][0][lc]; b += red[w][1][lc]; c += red[w][2][lc]; }
+    const int col = n0 + lc;
+    if (col < nsplit) {
+      double* st = e.yref ? e.bstats : e.stats;
+      if (st) {
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b);
+      }
+    } else if (e.colsum1) {
+      const int n2 = N - nsplit;
+      atomicAdd(e.colsum1 + (size_t)grp * n2 + (col - nsplit), (double)c);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_wgrad: C[i][j] = sum_p A_p[i] * B_p[j], p = pixels (split over blockIdx.z).
+// LDS tiles are [16 pixels][BM] and [16 pixels][BN] (channel contiguous).
+// ---------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
+  constexpr int BK = 16;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  constexpr int AR = BM / 4, BR = BN / 4;            // float4 per staged pixel row
+  constexpr int AP = BK * AR / 256, BP = BK * BR / 256;  // rows per thread
+  static_assert(AP >= 1 && BP >= 1, "tile too small");
+  __shared__ __attribute__((aligned(16))) float lds[2 * BK * (BM + BN)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int i0 = blockIdx.x * BM, j0 = blockIdx.y * BN;
+  const int pbeg = blockIdx.z * args.pix_per_split;
+  const int pend = min(args.P, pbeg + args.pix_per_split);
+  const Gather& ga = args.ga;
+  const Gather& gb = args.gb;
+  const int HWg = ga.Hg * ga.Wg;
+
+  // A: fixed channel slice of the (single) source of ga.
+  const int acol4 = tid % AR;
+  const int arow = tid / AR;                  // + (256/AR)*q
+  const int ac = i0 + acol4 * 4;
+  // B: fixed (tap, channel) per thread.
+  const int bcol4 = tid % BR;
+  const int brow = tid / BR;
+  const int bj = j0 + bcol4 * 4;
+  const int btap = bj / gb.Cg;
+  const int bc0 = bj - btap * gb.Cg;
+  const bool bsecond = bc0 >= gb.c_split;
+  const Src& bs = bsecond ? gb.s[1] : gb.s[0];
+  const int bc = bsecond ? bc0 - gb.c_split : bc0;
+  const int bty = btap / gb.taps_w, btx = btap - bty * gb.taps_w;
+  const Src& as = ga.s[0];
+
+  float4 ra[AP], rb[BP];
+  auto load_regs = [&](int p0) {
+#pragma unroll
+    for (int q = 0; q < AP; ++q) {
+      const int p = p0 + arow + (256 / AR) * q;
+      if (p < pend) {
+        const int n = p / HWg, r = p - n * HWg;
+        const int y = r / ga.Wg, x = r - y * ga.Wg;
+        const int pix = (n * as.H + y * ga.stride + as.oy) * as.W + x * ga.stride + as.ox;
+        float4 v = ld4(as.ptr + (size_t)pix * as.C + ac);
+        if (as.scale) v = affine_relu4(v, as.scale, as.shift, ac);
+        ra[q] = v;
+      } else {
+        ra[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < BP; ++q) {
+      const int p = p0 + brow + (256 / BR) * q;
+      if (p < pend) {
+        const int n = p / HWg, r = p - n * HWg;
+        const int y = r / gb.Wg, x = r - y * gb.Wg;
+        const int pix = (n * bs.H + y * gb.stride + bty + bs.oy) * bs.W + x * gb.stride + btx + bs.ox;
+        float4 v = ld4(bs.ptr + (size_t)pix * bs.C + bc);
+        if (bs.scale) v = affine_relu4(v, bs.scale, bs.shift, bc);
+        rb[q] = v;
+      } else {
+        rb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+    }
+  };
+  auto store_lds = [&](int buf) {
+    float* As = lds + buf * BK * (BM + BN);
+    float* Bs = As + BK * BM;
+#pragma unroll
+    for (int q = 0; q < AP; ++q) st4(As + (arow + (256 / AR) * q) * BM + acol4 * 4, ra[q]);
+#pragma unroll
+    for (int q = 0; q < BP; ++q) st4(Bs + (brow + (256 / BR) * q) * BN + bcol4 * 4, rb[q]);
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int h = lane >> 5, li = lane & 31;
+  const int nk = (pend - pbeg + BK - 1) / BK;
+  if (nk > 0) {
+    load_regs(pbeg);
+    store_lds(0);
+  }
+  __syncthreads();
+  for (int kc = 0; kc < nk; ++kc) {
+    const int cur = kc & 1;
+    if (kc + 1 < nk) load_regs(pbeg + (kc + 1) * BK);
+    const float* As = lds + cur * BK * (BM + BN);
+    const float* Bs = As + BK * BM;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) {
+      float a[TM], b[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) a[i] = As[(h * 8 + s) * BM + wm * TM * 32 + i * 32 + li];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) b[j] = Bs[(h * 8 + s) * BN + wn * TN * 32 + j * 32 + li];
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    if (kc + 1 < nk) store_lds(cur ^ 1);
+    __syncthreads();
+  }
+  if (nk == 0) return;
+  // accumulate the tile into out (fp32 atomics; output is small vs the reduction)
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = i0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = j0 + wn * TN * 32 + j * 32 + li;
+        atomicAdd(args.out + (size_t)row * args.No + col, acc[i][j][r]);
+      }
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
+hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s) {
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.K % 16) != 0 || (a.a.Cg % 16) != 0 ||
+      (a.a.c_split % 16) != 0)
+    return hipErrorInvalidValue;
+  if (a.N % 128 == 0) {
+    dim3 grid((a.M + 127) / 128, a.N / 128);
+    hipLaunchKernelGGL((k_igemm<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
+  } else if (a.N % 64 == 0) {
+    dim3 grid((a.M + 255) / 256, a.N / 64);
+    hipLaunchKernelGGL((k_igemm<256, 64, 4, 1>), grid, dim3(256), 0, s, a);
+  } else {
+    return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_wgrad(const WgradArgs& a0, hipStream_t s) {
+  WgradArgs a = a0;
+  if (a.Mo % 64 != 0 || a.No % 64 != 0 || a.P <= 0) return hipErrorInvalidValue;
+  if (a.gb.Cg % 64 != 0 || a.gb.c_split % 4 != 0) return hipErrorInvalidValue;
+  const bool big = (a.Mo % 128 == 0) && (a.No % 128 == 0) && (a.gb.Cg % 128 == 0);
+  const int bm = big ? 128 : 64, bn = big ? 128 : 64;
+  const int tiles = (a.Mo / bm) * (a.No / bn);
+  // split the pixel reduction so that the grid has ~2048 workgroups
+  int splits = (2048 + tiles - 1) / tiles;
+  int max_splits = (a.P + 255) / 256;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  int pps = (a.P + splits - 1) / splits;
+  pps = (pps + 15) / 16 * 16;
+  splits = (a.P + pps - 1) / pps;
+  a.pix_per_split = pps;
+  dim3 grid(a.Mo / bm, a.No / bn, splits);
+  if (big)
+    hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((k_wgrad<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+}  // namespace unet

@@ -1,0 +1,320 @@
+// Per-op C-ABI entry points (include/unet_hip.h): single reference ops on
+// caller buffers, built from the same kernels the network plan schedules.
+// They exist for op-level parity tests and for callers that compose their own
+// graph; the training path uses unet_plan_*.
+#include <cerrno>
+#include <string>
+
+#include "../../include/unet_hip.h"
+#include "unet_internal.h"
+
+using namespace unet;
+
+namespace unet {
+hipError_t launch_fill(float* p, size_t n, float v, hipStream_t s);
+hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream_t s);
+}  // namespace unet
+
+namespace {
+thread_local std::string g_op_err;
+inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+}  // namespace
+
+#define OPCK(x)                                                           \
+  do {                                                                    \
+    hipError_t e_ = (x);                                                  \
+    if (e_ != hipSuccess) return e_ == hipErrorInvalidValue ? -EINVAL : -EIO; \
+  } while (0)
+
+extern "C" {
+
+size_t unet_conv_ws_bytes(int n, int h, int w, int ci, int co) {
+  const size_t wb = al256(sizeof(float) * 9 * (size_t)ci * co);
+  const size_t pad = al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co);  // (h-2+4)
+  const size_t misc = al256(sizeof(float) * 4 * co) + al256(sizeof(double) * kStatGroups * 2 * co);
+  return 2 * wb + pad + misc;
+}
+
+int unet_conv3x3_fwd(const float* x, int n, int h, int w, int ci, const float* wt, const float* bias, int co,
+                     const float* xs, const float* xb, float* y, void* ws, unet_stream_t st) {
+  if (ci % 16 || co % 64 || h < 3 || w < 3) return -EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  float* wf = reinterpret_cast<float*>(ws);
+  OPCK(launch_pack_conv(wt, co, ci, 3, 3, wf, nullptr, s));
+  IgemmArgs a;
+  Src x0;
+  x0.ptr = x;
+  x0.H = h;
+  x0.W = w;
+  x0.C = ci;
+  x0.scale = xs;
+  x0.shift = xb;
+  a.a.s[0] = a.a.s[1] = x0;
+  a.a.Cg = a.a.c_split = ci;
+  a.a.taps_h = a.a.taps_w = 3;
+  a.a.Hg = h - 2;
+  a.a.Wg = w - 2;
+  a.a.nimg = n;
+  a.b = wf;
+  a.M = n * (h - 2) * (w - 2);
+  a.N = co;
+  a.K = 9 * ci;
+  a.e.bias = bias;
+  a.e.d[0] = Dst{y, h - 2, w - 2, co, 0, 0};
+  OPCK(launch_igemm(a, s));
+  return 0;
+}
+
+int unet_conv3x3_dgrad(const float* dy, int n, int h, int w, int ci, const float* wt, int co, float* dx, void* ws,
+                       unet_stream_t st) {
+  if (ci % 64 || co % 16 || h < 3 || w < 3) return -EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  const size_t wb = al256(sizeof(float) * 9 * (size_t)ci * co);
+  float* wf = reinterpret_cast<float*>(p);
+  float* wd = reinterpret_cast<float*>(p + wb);
+  float* dyp = reinterpret_cast<float*>(p + 2 * wb);
+  float* coef = reinterpret_cast<float*>(p + 2 * wb + al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co));
+  OPCK(launch_pack_conv(wt, co, ci, 3, 3, wf, wd, s));
+  // zero-bordered copy of dy: dYpad = 1*dy + 0*(y-0) + 0
+  OPCK(launch_fill(coef, co, 1.f, s));
+  OPCK(launch_fill(coef + co, 3 * (size_t)co, 0.f, s));
+  OPCK(launch_bnb_apply(dy, dy, coef, n, h - 2, w - 2, co, dyp, 2, s));
+  IgemmArgs a;
+  Src d;
+  d.ptr = dyp;
+  d.H = h + 2;
+  d.W = w + 2;
+  d.C = co;
+  a.a.s[0] = a.a.s[1] = d;
+  a.a.Cg = a.a.c_split = co;
+  a.a.taps_h = a.a.taps_w = 3;
+  a.a.Hg = h;
+  a.a.Wg = w;
+  a.a.nimg = n;
+  a.b = wd;
+  a.M = n * h * w;
+  a.N = ci;
+  a.K = 9 * co;
+  a.e.d[0] = Dst{dx, h, w, ci, 0, 0};
+  OPCK(launch_igemm(a, s));
+  return 0;
+}
+
+int unet_conv3x3_wgrad(const float* x, const float* dy, int n, int h, int w, int ci, int co, float* dw, float* db,
+                       void* ws, unet_stream_t st) {
+  if (ci % 64 || co % 64 || h < 3 || w < 3) return -EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  const size_t wb = al256(sizeof(float) * 9 * (size_t)ci * co);
+  float* dwp = reinterpret_cast<float*>(p);
+  double* st2 = reinterpret_cast<double*>(p + 2 * wb + al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co) +
+                                          al256(sizeof(float) * 4 * co));
+  OPCK(hipMemsetAsync(dwp, 0, sizeof(float) * 9 * (size_t)ci * co, s));
+  WgradArgs a;
+  Src d;
+  d.ptr = dy;
+  d.H = h - 2;
+  d.W = w - 2;
+  d.C = co;
+  a.ga.s[0] = a.ga.s[1] = d;
+  a.ga.Cg = a.ga.c_split = co;
+  a.ga.Hg = h - 2;
+  a.ga.Wg = w - 2;
+  a.ga.nimg = n;
+  Src xs;
+  xs.ptr = x;
+  xs.H = h;
+  xs.W = w;
+  xs.C = ci;
+  a.gb.s[0] = a.gb.s[1] = xs;
+  a.gb.Cg = a.gb.c_split = ci;
+  a.gb.taps_h = a.gb.taps_w = 3;
+  a.gb.Hg = h - 2;
+  a.gb.Wg = w - 2;
+  a.gb.nimg = n;
+  a.Mo = co;
+  a.No = 9 * ci;
+  a.P = n * (h - 2) * (w - 2);
+  a.out = dwp;
+  OPCK(launch_wgrad(a, s));
+  OPCK(launch_permute_last2(dwp, co, 9, ci, dw, s));
+  if (db) {
+    OPCK(hipMemsetAsync(st2, 0, sizeof(double) * kStatGroups * 2 * co, s));
+    OPCK(launch_channel_stats(dy, (size_t)n * (h - 2) * (w - 2), co, st2, s));
+    OPCK(launch_pair_sum(st2, kStatGroups, co, db, s));
+  }
+  return 0;
+}
+
+int unet_convT2_fwd(const float* x, int n, int h, int w, int ci, const float* wt, const float* bias, int co, float* y,
+                    void* ws, unet_stream_t st) {
+  if (ci % 16 || co % 16) return -EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  float* wf = reinterpret_cast<float*>(p);
+  float* wd = reinterpret_cast<float*>(p + al256(sizeof(float) * 4 * (size_t)ci * co));
+  OPCK(launch_pack_convT(wt, ci, co, wf, wd, s));
+  IgemmArgs a;
+  Src x0;
+  x0.ptr = x;
+  x0.H = h;
+  x0.W = w;
+  x0.C = ci;
+  a.a.s[0] = a.a.s[1] = x0;
+  a.a.Cg = a.a.c_split = ci;
+  a.a.Hg = h;
+  a.a.Wg = w;
+  a.a.nimg = n;
+  a.b = wf;
+  a.M = n * h * w;
+  a.N = 4 * co;
+  a.K = ci;
+  a.e.bias = bias;
+  a.e.shuffle_co = co;
+  a.e.d[0] = Dst{y, 2 * h, 2 * w, co, 0, 0};
+  OPCK(launch_igemm(a, s));
+  return 0;
+}
+
+int unet_convT2_bwd(const float* x, const float* dy, int n, int h, int w, int ci, const float* wt, int co, float* dx,
+                    float* dw, float* db, void* ws, unet_stream_t st) {
+  if (ci % 64 || co % 64) return -EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  const size_t wb = al256(sizeof(float) * 4 * (size_t)ci * co);
+  float* wf = reinterpret_cast<float*>(p);
+  float* wd = reinterpret_cast<float*>(p + wb);
+  float* dwp = reinterpret_cast<float*>(p + 2 * wb);
+  double* st2 = reinterpret_cast<double*>(p + 3 * wb);
+  OPCK(launch_pack_convT(wt, ci, co, wf, wd, s));
+  Src d;
+  d.ptr = dy;
+  d.H = 2 * h;
+  d.W = 2 * w;
+  d.C = co;
+  IgemmArgs a;
+  a.a.s[0] = a.a.s[1] = d;
+  a.a.Cg = a.a.c_split = co;
+  a.a.taps_h = a.a.taps_w = 2;
+  a.a.stride = 2;
+  a.a.Hg = h;
+  a.a.Wg = w;
+  a.a.nimg = n;
+  a.b = wd;
+  a.M = n * h * w;
+  a.N = ci;
+  a.K = 4 * co;
+  a.e.d[0] = Dst{dx, h, w, ci, 0, 0};
+  OPCK(launch_igemm(a, s));
+  OPCK(hipMemsetAsync(dwp, 0, sizeof(float) * 4 * (size_t)ci * co, s));
+  WgradArgs g;
+  Src x0;
+  x0.ptr = x;
+  x0.H = h;
+  x0.W = w;
+  x0.C = ci;
+  g.ga.s[0] = g.ga.s[1] = x0;
+  g.ga.Cg = g.ga.c_split = ci;
+  g.ga.Hg = h;
+  g.ga.Wg = w;
+  g.ga.nimg = n;
+  g.gb.s[0] = g.gb.s[1] = d;
+  g.gb.Cg = g.gb.c_split = co;
+  g.gb.taps_h = g.gb.taps_w = 2;
+  g.gb.stride = 2;
+  g.gb.Hg = h;
+  g.gb.Wg = w;
+  g.gb.nimg = n;
+  g.Mo = ci;
+  g.No = 4 * co;
+  g.P = n * h * w;
+  g.out = dwp;
+  OPCK(launch_wgrad(g, s));
+  OPCK(launch_permute_last2(dwp, ci, 4, co, dw, s));
+  OPCK(hipMemsetAsync(st2, 0, sizeof(double) * kStatGroups * 2 * co, s));
+  OPCK(launch_channel_stats(dy, (size_t)n * 4 * h * w, co, st2, s));
+  OPCK(launch_pair_sum(st2, kStatGroups, co, db, s));
+  return 0;
+}
+
+int unet_maxpool2_fwd(const float* x, int n, int h, int w, int c, float* y, uint8_t* arg, unet_stream_t st) {
+  Src s0;
+  s0.ptr = x;
+  s0.H = h;
+  s0.W = w;
+  s0.C = c;
+  OPCK(launch_maxpool_fwd(s0, n, h, w, y, arg, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_maxpool2_bwd(const float* dy, const uint8_t* arg, int n, int h, int w, int c, float* dx, unet_stream_t st) {
+  OPCK(launch_maxpool_bwd_fused(dy, arg, nullptr, 0, 0, 0, 0, nullptr, nullptr, nullptr, nullptr, nullptr, n, h, w, c,
+                                dx, nullptr, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+size_t unet_bn_ws_bytes(int c) { return al256(sizeof(double) * kStatGroups * 2 * c) + 8 * al256(sizeof(float) * c); }
+
+int unet_bn_train_fwd(const float* x, int n, int h, int w, int c, const float* gamma, const float* beta, float* rm,
+                      float* rv, float* y, float* save_mean, float* save_invstd, void* ws, unet_stream_t st) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  double* stats = reinterpret_cast<double*>(p);
+  float* scale = reinterpret_cast<float*>(p + al256(sizeof(double) * kStatGroups * 2 * c));
+  float* shift = scale + al256(sizeof(float) * c) / 4;
+  const size_t pix = (size_t)n * h * w;
+  OPCK(hipMemsetAsync(stats, 0, sizeof(double) * kStatGroups * 2 * c, s));
+  OPCK(launch_channel_stats(x, pix, c, stats, s));
+  OPCK(launch_bn_finalize(stats, c, (double)pix, gamma, beta, rm, rv, nullptr, save_mean, save_invstd, scale, shift,
+                          0.1f, 1e-5f, s));
+  OPCK(launch_affine_relu(x, pix, c, scale, shift, 0, y, s));
+  return 0;
+}
+
+int unet_bn_train_bwd(const float* x, const float* dy, int n, int h, int w, int c, const float* gamma,
+                      const float* mean, const float* invstd, float* dx, float* dgamma, float* dbeta, void* ws,
+                      unet_stream_t st) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  double* stats = reinterpret_cast<double*>(p);
+  float* coef = reinterpret_cast<float*>(p + al256(sizeof(double) * kStatGroups * 2 * c));
+  const size_t pix = (size_t)n * h * w;
+  OPCK(hipMemsetAsync(stats, 0, sizeof(double) * kStatGroups * 2 * c, s));
+  OPCK(launch_bn_bwd_stats(dy, x, mean, invstd, pix, c, stats, s));
+  OPCK(launch_bnb_finalize(stats, c, (double)pix, gamma, mean, invstd, dgamma, dbeta, nullptr, coef, s));
+  OPCK(launch_bnb_apply(dy, x, coef, n, h, w, c, dx, 0, s));
+  return 0;
+}
+
+int unet_wce_fwd_bwd(const float* logits, const int64_t* t, const float* wm, int n, int k, int h, int w,
+                     const int64_t* ts, const int64_t* wsd, float* loss, float* dl, float gscale, void* ws,
+                     unet_stream_t st) {
+  if (!ts || !wsd || k < 1 || k > 4) return -EINVAL;
+  OPCK(launch_wce(logits, t, wm, n, k, h, w, ts, wsd, loss, dl, gscale, reinterpret_cast<double*>(ws),
+                  reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_scale_by_device_scalar(float* x, size_t n, const float* g, unet_stream_t st) {
+  OPCK(launch_scale_by_dev(x, n, g, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_sgd_momentum(float* p, const float* g, float* buf, size_t n, float lr, float mom, float gscale, int first,
+                      unet_stream_t st) {
+  OPCK(launch_sgd(p, g, buf, n, lr, mom, gscale, first, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_iou_counts(const uint8_t* a, const uint8_t* b, size_t n, unsigned long long* out, unet_stream_t st) {
+  OPCK(launch_iou(a, b, n, out, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int w, unet_stream_t st) {
+  OPCK(launch_mask(logits, mask, n, h, w, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,710 @@
+// Network plan: the U-Net of models/unet_model.py:66-146 (bilinear=False) as a
+// fixed schedule of HIP launches over one caller-provided workspace, plus the
+// C-ABI declared in include/unet_hip.h.
+//
+// Forward (train):  conv outputs are stored RAW (pre-BN); each consumer applies
+// the BatchNorm+ReLU of its producer while loading (scale/shift per channel),
+// so no normalised activation is ever materialised except the 2x2-pooled
+// tensors (pool needs relu(bn(.)) before the max: gamma may be negative).
+// Backward: dz (grad after ReLU mask) -> BN-bwd stats -> dY into a zero-bordered
+// padded buffer -> weight grad (pixel-reduction GEMM) and input grad (implicit
+// GEMM with the flipped kernel) whose epilogue applies the next ReLU mask and
+// collects the next BN-bwd statistics.
+#include <cerrno>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/unet_hip.h"
+#include "unet_internal.h"
+
+using namespace unet;
+
+namespace {
+
+thread_local std::string g_err;
+void set_err(const std::string& s) { g_err = s; }
+
+constexpr float kEps = 1e-5f, kMom = 0.1f;
+
+struct Buf {
+  size_t off = 0, bytes = 0;
+};
+
+struct Alloc {
+  size_t top = 0;
+  Buf take(size_t bytes) {
+    Buf b;
+    b.off = top;
+    b.bytes = bytes;
+    top += (bytes + 255) / 256 * 256;
+    return b;
+  }
+};
+
+struct Conv {
+  int ci = 0, co = 0, hi = 0, wi = 0, ho = 0, wo = 0;
+  int pw = 0, gw = 0;  // param / grad table base (conv w, b, bn w, bn b, rm, rv, nbt)
+  Buf y, mean, invstd, scale, shift, wf, wd, dwp, dz, dyp, coef, stats, bstats;
+};
+struct ConvT {
+  int ci = 0, co = 0, h = 0, w = 0;  // input grid (h, w) -> output (2h, 2w)
+  int pw = 0, gw = 0;
+  Buf u, wf, wd, dwp, du, colsum;
+};
+struct Pool {
+  int c = 0, h = 0, w = 0;  // input grid
+  Buf p, arg, dp;
+};
+struct Skip {
+  int c = 0, th = 0, tw = 0, oy = 0, ox = 0;  // crop of encoder output
+  Buf d;                                      // compact gradient of the cropped region
+};
+
+double conv_flops(const Conv& c, int n) { return 2.0 * n * c.ho * c.wo * (double)c.co * c.ci * 9; }
+
+}  // namespace
+
+struct unet_plan {
+  int n = 0, cin = 0, h = 0, w = 0, ncls = 0, ho = 0, wo = 0;
+  Conv L[18];
+  ConvT T[4];
+  Pool P[4];
+  Skip S[4];
+  Buf stat_region, dwp_region, head_acc, wce_acc, dz_head;
+  size_t ws_bytes = 0;
+  // timing
+  bool timing = false;
+  struct Ev {
+    hipEvent_t a, b;
+    int cls;
+    double flops, bytes;
+  };
+  std::vector<Ev> evs;
+  double t_ms[UNET_KC_COUNT] = {0}, t_fl[UNET_KC_COUNT] = {0}, t_by[UNET_KC_COUNT] = {0};
+  int t_n[UNET_KC_COUNT] = {0};
+};
+
+namespace {
+
+// ---------------- parameter table layout (reference state_dict order) -----
+int block_pbase(int b) { return b <= 4 ? 14 * b : 70 + 16 * (b - 5) + 2; }
+int block_gbase(int b) { return b <= 4 ? 8 * b : 40 + 10 * (b - 5) + 2; }
+
+template <typename T>
+T* P(void* const* tab, int i) { return reinterpret_cast<T*>(tab[i]); }
+
+struct Ctx {
+  unet_plan* p;
+  char* ws;
+  hipStream_t s;
+  float* f(const Buf& b) const { return reinterpret_cast<float*>(ws + b.off); }
+  double* d(const Buf& b) const { return reinterpret_cast<double*>(ws + b.off); }
+  uint8_t* u8(const Buf& b) const { return reinterpret_cast<uint8_t*>(ws + b.off); }
+};
+
+#define CK(x)                                                   \
+  do {                                                          \
+    hipError_t e_ = (x);                                        \
+    if (e_ != hipSuccess) {                                     \
+      set_err(std::string(#x) + ": " + hipGetErrorString(e_));  \
+      return -EIO;                                              \
+    }                                                           \
+  } while (0)
+
+struct Timer {
+  unet_plan* p;
+  hipStream_t s;
+  hipEvent_t a{}, b{};
+  int cls;
+  double fl, by;
+  Timer(unet_plan* p_, hipStream_t s_, int c, double f, double by_) : p(p_), s(s_), cls(c), fl(f), by(by_) {
+    if (p->timing) {
+      hipEventCreate(&a);
+      hipEventCreate(&b);
+      hipEventRecord(a, s);
+    }
+  }
+  ~Timer() {
+    if (p->timing) {
+      hipEventRecord(b, s);
+      p->evs.push_back({a, b, cls, fl, by});
+    }
+  }
+};
+
+Src src_of(const Ctx& c, const Conv& L, bool transform) {
+  Src s;
+  s.ptr = c.f(L.y);
+  s.H = L.ho;
+  s.W = L.wo;
+  s.C = L.co;
+  if (transform) {
+    s.scale = c.f(L.scale);
+    s.shift = c.f(L.shift);
+  }
+  return s;
+}
+
+// Gather describing the input of conv layer l (1..17), as rows over its OUTPUT grid
+// with 3x3 taps (forward A operand and wgrad B operand).
+Gather input_gather(const Ctx& c, int l) {
+  unet_plan* p = c.p;
+  const Conv& L = p->L[l];
+  Gather g;
+  g.taps_h = g.taps_w = 3;
+  g.stride = 1;
+  g.Hg = L.ho;
+  g.Wg = L.wo;
+  g.nimg = p->n;
+  if (l % 2 == 1) {  // second conv of a DoubleConv: input = relu(bn(y[l-1]))
+    g.s[0] = src_of(c, p->L[l - 1], true);
+    g.Cg = g.c_split = L.ci;
+  } else if (l <= 8) {  // first conv of down block: pooled tensor
+    const Pool& pl = p->P[l / 2 - 1];
+    Src s;
+    s.ptr = c.f(pl.p);
+    s.H = pl.h / 2;
+    s.W = pl.w / 2;
+    s.C = pl.c;
+    g.s[0] = s;
+    g.Cg = g.c_split = L.ci;
+  } else {  // first conv of up block: cat([crop(skip), up], 1)
+    const int k = (l - 10) / 2;
+    const Skip& sk = p->S[k];
+    const int enc = 7 - 2 * k;
+    Src a = src_of(c, p->L[enc], true);
+    a.oy = sk.oy;
+    a.ox = sk.ox;
+    Src b;
+    b.ptr = c.f(p->T[k].u);
+    b.H = 2 * p->T[k].h;
+    b.W = 2 * p->T[k].w;
+    b.C = p->T[k].co;
+    g.s[0] = a;
+    g.s[1] = b;
+    g.c_split = sk.c;
+    g.Cg = sk.c + p->T[k].co;
+  }
+  if (g.s[1].ptr == nullptr) g.s[1] = g.s[0];
+  return g;
+}
+
+int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, char* ws, int train, hipStream_t s) {
+  Ctx c{p, ws, s};
+  const int n = p->n;
+  CK(hipMemsetAsync(ws + p->stat_region.off, 0, p->stat_region.bytes, s));
+  // ---- repack weights (per call: the optimizer moves them every step) ----
+  {
+    Timer t(p, s, UNET_KC_ELEMWISE, 0, 0);
+    for (int l = 1; l < 18; ++l) {
+      Conv& L = p->L[l];
+      CK(launch_pack_conv(P<float>(prm, L.pw), L.co, L.ci, 3, 3, c.f(L.wf), train ? c.f(L.wd) : nullptr, s));
+    }
+    for (int k = 0; k < 4; ++k) {
+      ConvT& T = p->T[k];
+      CK(launch_pack_convT(P<float>(prm, T.pw), T.ci, T.co, c.f(T.wf), c.f(T.wd), s));
+    }
+  }
+  if (!train) {
+    for (int l = 0; l < 18; ++l) {
+      Conv& L = p->L[l];
+      CK(launch_bn_eval_prepare(L.co, P<float>(prm, L.pw + 2), P<float>(prm, L.pw + 3), P<float>(prm, L.pw + 4),
+                                P<float>(prm, L.pw + 5), c.f(L.scale), c.f(L.shift), kEps, s));
+    }
+  }
+  auto finalize = [&](int l) -> int {
+    if (!train) return 0;
+    Conv& L = p->L[l];
+    CK(launch_bn_finalize(c.d(L.stats), L.co, (double)n * L.ho * L.wo, P<float>(prm, L.pw + 2),
+                          P<float>(prm, L.pw + 3), P<float>(prm, L.pw + 4), P<float>(prm, L.pw + 5),
+                          P<int64_t>(prm, L.pw + 6), c.f(L.mean), c.f(L.invstd), c.f(L.scale), c.f(L.shift), kMom,
+                          kEps, s));
+    return 0;
+  };
+  // ---- inc.c0 ----
+  {
+    Conv& L = p->L[0];
+    Timer t(p, s, UNET_KC_STAGE1, conv_flops(L, n),
+            4.0 * n * ((double)p->cin * p->h * p->w + (double)L.ho * L.wo * L.co));
+    CK(launch_conv_first_fwd(x, n, p->cin, p->h, p->w, P<float>(prm, L.pw), P<float>(prm, L.pw + 1), L.co,
+                             c.f(L.y), train ? c.d(L.stats) : nullptr, s));
+  }
+  if (int r = finalize(0)) return r;
+  for (int l = 1; l < 18; ++l) {
+    Conv& L = p->L[l];
+    if (l >= 10 && l % 2 == 0) {  // ConvTranspose2d of up block k, input = y[l-1]
+      const int k = (l - 10) / 2;
+      ConvT& T = p->T[k];
+      IgemmArgs a;
+      a.a.s[0] = src_of(c, p->L[l - 1], true);
+      a.a.s[1] = a.a.s[0];
+      a.a.Cg = a.a.c_split = T.ci;
+      a.a.Hg = T.h;
+      a.a.Wg = T.w;
+      a.a.nimg = n;
+      a.b = c.f(T.wf);
+      a.M = n * T.h * T.w;
+      a.N = 4 * T.co;
+      a.K = T.ci;
+      a.e.bias = P<float>(prm, T.pw + 1);  // bias[co], col = ab*Co + co
+      a.e.shuffle_co = T.co;
+      a.e.d[0] = Dst{c.f(T.u), 2 * T.h, 2 * T.w, T.co, 0, 0};
+      Timer t(p, s, UNET_KC_CONV_FWD, 2.0 * a.M * a.N * a.K, 0);
+      CK(launch_igemm(a, s));
+    }
+    IgemmArgs a;
+    a.a = input_gather(c, l);
+    a.b = c.f(L.wf);
+    a.M = n * L.ho * L.wo;
+    a.N = L.co;
+    a.K = 9 * L.ci;
+    a.e.bias = P<float>(prm, L.pw + 1);
+    a.e.d[0] = Dst{c.f(L.y), L.ho, L.wo, L.co, 0, 0};
+    a.e.stats = train ? c.d(L.stats) : nullptr;
+    {
+      Timer t(p, s, UNET_KC_CONV_FWD, conv_flops(L, n), 0);
+      CK(launch_igemm(a, s));
+    }
+    if (int r = finalize(l)) return r;
+    if (l <= 7 && l % 2 == 1) {  // encoder output -> MaxPool2d(2)
+      Pool& pl = p->P[l / 2];
+      Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * pl.h * pl.w * pl.c * 1.25);
+      CK(launch_maxpool_fwd(src_of(c, L, true), n, pl.h, pl.w, c.f(pl.p), c.u8(pl.arg), s));
+    }
+  }
+  {
+    Conv& L = p->L[17];
+    Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * L.ho * L.wo * (L.co + p->ncls));
+    CK(launch_head_fwd(src_of(c, L, true), n, L.ho, L.wo, L.co, P<float>(prm, 134), P<float>(prm, 135), p->ncls,
+                       logits, s));
+  }
+  return 0;
+}
+
+// segment id of each backward step (for DP overlap): 0 = head+up4 ... 3 = up1,
+// 4 = down4 ... 7 = down1, 8 = inc.
+int seg_of_layer(int l) {
+  if (l >= 10) return (17 - l) / 2;  // 17,16 -> 0 ; 11,10 -> 3
+  return 4 + (9 - l) / 2;            // 9,8 -> 4 ; 1,0 -> 8
+}
+
+int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* x, const float* dlogits, char* ws,
+                 int seg_b, int seg_e, hipStream_t s) {
+  Ctx c{p, ws, s};
+  const int n = p->n;
+  auto in_seg = [&](int sg) { return sg >= seg_b && sg < seg_e; };
+  if (seg_b == 0) {
+    // bstats live in the stat region next to the forward stats: clear only them
+    for (int l = 0; l < 18; ++l) CK(hipMemsetAsync(c.d(p->L[l].bstats), 0, p->L[l].bstats.bytes, s));
+    for (int k = 0; k < 4; ++k) CK(hipMemsetAsync(c.d(p->T[k].colsum), 0, sizeof(double) * kStatGroups * p->T[k].co, s));
+    CK(hipMemsetAsync(ws + p->dwp_region.off, 0, p->dwp_region.bytes, s));
+    Conv& L = p->L[17];
+    Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * L.ho * L.wo * (2 * L.co + p->ncls));
+    CK(launch_head_bwd(src_of(c, L, true), dlogits, n, L.ho, L.wo, L.co, P<float>(prm, 134), p->ncls, c.f(L.y),
+                       c.f(L.mean), c.f(L.invstd), c.f(L.dz), c.d(L.bstats), P<float>(grd, 80), P<float>(grd, 81),
+                       c.d(p->head_acc), s));
+  }
+  for (int l = 17; l >= 0; --l) {
+    if (!in_seg(seg_of_layer(l))) continue;
+    Conv& L = p->L[l];
+    const double M = (double)n * L.ho * L.wo;
+    CK(launch_bnb_finalize(c.d(L.bstats), L.co, M, P<float>(prm, L.pw + 2), c.f(L.mean), c.f(L.invstd),
+                           P<float>(grd, L.gw + 2), P<float>(grd, L.gw + 3), P<float>(grd, L.gw + 1), c.f(L.coef), s));
+    {
+      Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * ((double)(L.ho + 4) * (L.wo + 4) + 2.0 * L.ho * L.wo) * L.co);
+      CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), n, L.ho, L.wo, L.co, c.f(L.dyp), 2, s));
+    }
+    Src dy;  // dY interior of the padded buffer
+    dy.ptr = c.f(L.dyp);
+    dy.H = L.ho + 4;
+    dy.W = L.wo + 4;
+    dy.C = L.co;
+    dy.oy = dy.ox = 2;
+    if (l == 0) {
+      CK(hipMemsetAsync(P<float>(grd, L.gw), 0, sizeof(float) * L.co * L.ci * 9, s));
+      Timer t(p, s, UNET_KC_STAGE1, 2.0 * M * L.co * L.ci * 9,
+              4.0 * n * ((double)p->cin * p->h * p->w + (double)L.ho * L.wo * L.co));
+      CK(launch_conv_first_wgrad(x, n, p->cin, p->h, p->w, dy, L.co, P<float>(grd, L.gw), s));
+      continue;
+    }
+    // weight gradient
+    {
+      WgradArgs w;
+      w.ga.s[0] = dy;
+      w.ga.s[1] = dy;
+      w.ga.Cg = w.ga.c_split = L.co;
+      w.ga.Hg = L.ho;
+      w.ga.Wg = L.wo;
+      w.ga.nimg = n;
+      w.gb = input_gather(c, l);
+      w.Mo = L.co;
+      w.No = 9 * L.ci;
+      w.P = n * L.ho * L.wo;
+      w.out = c.f(L.dwp);
+      Timer t(p, s, UNET_KC_CONV_WGRAD, conv_flops(L, n), 0);
+      CK(launch_wgrad(w, s));
+    }
+    CK(launch_permute_last2(c.f(L.dwp), L.co, 9, L.ci, P<float>(grd, L.gw), s));
+    // input gradient
+    IgemmArgs a;
+    a.a.s[0] = dy;
+    a.a.s[0].oy = a.a.s[0].ox = 0;  // padded coordinates: rows index the input grid
+    a.a.s[1] = a.a.s[0];
+    a.a.Cg = a.a.c_split = L.co;
+    a.a.taps_h = a.a.taps_w = 3;
+    a.a.Hg = L.hi;
+    a.a.Wg = L.wi;
+    a.a.nimg = n;
+    a.b = c.f(L.wd);
+    a.M = n * L.hi * L.wi;
+    a.N = L.ci;
+    a.K = 9 * L.co;
+    if (l % 2 == 1) {  // -> dz of layer l-1 (masked + BN-bwd stats)
+      Conv& Q = p->L[l - 1];
+      a.e.d[0] = Dst{c.f(Q.dz), Q.ho, Q.wo, Q.co, 0, 0};
+      a.e.yref = c.f(Q.y);
+      a.e.bn_scale = c.f(Q.scale);
+      a.e.bn_shift = c.f(Q.shift);
+      a.e.bn_mean = c.f(Q.mean);
+      a.e.bn_invstd = c.f(Q.invstd);
+      a.e.bstats = c.d(Q.bstats);
+      Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+      CK(launch_igemm(a, s));
+    } else if (l <= 8) {  // -> gradient of the pooled tensor, then pool backward
+      const int k = l / 2 - 1;
+      Pool& pl = p->P[k];
+      a.e.d[0] = Dst{c.f(pl.dp), pl.h / 2, pl.w / 2, pl.c, 0, 0};
+      {
+        Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+        CK(launch_igemm(a, s));
+      }
+      Conv& Q = p->L[l - 1];  // encoder output feeding this pool (and a skip)
+      const Skip& sk = p->S[3 - k];
+      Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * (double)Q.ho * Q.wo * Q.co * 2.6);
+      CK(launch_maxpool_bwd_fused(c.f(pl.dp), c.u8(pl.arg), c.f(sk.d), sk.oy, sk.ox, sk.th, sk.tw, c.f(Q.y),
+                                  c.f(Q.scale), c.f(Q.shift), c.f(Q.mean), c.f(Q.invstd), n, Q.ho, Q.wo, Q.co,
+                                  c.f(Q.dz), c.d(Q.bstats), s));
+    } else {  // first conv of up block: split into skip grad and upsampled grad
+      const int k = (l - 10) / 2;
+      ConvT& T = p->T[k];
+      Skip& sk = p->S[k];
+      a.e.d[0] = Dst{c.f(sk.d), sk.th, sk.tw, sk.c, 0, 0};
+      a.e.d[1] = Dst{c.f(T.du), 2 * T.h, 2 * T.w, T.co, 0, 0};
+      a.e.n_split = sk.c;
+      a.e.colsum1 = c.d(T.colsum);
+      {
+        Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+        CK(launch_igemm(a, s));
+      }
+      CK(launch_colsum(c.d(T.colsum), kStatGroups, T.co, P<float>(grd, T.gw + 1), s));
+      // ConvTranspose2d weight grad: C[ci][ab*Co+co] = sum_p z[p][ci] * du[2p+ab][co]
+      Conv& Q = p->L[l - 1];
+      {
+        WgradArgs w;
+        w.ga.s[0] = src_of(c, Q, true);
+        w.ga.s[1] = w.ga.s[0];
+        w.ga.Cg = w.ga.c_split = T.ci;
+        w.ga.Hg = T.h;
+        w.ga.Wg = T.w;
+        w.ga.nimg = n;
+        Src du;
+        du.ptr = c.f(T.du);
+        du.H = 2 * T.h;
+        du.W = 2 * T.w;
+        du.C = T.co;
+        w.gb.s[0] = du;
+        w.gb.s[1] = du;
+        w.gb.Cg = w.gb.c_split = T.co;
+        w.gb.taps_h = w.gb.taps_w = 2;
+        w.gb.stride = 2;
+        w.gb.Hg = T.h;
+        w.gb.Wg = T.w;
+        w.gb.nimg = n;
+        w.Mo = T.ci;
+        w.No = 4 * T.co;
+        w.P = n * T.h * T.w;
+        w.out = c.f(T.dwp);
+        Timer t(p, s, UNET_KC_CONV_WGRAD, 2.0 * w.P * (double)w.Mo * w.No, 0);
+        CK(launch_wgrad(w, s));
+      }
+      CK(launch_permute_last2(c.f(T.dwp), T.ci, 4, T.co, P<float>(grd, T.gw), s));
+      // ConvTranspose2d input grad -> dz of layer l-1
+      IgemmArgs b;
+      Src du;
+      du.ptr = c.f(T.du);
+      du.H = 2 * T.h;
+      du.W = 2 * T.w;
+      du.C = T.co;
+      b.a.s[0] = du;
+      b.a.s[1] = du;
+      b.a.Cg = b.a.c_split = T.co;
+      b.a.taps_h = b.a.taps_w = 2;
+      b.a.stride = 2;
+      b.a.Hg = T.h;
+      b.a.Wg = T.w;
+      b.a.nimg = n;
+      b.b = c.f(T.wd);
+      b.M = n * T.h * T.w;
+      b.N = T.ci;
+      b.K = 4 * T.co;
+      b.e.d[0] = Dst{c.f(Q.dz), Q.ho, Q.wo, Q.co, 0, 0};
+      b.e.yref = c.f(Q.y);
+      b.e.bn_scale = c.f(Q.scale);
+      b.e.bn_shift = c.f(Q.shift);
+      b.e.bn_mean = c.f(Q.mean);
+      b.e.bn_invstd = c.f(Q.invstd);
+      b.e.bstats = c.d(Q.bstats);
+      Timer t(p, s, UNET_KC_CONV_DGRAD, 2.0 * b.M * (double)b.N * b.K, 0);
+      CK(launch_igemm(b, s));
+    }
+  }
+  return 0;
+}
+
+}  // namespace
+
+// =========================== C-ABI =======================================
+extern "C" {
+
+const char* unet_version(void) { return "unet_hip 0.1 gfx950 fp32-mfma"; }
+const char* unet_last_error(void) { return g_err.c_str(); }
+
+unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
+  if (n < 1 || c_in < 1 || c_in > 4 || n_classes < 1 || n_classes > 4) {
+    set_err("unet_plan_create: need n>=1, 1<=c_in<=4, 1<=n_classes<=4");
+    return nullptr;
+  }
+  auto* p = new unet_plan();
+  p->n = n;
+  p->cin = c_in;
+  p->h = h;
+  p->w = w;
+  p->ncls = n_classes;
+  const int chans[5] = {64, 128, 256, 512, 1024};
+  Alloc al;
+  auto fsz = [&](long long elems) { return (size_t)elems * 4; };
+  // encoder shapes (models/unet_model.py:106-110)
+  int hh = h, ww = w;
+  int cprev = c_in;
+  for (int b = 0; b < 5; ++b) {
+    if (b > 0) {
+      Pool& pl = p->P[b - 1];
+      pl.c = chans[b - 1];
+      pl.h = hh;
+      pl.w = ww;
+      hh /= 2;
+      ww /= 2;
+    }
+    for (int j = 0; j < 2; ++j) {
+      Conv& L = p->L[2 * b + j];
+      L.ci = j == 0 ? cprev : chans[b];
+      L.co = chans[b];
+      L.hi = hh;
+      L.wi = ww;
+      hh -= 2;
+      ww -= 2;
+      L.ho = hh;
+      L.wo = ww;
+      if (L.ho < 1 || L.wo < 1) {
+        set_err("input too small for the valid U-Net");
+        delete p;
+        return nullptr;
+      }
+    }
+    cprev = chans[b];
+  }
+  // decoder (models/unet_model.py:129-143)
+  for (int k = 0; k < 4; ++k) {
+    ConvT& T = p->T[k];
+    const Conv& prev = p->L[9 + 2 * k];
+    T.ci = prev.co;
+    T.co = prev.co / 2;
+    T.h = prev.ho;
+    T.w = prev.wo;
+    const Conv& enc = p->L[7 - 2 * k];
+    Skip& sk = p->S[k];
+    sk.c = enc.co;
+    sk.th = 2 * T.h;
+    sk.tw = 2 * T.w;
+    if (enc.ho < sk.th || enc.wo < sk.tw) {
+      set_err("skip connection smaller than the upsampled map (input size not supported by the valid U-Net)");
+      delete p;
+      return nullptr;
+    }
+    sk.oy = (enc.ho - sk.th) / 2;  // UNet._center_crop, models/unet_model.py:97-100
+    sk.ox = (enc.wo - sk.tw) / 2;
+    int hh2 = sk.th, ww2 = sk.tw;
+    for (int j = 0; j < 2; ++j) {
+      Conv& L = p->L[10 + 2 * k + j];
+      L.ci = j == 0 ? sk.c + T.co : T.co;
+      L.co = T.co;
+      L.hi = hh2;
+      L.wi = ww2;
+      hh2 -= 2;
+      ww2 -= 2;
+      L.ho = hh2;
+      L.wo = ww2;
+      if (L.ho < 1 || L.wo < 1) {
+        set_err("input too small for the valid U-Net");
+        delete p;
+        return nullptr;
+      }
+    }
+  }
+  p->ho = p->L[17].ho;
+  p->wo = p->L[17].wo;
+  // parameter table indices
+  for (int l = 0; l < 18; ++l) {
+    const int b = l / 2, j = l % 2;
+    p->L[l].pw = block_pbase(b) + 7 * j;
+    p->L[l].gw = block_gbase(b) + 4 * j;
+  }
+  for (int k = 0; k < 4; ++k) {
+    p->T[k].pw = 70 + 16 * k;
+    p->T[k].gw = 40 + 10 * k;
+  }
+  // ---- workspace ----
+  // stat region first (zeroed per forward/backward)
+  const size_t stat_start = al.top;
+  for (int l = 0; l < 18; ++l) {
+    Conv& L = p->L[l];
+    L.stats = al.take(sizeof(double) * kStatGroups * L.co * 2);
+    L.bstats = al.take(sizeof(double) * kStatGroups * L.co * 2);
+  }
+  for (int k = 0; k < 4; ++k)  // colsum groups + (tail) expanded bias table
+    p->T[k].colsum = al.take(sizeof(double) * kStatGroups * p->T[k].co);
+  p->head_acc = al.take(sizeof(double) * (64 * 4 + 4));
+  p->wce_acc = al.take(64);
+  p->stat_region.off = stat_start;
+  p->stat_region.bytes = al.top - stat_start;
+  const size_t dwp_start = al.top;
+  for (int l = 1; l < 18; ++l) p->L[l].dwp = al.take(fsz(9LL * p->L[l].co * p->L[l].ci));
+  for (int k = 0; k < 4; ++k) p->T[k].dwp = al.take(fsz(4LL * p->T[k].co * p->T[k].ci));
+  p->dwp_region.off = dwp_start;
+  p->dwp_region.bytes = al.top - dwp_start;
+  for (int l = 0; l < 18; ++l) {
+    Conv& L = p->L[l];
+    const long long pix = (long long)n * L.ho * L.wo;
+    L.y = al.take(fsz(pix * L.co));
+    L.mean = al.take(fsz(L.co));
+    L.invstd = al.take(fsz(L.co));
+    L.scale = al.take(fsz(L.co));
+    L.shift = al.take(fsz(L.co));
+    L.coef = al.take(fsz(4LL * L.co));
+    if (l > 0) {
+      L.wf = al.take(fsz(9LL * L.co * L.ci));
+      L.wd = al.take(fsz(9LL * L.co * L.ci));
+    }
+    L.dz = al.take(fsz(pix * L.co));
+    L.dyp = al.take(fsz((long long)n * (L.ho + 4) * (L.wo + 4) * L.co));
+  }
+  for (int k = 0; k < 4; ++k) {
+    ConvT& T = p->T[k];
+    const long long opix = (long long)n * 4 * T.h * T.w;
+    T.u = al.take(fsz(opix * T.co));
+    T.du = al.take(fsz(opix * T.co));
+    T.wf = al.take(fsz(4LL * T.co * T.ci));
+    T.wd = al.take(fsz(4LL * T.co * T.ci));
+    Skip& sk = p->S[k];
+    sk.d = al.take(fsz((long long)n * sk.th * sk.tw * sk.c));
+  }
+  for (int k = 0; k < 4; ++k) {
+    Pool& pl = p->P[k];
+    const long long pp = (long long)n * (pl.h / 2) * (pl.w / 2) * pl.c;
+    pl.p = al.take(fsz(pp));
+    pl.arg = al.take((size_t)pp);
+    pl.dp = al.take(fsz(pp));
+  }
+  p->ws_bytes = al.top;
+  return p;
+}
+
+void unet_plan_destroy(unet_plan* p) {
+  if (!p) return;
+  for (auto& e : p->evs) {
+    hipEventDestroy(e.a);
+    hipEventDestroy(e.b);
+  }
+  delete p;
+}
+
+int unet_plan_out_hw(const unet_plan* p, int* oh, int* ow) {
+  if (!p) return -EINVAL;
+  if (oh) *oh = p->ho;
+  if (ow) *ow = p->wo;
+  return 0;
+}
+size_t unet_plan_workspace_bytes(const unet_plan* p) { return p ? p->ws_bytes : 0; }
+int unet_plan_num_params(const unet_plan*) { return 136; }
+int unet_plan_num_grads(const unet_plan*) { return 82; }
+int unet_plan_num_segments(const unet_plan*) { return 9; }
+int unet_plan_segment_grads(const unet_plan*, int seg, int* first, int* cnt) {
+  // grad table: inc 0-7, down1..4 8-39, up1..4 40-79, outc 80-81
+  int f, k;
+  if (seg == 0) { f = 70; k = 12; }            // head + up4
+  else if (seg <= 3) { f = 70 - 10 * seg; k = 10; }  // up3, up2, up1
+  else if (seg <= 8) { f = 8 * (8 - seg); k = 8; }   // down4 .. inc
+  else return -EINVAL;
+  if (first) *first = f;
+  if (cnt) *cnt = k;
+  return 0;
+}
+
+int unet_plan_forward(unet_plan* p, void* const* prm, const float* x, float* logits, void* ws, int train,
+                      unet_stream_t stream) {
+  if (!p || !prm || !x || !logits || !ws) {
+    set_err("unet_plan_forward: null argument");
+    return -EINVAL;
+  }
+  if (reinterpret_cast<uintptr_t>(ws) & 255) {
+    set_err("unet_plan_forward: workspace must be 256-byte aligned");
+    return -EINVAL;
+  }
+  return run_forward(p, prm, x, logits, reinterpret_cast<char*>(ws), train, reinterpret_cast<hipStream_t>(stream));
+}
+
+int unet_plan_backward(unet_plan* p, void* const* prm, void* const* grd, const float* x, const float* dlogits,
+                       void* ws, int sb, int se, unet_stream_t stream) {
+  if (!p || !prm || !grd || !x || !dlogits || !ws || sb < 0 || se > 9 || sb >= se) {
+    set_err("unet_plan_backward: bad argument");
+    return -EINVAL;
+  }
+  return run_backward(p, prm, grd, x, dlogits, reinterpret_cast<char*>(ws), sb, se,
+                      reinterpret_cast<hipStream_t>(stream));
+}
+
+int unet_plan_set_timing(unet_plan* p, int enable) {
+  if (!p) return -EINVAL;
+  p->timing = enable != 0;
+  return 0;
+}
+
+int unet_plan_timing(const unet_plan* pc, double* ms, double* fl, double* by, int* cnt) {
+  auto* p = const_cast<unet_plan*>(pc);
+  if (!p) return -EINVAL;
+  for (auto& e : p->evs) {
+    hipEventSynchronize(e.b);
+    float t = 0;
+    hipEventElapsedTime(&t, e.a, e.b);
+    p->t_ms[e.cls] += t;
+    p->t_fl[e.cls] += e.flops;
+    p->t_by[e.cls] += e.bytes;
+    p->t_n[e.cls] += 1;
+    hipEventDestroy(e.a);
+    hipEventDestroy(e.b);
+  }
+  p->evs.clear();
+  for (int i = 0; i < UNET_KC_COUNT; ++i) {
+    if (ms) ms[i] = p->t_ms[i];
+    if (fl) fl[i] = p->t_fl[i];
+    if (by) by[i] = p->t_by[i];
+    if (cnt) cnt[i] = p->t_n[i];
+    p->t_ms[i] = p->t_fl[i] = p->t_by[i] = 0;
+    p->t_n[i] = 0;
+  }
+  return 0;
+}
+
+}  // extern "C"

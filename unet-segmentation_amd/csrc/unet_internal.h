@@ -1,0 +1,155 @@
+// Internal declarations shared by the kernel file and the network plan.
+// Not part of the C-ABI (include/unet_hip.h is).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+
+namespace unet {
+
+// A tensor in NHWC, addressed as an (H, W, C) grid per image with an (oy, ox)
+// origin: element (n, y, x, c) lives at ((n*H + y+oy)*W + x+ox)*C + c.
+// An optional per-channel affine+ReLU (BatchNorm2d train/eval + nn.ReLU,
+// models/unet_model.py:12-17) is applied when the tensor is READ: the network
+// stores raw conv outputs and normalises them on load in the consumer.
+struct Src {
+  const float* ptr = nullptr;
+  int H = 0, W = 0, C = 0;   // grid of the stored tensor
+  int oy = 0, ox = 0;        // origin added to the pixel position (crop / pad)
+  const float* scale = nullptr;  // nullptr: identity
+  const float* shift = nullptr;
+};
+
+// Implicit-GEMM gather of operand rows: row m enumerates pixels of an
+// (Nimg, Hg, Wg) grid; column k enumerates (tap, channel) with
+// tap = (ty, tx) in a taps_h x taps_w window and channel in [0, Cg).
+// Channels < c_split come from s[0], the rest from s[1] (channel - c_split):
+// that is torch.cat([skip_cropped, up], dim=1) (models/unet_model.py:131)
+// without a copy.  Source pixel = (y*stride + ty, x*stride + tx) + origin.
+struct Gather {
+  Src s[2];
+  int c_split = 0;      // == Cg when single source
+  int Cg = 0;           // channels per tap
+  int taps_h = 1, taps_w = 1;
+  int stride = 1;
+  int Hg = 0, Wg = 0;   // pixel grid of the rows
+  int nimg = 0;
+};
+
+// Destination of GEMM outputs (fwd/dgrad epilogue), NHWC grid with origin.
+struct Dst {
+  float* ptr = nullptr;
+  int H = 0, W = 0, C = 0;
+  int oy = 0, ox = 0;
+};
+
+struct Epilogue {
+  const float* bias = nullptr;   // per output column
+  int shuffle_co = 0;            // >0: ConvTranspose2d k2s2 pixel shuffle
+  Dst d[2];
+  int n_split = 1 << 30;         // columns < n_split -> d[0], else d[1]
+  // forward BN statistics of the stored values: stats[g][col][2] (sum, sumsq)
+  double* stats = nullptr;
+  // backward: mask the d[0] values with ReLU'(yref*scale+shift) and collect
+  // bstats[g][col][2] = (sum dz', sum dz' * xhat), xhat = (yref-mean)*invstd
+  const float* yref = nullptr;
+  const float* bn_scale = nullptr;
+  const float* bn_shift = nullptr;
+  const float* bn_mean = nullptr;
+  const float* bn_invstd = nullptr;
+  double* bstats = nullptr;
+  double* colsum1 = nullptr;     // [g][col - n_split] sums of d[1] values
+};
+
+constexpr int kStatGroups = 64;  // fp64 atomic accumulators are spread over groups
+
+struct IgemmArgs {
+  Gather a;          // A rows (M = nimg*Hg*Wg pixels), K = taps*Cg
+  const float* b;    // packed B[N][K] (k contiguous)
+  int M, N, K;
+  Epilogue e;
+};
+
+struct WgradArgs {
+  // C[i][j] = sum_p A_p[i] * B_p[j] over the pixels p of the grid of `ga`.
+  Gather ga;         // taps = 1: row p -> channels i (contiguous)
+  Gather gb;         // row p, column j = (tap, channel)
+  int Mo, No;        // output rows (ga.Cg) and cols (gb taps * gb.Cg)
+  int P;             // pixels
+  int pix_per_split;
+  float* out;        // [Mo][No] fp32, accumulated with atomics (zeroed by caller)
+};
+
+// ---------------- launchers (kernels.hip) ----------------
+hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s);
+hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s);
+
+// inc.c0: Ci in {1,2,3,4} direct conv from an NCHW input; y NHWC (Co = 64 multiple).
+hipError_t launch_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w,
+                                 const float* wt_oihw, const float* bias, int co, float* y,
+                                 double* stats, hipStream_t s);
+hipError_t launch_conv_first_wgrad(const float* x_nchw, int n, int ci, int h, int w,
+                                   const Src& dy, int co, float* dw_oihw, hipStream_t s);
+
+// BN finalize (train): stats[G][C][2] -> mean, invstd, scale, shift; running update.
+hipError_t launch_bn_finalize(const double* stats, int c, double count, const float* gamma,
+                              const float* beta, float* rmean, float* rvar, int64_t* nbt,
+                              float* mean, float* invstd, float* scale, float* shift,
+                              float momentum, float eps, hipStream_t s);
+// BN eval prepare: scale/shift from running stats.
+hipError_t launch_bn_eval_prepare(int c, const float* gamma, const float* beta,
+                                  const float* rmean, const float* rvar, float* scale,
+                                  float* shift, float eps, hipStream_t s);
+// BN backward finalize: bstats -> dgamma, dbeta, conv-bias grad, coefficients
+// k[3][C] for dY = k0*dz' + k1*y + k2.
+hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const float* gamma,
+                               const float* mean, const float* invstd, float* dgamma,
+                               float* dbeta, float* dbias_conv, float* coef, hipStream_t s);
+// dYpad interior = coef0*dz + coef1*y + coef2; border (pad each side) = 0.
+hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h,
+                            int w, int c, float* dypad, int pad, hipStream_t s);
+// MaxPool2d(2) fwd with BN+ReLU transform on load (src grid H x W, pooled H/2 x W/2).
+hipError_t launch_maxpool_fwd(const Src& src, int n, int h, int w, float* y, uint8_t* arg,
+                              hipStream_t s);
+// Maxpool bwd fused: dz = route(dpool) + crop-embedded dskip (may be null), then
+// ReLU mask + BN-bwd stats (if scale != null).  Writes dz' (n,h,w,c).
+hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, const float* dskip,
+                                    int skip_oy, int skip_ox, int skip_h, int skip_w,
+                                    const float* y, const float* scale, const float* shift,
+                                    const float* mean, const float* invstd, int n, int h, int w,
+                                    int c, float* dz, double* bstats, hipStream_t s);
+// 1x1 head (OutConv, models/unet_model.py:56-63) forward: logits NCHW.
+hipError_t launch_head_fwd(const Src& src, int n, int h, int w, int c, const float* wt,
+                           const float* bias, int k, float* logits, hipStream_t s);
+// head backward: dz' (masked, + BN-bwd stats), dW (k x c), db (k) (written, not accumulated).
+hipError_t launch_head_bwd(const Src& src, const float* dlogits, int n, int h, int w, int c,
+                           const float* wt, int k, const float* yraw, const float* mean,
+                           const float* invstd, float* dz, double* bstats, float* dw, float* db,
+                           double* ws_acc, hipStream_t s);
+hipError_t launch_wce(const float* logits, const int64_t* t, const float* wm, int n, int k, int h,
+                      int w, const int64_t* ts, const int64_t* wsd, float* loss, float* dlogits,
+                      float grad_scale, double* acc, hipStream_t s);
+hipError_t launch_sgd(float* p, const float* g, float* buf, size_t n, float lr, float mom,
+                      float gscale, int first, hipStream_t s);
+hipError_t launch_scale_by_dev(float* x, size_t n, const float* g, hipStream_t s);
+// weight repacks
+hipError_t launch_pack_conv(const float* w_oihw, int co, int ci, int kh, int kw, float* wf,
+                            float* wd, hipStream_t s);
+hipError_t launch_pack_convT(const float* w, int ci, int co, float* wf, float* wd, hipStream_t s);
+// out[a][c][b] = in[a][b][c]
+hipError_t launch_permute_last2(const float* in, int A, int B, int C, float* out, hipStream_t s);
+// column sums over rows: out[c] = sum_r in[r][c] via double groups
+hipError_t launch_colsum(const double* groups, int g, int c, float* out, hipStream_t s);
+hipError_t launch_iou(const uint8_t* a, const uint8_t* b, size_t n, unsigned long long* out,
+                      hipStream_t s);
+hipError_t launch_mask(const float* logits, uint8_t* mask, int n, int h, int w, hipStream_t s);
+// generic BN stats over an NHWC tensor (per-op BN API)
+hipError_t launch_channel_stats(const float* x, size_t pixels, int c, double* stats,
+                                hipStream_t s);
+hipError_t launch_affine_relu(const float* x, size_t pixels, int c, const float* scale,
+                              const float* shift, int relu, float* y, hipStream_t s);
+hipError_t launch_bn_bwd_stats(const float* dy, const float* x, const float* mean,
+                               const float* invstd, size_t pixels, int c, double* bstats,
+                               hipStream_t s);
+
+}  // namespace unet

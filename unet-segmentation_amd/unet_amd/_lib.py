@@ -1,0 +1,103 @@
+"""ctypes binding of libunet_hip.so (include/unet_hip.h).
+
+This is the Python side of the C-ABI boundary.  The library is built in-tree
+(``unet-segmentation_amd/csrc/Makefile`` -> ``unet_amd/libunet_hip.so``); there
+is no fallback: if it cannot be loaded every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("UNET_HIP_LIB", os.path.join(_HERE, "libunet_hip.so"))
+
+_vp = ctypes.c_void_p
+_i = ctypes.c_int
+_f = ctypes.c_float
+_sz = ctypes.c_size_t
+
+# name -> (restype, argtypes); every symbol include/unet_hip.h declares.
+SIGNATURES = {
+    "unet_version": (ctypes.c_char_p, []),
+    "unet_last_error": (ctypes.c_char_p, []),
+    "unet_plan_create": (_vp, [_i, _i, _i, _i, _i]),
+    "unet_plan_destroy": (None, [_vp]),
+    "unet_plan_out_hw": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "unet_plan_workspace_bytes": (_sz, [_vp]),
+    "unet_plan_num_params": (_i, [_vp]),
+    "unet_plan_num_grads": (_i, [_vp]),
+    "unet_plan_forward": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp]),
+    "unet_plan_num_segments": (_i, [_vp]),
+    "unet_plan_segment_grads": (_i, [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
+    "unet_plan_backward": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
+    "unet_plan_set_timing": (_i, [_vp, _i]),
+    "unet_plan_timing": (_i, [_vp, _vp, _vp, _vp, _vp]),
+    "unet_wce_fwd_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp]),
+    "unet_scale_by_device_scalar": (_i, [_vp, _sz, _vp, _vp]),
+    "unet_sgd_momentum": (_i, [_vp, _vp, _vp, _sz, _f, _f, _f, _i, _vp]),
+    "unet_iou_counts": (_i, [_vp, _vp, _sz, _vp, _vp]),
+    "unet_mask_from_logits": (_i, [_vp, _vp, _i, _i, _i, _vp]),
+    "unet_conv3x3_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "unet_conv3x3_dgrad": (_i, [_vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp]),
+    "unet_conv3x3_wgrad": (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "unet_conv_ws_bytes": (_sz, [_i, _i, _i, _i, _i]),
+    "unet_convT2_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp, _vp]),
+    "unet_convT2_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "unet_maxpool2_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "unet_maxpool2_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    "unet_bn_train_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "unet_bn_train_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "unet_bn_ws_bytes": (_sz, [_i]),
+}
+
+_lib = None
+_load_error = None
+
+
+def load():
+    """Load the shared library (once).  Raises RuntimeError if it is missing."""
+    global _lib, _load_error
+    if _lib is not None:
+        return _lib
+    if _load_error is not None:
+        raise RuntimeError(_load_error)
+    try:
+        lib = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+    except OSError as e:  # pragma: no cover - exercised only without a build
+        _load_error = (f"libunet_hip.so could not be loaded from {LIB_PATH} ({e}); "
+                       "build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+        raise RuntimeError(_load_error) from e
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().unet_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (rc={rc}): {last_error()}")
+
+
+def ptr(t) -> int:
+    """Device pointer of a tensor (None -> NULL)."""
+    return None if t is None else t.data_ptr()
+
+
+def ptr_array(tensors):
+    arr = (ctypes.c_void_p * len(tensors))()
+    for i, t in enumerate(tensors):
+        arr[i] = t.data_ptr()
+    return arr
+
+
+def stream_of(device=None):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)

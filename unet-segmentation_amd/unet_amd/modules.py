@@ -1,0 +1,233 @@
+"""Drop-in ``UNet`` and ``WeightedCrossEntropyLoss`` backed by libunet_hip.so.
+
+Mirrors the reference interface:
+
+* ``UNet(n_channels, n_classes, bilinear=False)`` -- models/unet_model.py:66-146
+  (same submodule tree, so ``state_dict`` keys/shapes, ``.apply(init_weights)``
+  from scripts/train.py:54-61, ``.parameters()`` for optim.SGD and
+  ``.train()/.eval()`` behave as in the reference).  The submodules are
+  parameter holders; ``UNet.forward`` runs the whole network as one HIP plan
+  (NHWC activations, fp32 MFMA implicit GEMM) inside one autograd node.
+* ``WeightedCrossEntropyLoss()(inputs, targets, weight_maps)`` --
+  utils/losses.py:29-57, fused forward+backward kernel.
+
+There is no CPU or PyTorch fallback: a non-HIP input raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .plan import Plan
+
+
+def _param_holder_forward(self, *a, **k):
+    raise RuntimeError(
+        f"{type(self).__name__} is a parameter holder of the MI355X UNet; call UNet.forward "
+        "(the whole network runs as one HIP plan)")
+
+
+class DoubleConv(nn.Module):
+    """(conv3x3 valid => BN => ReLU) * 2 -- models/unet_model.py:5-21."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.double_conv = nn.Sequential(
+            nn.Conv2d(in_channels, out_channels, kernel_size=3, padding=0),
+            nn.BatchNorm2d(out_channels),
+            nn.ReLU(inplace=True),
+            nn.Conv2d(out_channels, out_channels, kernel_size=3, padding=0),
+            nn.BatchNorm2d(out_channels),
+            nn.ReLU(inplace=True),
+        )
+
+    forward = _param_holder_forward
+
+
+class Down(nn.Module):
+    """MaxPool2d(2) then DoubleConv -- models/unet_model.py:23-33."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.maxpool_conv = nn.Sequential(nn.MaxPool2d(2), DoubleConv(in_channels, out_channels))
+
+    forward = _param_holder_forward
+
+
+class Up(nn.Module):
+    """ConvTranspose2d(k2,s2) + crop/concat + DoubleConv -- models/unet_model.py:35-54."""
+
+    def __init__(self, in_channels_from_prev_decoder, skip_channels, out_channels, bilinear=False):
+        super().__init__()
+        if bilinear:
+            raise NotImplementedError(
+                "bilinear=True (nn.Upsample branch, models/unet_model.py:40-43) is not on the MI355X "
+                "hot path; the reference default and train.py use bilinear=False")
+        c = in_channels_from_prev_decoder
+        self.up = nn.ConvTranspose2d(c, c // 2, kernel_size=2, stride=2)
+        self.conv = DoubleConv(c // 2 + skip_channels, out_channels)
+
+    forward = _param_holder_forward
+
+
+class OutConv(nn.Module):
+    """1x1 head -- models/unet_model.py:56-63."""
+
+    def __init__(self, in_channels, out_channels):
+        super().__init__()
+        self.conv = nn.Conv2d(in_channels, out_channels, kernel_size=1)
+
+    forward = _param_holder_forward
+
+
+class _Runner:
+    """Per-module cache of HIP plans keyed by input shape."""
+
+    def __init__(self):
+        self.plans = {}
+        self.lock = threading.Lock()
+
+    def plan(self, n, c, h, w, k):
+        key = (n, c, h, w, k)
+        with self.lock:
+            p = self.plans.get(key)
+            if p is None:
+                p = Plan(n, c, h, w, k)
+                self.plans[key] = p
+            return p
+
+
+def _check_tensor(t, name):
+    if not t.is_cuda:
+        raise RuntimeError(f"{name} must be on a HIP device (the MI355X UNet has no CPU path)")
+    if t.dtype != torch.float32:
+        raise RuntimeError(f"{name} must be float32, got {t.dtype}")
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be contiguous")
+
+
+class _UNetFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, module, train, *params):
+        plan = module._runner.plan(x.shape[0], x.shape[1], x.shape[2], x.shape[3], module.n_classes)
+        state = module._state_tensors()
+        for name, t in state:
+            if t.is_floating_point():
+                _check_tensor(t, name)
+            elif not t.is_cuda:
+                raise RuntimeError(f"{name} must be on a HIP device")
+        ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=x.device)
+        logits = torch.empty((x.shape[0], module.n_classes, plan.out_h, plan.out_w), dtype=torch.float32,
+                             device=x.device)
+        tab = _lib.ptr_array([t for _, t in state])
+        plan.forward(tab, x, logits, ws, train)
+        ctx.plan, ctx.ws, ctx.tab, ctx.train = plan, ws, tab, train
+        ctx.params = params
+        ctx.save_for_backward(x)
+        return logits
+
+    @staticmethod
+    def backward(ctx, dlogits):
+        if not ctx.train:
+            raise RuntimeError("backward through an eval-mode UNet forward is not supported by the MI355X "
+                               "plan (train.py only differentiates train-mode forwards)")
+        (x,) = ctx.saved_tensors
+        dlogits = dlogits.contiguous()
+        grads = [torch.empty_like(p) for p in ctx.params]
+        ctx.plan.backward(ctx.tab, _lib.ptr_array(grads), x, dlogits, ctx.ws)
+        ctx.ws = None
+        return (None, None, None, *grads)
+
+
+class UNet(nn.Module):
+    """Valid-convolution U-Net (models/unet_model.py:65-146) on MI355X."""
+
+    def __init__(self, n_channels, n_classes, bilinear=False):
+        super().__init__()
+        if bilinear:
+            raise NotImplementedError("bilinear=True is outside the MI355X hot path (reference default False)")
+        if not 1 <= n_channels <= 4:
+            raise ValueError("n_channels must be in 1..4 (first conv is the Ci<=4 direct kernel)")
+        if not 1 <= n_classes <= 4:
+            raise ValueError("n_classes must be in 1..4")
+        self.n_channels = n_channels
+        self.n_classes = n_classes
+        self.bilinear = bilinear
+        self.inc = DoubleConv(n_channels, 64)
+        self.down1 = Down(64, 128)
+        self.down2 = Down(128, 256)
+        self.down3 = Down(256, 512)
+        self.down4 = Down(512, 1024)
+        self.up1 = Up(1024, 512, 512, bilinear)
+        self.up2 = Up(512, 256, 256, bilinear)
+        self.up3 = Up(256, 128, 128, bilinear)
+        self.up4 = Up(128, 64, 64, bilinear)
+        self.outc = OutConv(64, n_classes)
+        self._runner = _Runner()
+
+    # reference helper (models/unet_model.py:88-102), kept for API parity
+    @staticmethod
+    def _center_crop(feature_map, target_size):
+        _, _, h, w = feature_map.size()
+        th, tw = target_size
+        hs, ws = max(0, (h - th) // 2), max(0, (w - tw) // 2)
+        return feature_map[:, :, hs:hs + th, ws:ws + tw]
+
+    def _state_tensors(self):
+        """(name, tensor) of all 136 state_dict entries in reference order."""
+        return list(self.state_dict(keep_vars=True).items())
+
+    def forward(self, x):
+        _check_tensor(x, "input")
+        if x.dim() != 4 or x.shape[1] != self.n_channels:
+            raise ValueError(f"expected input (N, {self.n_channels}, H, W), got {tuple(x.shape)}")
+        params = tuple(self.parameters())
+        return _UNetFunction.apply(x, self, bool(self.training), *params)
+
+
+class _WCEFunction(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, logits, targets, weights):
+        _check_tensor(logits, "inputs")
+        if targets.dtype != torch.int64 or not targets.is_cuda:
+            raise RuntimeError("targets must be an int64 HIP tensor")
+        if weights.dtype != torch.float32:
+            weights = weights.float()
+        n, k, h, w = logits.shape
+        if targets.shape != (n, h, w) or weights.shape != (n, h, w):
+            raise ValueError(f"targets/weight_maps must be (N,H,W)=({n},{h},{w}); got {tuple(targets.shape)}, "
+                             f"{tuple(weights.shape)}")
+        lib = _lib.load()
+        loss = torch.empty((), dtype=torch.float32, device=logits.device)
+        dl = torch.empty_like(logits)
+        acc = torch.empty(8, dtype=torch.float64, device=logits.device)
+        ts = (ctypes.c_int64 * 3)(*targets.stride())
+        wsd = (ctypes.c_int64 * 3)(*weights.stride())
+        _lib.check(lib.unet_wce_fwd_bwd(logits.data_ptr(), targets.data_ptr(), weights.data_ptr(), n, k, h, w,
+                                        ts, wsd, loss.data_ptr(), dl.data_ptr(), ctypes.c_float(1.0),
+                                        acc.data_ptr(), _lib.stream_of(logits.device)), "unet_wce_fwd_bwd")
+        ctx.save_for_backward(dl)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        (dl,) = ctx.saved_tensors
+        g = g.to(torch.float32).contiguous()
+        lib = _lib.load()
+        _lib.check(lib.unet_scale_by_device_scalar(dl.data_ptr(), dl.numel(), g.data_ptr(),
+                                                   _lib.stream_of(dl.device)), "unet_scale_by_device_scalar")
+        return dl, None, None
+
+
+class WeightedCrossEntropyLoss(nn.Module):
+    """Pixel-weighted cross-entropy (utils/losses.py:6-57): mean(w * CE_none(l, t))."""
+
+    def __init__(self):
+        super().__init__()
+
+    def forward(self, inputs, targets, weight_maps):
+        return _WCEFunction.apply(inputs, targets, weight_maps)

@@ -1,0 +1,62 @@
+"""Python handle of a ``unet_plan`` (include/unet_hip.h)."""
+from __future__ import annotations
+
+import ctypes
+
+from . import _lib
+
+N_PARAMS = 136   # state_dict entries (parameters + BN buffers)
+N_GRADS = 82     # named_parameters
+N_SEGMENTS = 9   # backward segments: head+up4, up3, up2, up1, down4, down3, down2, down1, inc
+
+
+class Plan:
+    """One compiled schedule for input shape (n, c, h, w) and n_classes."""
+
+    def __init__(self, n, c, h, w, n_classes):
+        self.lib = _lib.load()
+        self.handle = self.lib.unet_plan_create(n, c, h, w, n_classes)
+        if not self.handle:
+            raise ValueError(f"unet_plan_create({n},{c},{h},{w},{n_classes}): {_lib.last_error()}")
+        oh, ow = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.unet_plan_out_hw(self.handle, ctypes.byref(oh), ctypes.byref(ow)), "unet_plan_out_hw")
+        self.shape = (n, c, h, w)
+        self.n_classes = n_classes
+        self.out_h, self.out_w = oh.value, ow.value
+        self.workspace_bytes = int(self.lib.unet_plan_workspace_bytes(self.handle))
+
+    def __del__(self):
+        h = getattr(self, "handle", None)
+        if h:
+            self.lib.unet_plan_destroy(h)
+            self.handle = None
+
+    def segment_grads(self, seg):
+        f, k = ctypes.c_int(), ctypes.c_int()
+        _lib.check(self.lib.unet_plan_segment_grads(self.handle, seg, ctypes.byref(f), ctypes.byref(k)),
+                   "unet_plan_segment_grads")
+        return f.value, k.value
+
+    def forward(self, param_tab, x, logits, ws, train):
+        _lib.check(self.lib.unet_plan_forward(self.handle, param_tab, x.data_ptr(), logits.data_ptr(),
+                                              ws.data_ptr(), int(bool(train)), _lib.stream_of(x.device)),
+                   "unet_plan_forward")
+
+    def backward(self, param_tab, grad_tab, x, dlogits, ws, seg_begin=0, seg_end=N_SEGMENTS):
+        _lib.check(self.lib.unet_plan_backward(self.handle, param_tab, grad_tab, x.data_ptr(), dlogits.data_ptr(),
+                                               ws.data_ptr(), seg_begin, seg_end, _lib.stream_of(x.device)),
+                   "unet_plan_backward")
+
+    def set_timing(self, enable):
+        _lib.check(self.lib.unet_plan_set_timing(self.handle, int(bool(enable))), "unet_plan_set_timing")
+
+    def timing(self):
+        """{class: (ms, flops, bytes, launches)} accumulated since the last call."""
+        n = 5
+        ms = (ctypes.c_double * n)()
+        fl = (ctypes.c_double * n)()
+        by = (ctypes.c_double * n)()
+        cnt = (ctypes.c_int * n)()
+        _lib.check(self.lib.unet_plan_timing(self.handle, ms, fl, by, cnt), "unet_plan_timing")
+        names = ["conv_fwd", "conv_dgrad", "conv_wgrad", "stage1", "elementwise"]
+        return {names[i]: (ms[i], fl[i], by[i], cnt[i]) for i in range(n)}
