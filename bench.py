@@ -1,0 +1,200 @@
+"""Benchmark: U-Net training images/s at 512x512x1, batch 8 per GPU, fp32
+(BASELINE.json configs[1]; weak scaling over 1/2/4/8 MI355X with an RCCL
+gradient all-reduce over xGMI).
+
+A step = forward + WeightedCrossEntropyLoss + backward + all-reduce (N>1) +
+SGD(momentum 0.99) over one synthetic batch resident in HBM, exactly the body
+of scripts/train.py:108-131 (no per-step .item()).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "unet-segmentation_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+METRIC = "training images/sec (512×512×1, batch=8) at 1/2/4/8 MI355X; IoU vs ref"
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak
+HBM_PEAK_GBS = 8000.0
+
+
+def init_weights(m):
+    """scripts/train.py:54-61."""
+    if isinstance(m, torch.nn.Conv2d):
+        torch.nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+        if m.bias is not None:
+            torch.nn.init.constant_(m.bias, 0)
+    elif isinstance(m, torch.nn.BatchNorm2d):
+        torch.nn.init.constant_(m.weight, 1)
+        torch.nn.init.constant_(m.bias, 0)
+
+
+def synthetic_batch(n, size, out, device, seed):
+    """x ~ U[0,1), target ~ Bernoulli(0.4), weight = 10 + 1/freq(class) per image
+    (the committed HeLa weight maps have exactly this form)."""
+    g = torch.Generator(device=device)
+    g.manual_seed(seed)
+    x = torch.rand((n, 1, size, size), generator=g, device=device)
+    t = (torch.rand((n, out, out), generator=g, device=device) < 0.4).long()
+    f1 = t.float().mean(dim=(1, 2), keepdim=True).clamp_min(1e-6)
+    w = torch.where(t > 0, 10.0 + 1.0 / f1, 10.0 + 1.0 / (1.0 - f1).clamp_min(1e-6))
+    return x.contiguous(), t.contiguous(), w.contiguous()
+
+
+def cpu_baseline(seconds_hint=20.0):
+    """The CPU restatement of the reference train step (oracle/, a port: the
+    reference .py does not travel), 512x512x1 batch 1, fp32, timed on this host."""
+    import numpy as np
+    from oracle import unet_oracle as O
+    from oracle import fixtures as F
+    threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
+    params = O.hash_init(1, 2, seed=0)
+    x, t, w = F.make_inputs(0, 1, 1, 512)
+    p = {k: np.asarray(v, np.float32) for k, v in params.items()}
+    bufs = {}
+    steps, t0 = 0, time.time()
+    while True:
+        net = O.UNetOracle(p, dtype=np.float32)
+        logits, cache, nb = net.forward(x)
+        loss, dl = O.weighted_ce(logits, t, w)
+        grads = net.backward(dl.astype(np.float32), cache)
+        for k, g in grads.items():
+            p[k], bufs[k] = O.sgd_momentum_step(p[k], g.astype(np.float32), bufs.get(k))
+        p.update(nb)
+        steps += 1
+        if time.time() - t0 > seconds_hint or steps >= 3:
+            break
+    dt = time.time() - t0
+    return {"value": round(steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{steps} train step(s) (fwd+WCE+bwd+SGD) of one 512x512x1 image, NumPy/OpenBLAS fp32 "
+                      f"restatement in oracle/, {dt:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=8, help="images per GPU")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    device = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+        pg = dist.group.WORLD
+
+    from unet_amd import UNet
+    from unet_amd.train import Trainer
+
+    torch.manual_seed(0)
+    model = UNet(n_channels=1, n_classes=2)
+    model.apply(init_weights)
+    model = model.to(device).train()
+    if pg is not None:  # identical start on every rank
+        for t in model.state_dict().values():
+            dist.broadcast(t, 0)
+    trainer = Trainer(model, args.batch, args.size, args.size, lr=1e-4, momentum=0.99, process_group=pg,
+                      overlap=not args.no_overlap)
+    oh, ow = trainer.out_hw
+    x, t, w = synthetic_batch(args.batch, args.size, oh, device, seed=1234 + rank)
+
+    for _ in range(args.warmup):
+        trainer.step(x, t, w)
+    torch.cuda.synchronize()
+    if pg is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = trainer.step(x, t, w)
+    torch.cuda.synchronize()
+    if pg is not None:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if pg is not None:
+        e = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(e, op=dist.ReduceOp.MAX)
+        elapsed = float(e.item())
+    final_loss = float(loss.item())
+
+    # per-kernel-class timing of one extra (untimed) step: HIP events recorded by
+    # the plan on the stream its kernels run on
+    trainer.plan.set_timing(True)
+    trainer.step(x, t, w)
+    torch.cuda.synchronize()
+    trainer.plan.set_timing(False)
+    tim = trainer.plan.timing()
+
+    if rank == 0:
+        imgs = world * args.batch * args.steps
+        value = imgs / elapsed
+        conv = [tim[k] for k in ("conv_fwd", "conv_dgrad", "conv_wgrad")]
+        conv_ms = sum(c[0] for c in conv)
+        conv_fl = sum(c[1] for c in conv)
+        achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+        launches = sum(c[3] for c in conv)
+        st = tim["stage1"]
+        kernels = {k: {"ms": round(v[0], 3), "launches": v[3],
+                       "tflops": round(v[1] / (v[0] * 1e-3) / 1e12, 2) if v[0] > 0 and v[1] else None,
+                       "gbs": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 and v[2] else None}
+                   for k, v in tim.items()}
+        out = {
+            "metric": METRIC,
+            "value": round(value, 3),
+            "unit": "images/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "fp32",
+            "data": "synthetic: x~U[0,1) (N,1,512,512), Bernoulli(0.4) targets, 10+1/freq(class) weight maps; "
+                    "kaiming fan_out init (scripts/train.py:54-61)",
+            "config": {"workload": f"U-Net train step {args.size}x{args.size}x1, batch {args.batch}/GPU, fp32: "
+                                   "fwd + weighted CE + bwd + SGD(0.99)" + (" + RCCL all-reduce" if world > 1 else ""),
+                       "global_batch": world * args.batch, "image": args.size,
+                       "parallelism": f"dp{world}"},
+            "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv family (k_igemm fwd/dgrad + k_wgrad)",
+                         "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                         "flops_per_step": conv_fl, "launches_per_step": launches,
+                         "avg_launch_ms": round(conv_ms / max(launches, 1), 4)},
+            "stage1": {"bound": "hbm", "ms": round(st[0], 3),
+                       "achieved_gbs": round(st[2] / (st[0] * 1e-3) / 1e9, 1) if st[0] > 0 else None,
+                       "peak_gbs": HBM_PEAK_GBS},
+            "kernels": kernels,
+            "final_loss": round(final_loss, 5),
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline()
+        print(json.dumps(out))
+    if pg is not None:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -21,8 +21,22 @@ def lib():
     return _lib.load()
 
 
+_KEEP = []
+
+
 def dev(a, dtype=torch.float32):
-    return torch.from_numpy(np.ascontiguousarray(a)).to("cuda", dtype)
+    """Device copy that stays alive until the test ends (raw pointers are
+    handed to the C-ABI, so the caching allocator must not recycle it)."""
+    t = torch.from_numpy(np.ascontiguousarray(a)).to("cuda", dtype)
+    _KEEP.append(t)
+    return t
+
+
+@pytest.fixture(autouse=True)
+def _release():
+    yield
+    torch.cuda.synchronize()
+    _KEEP.clear()
 
 
 def host(t):

@@ -84,6 +84,7 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict_
       s2 += acc * acc;
     }
   }
+  if (stats == nullptr) return;  // eval mode: no batch statistics
   __shared__ float red[4][2][64];
   red[q][0][c] = s1;
   red[q][1][c] = s2;

@@ -1,0 +1,137 @@
+"""Autograd-free training step for the MI355X UNet (scripts/train.py loop body).
+
+``Trainer.step(x, targets, weights)`` does exactly what scripts/train.py:114-131
+does per minibatch -- zero_grad, forward, WeightedCrossEntropyLoss, backward,
+SGD(lr, momentum=0.99).step() -- with the same arithmetic as the drop-in
+``UNet``/``WeightedCrossEntropyLoss``/``torch.optim.SGD`` trio, but:
+
+* parameters, gradients and momentum live in three flat fp32 buffers (the
+  module's parameters are re-homed as views, so ``state_dict`` is unchanged);
+* one persistent plan workspace (no per-step allocation);
+* the optimizer is one fused kernel over the flat buffer;
+* with a process group, the backward runs in 9 segments and each segment's
+  gradient bucket is all-reduced (RCCL over xGMI) while later segments compute.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib
+from .plan import N_SEGMENTS, Plan
+
+
+def _align4(n):
+    return (n + 3) // 4 * 4
+
+
+class FlatParams:
+    """Re-home a module's parameters into one flat buffer (16-B aligned slots)."""
+
+    def __init__(self, module: torch.nn.Module):
+        params = list(module.parameters())
+        dev = params[0].device
+        offs, total = [], 0
+        for p in params:
+            offs.append(total)
+            total += _align4(p.numel())
+        self.numel = total
+        self.offsets = offs
+        self.params = params
+        self.flat = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.grad = torch.zeros(total, dtype=torch.float32, device=dev)
+        self.momentum = torch.zeros(total, dtype=torch.float32, device=dev)
+        with torch.no_grad():
+            for p, o in zip(params, offs):
+                view = self.flat[o:o + p.numel()].view_as(p)
+                view.copy_(p.data)
+                p.data = view
+        self.grad_views = [self.grad[o:o + p.numel()].view_as(p) for p, o in zip(params, offs)]
+
+    def slice_for(self, first, count):
+        """Flat-buffer slice holding parameters [first, first+count)."""
+        a = self.offsets[first]
+        b = self.offsets[first + count] if first + count < len(self.offsets) else self.numel
+        return self.grad[a:b]
+
+
+class Trainer:
+    def __init__(self, model, batch, height, width, lr=1e-4, momentum=0.99, process_group=None,
+                 overlap=True):
+        from .modules import UNet
+        if not isinstance(model, UNet):
+            raise TypeError("Trainer drives the MI355X UNet")
+        self.model = model
+        self.lr, self.mom = float(lr), float(momentum)
+        self.pg = process_group
+        self.overlap = overlap
+        self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
+        self.flat = FlatParams(model)
+        dev = self.flat.flat.device
+        self.plan = Plan(batch, model.n_channels, height, width, model.n_classes)
+        self.ws = torch.empty(self.plan.workspace_bytes, dtype=torch.uint8, device=dev)
+        self.state = [t for _, t in model.state_dict(keep_vars=True).items()]
+        self.param_tab = _lib.ptr_array(self.state)
+        self.grad_tab = _lib.ptr_array(self.flat.grad_views)
+        k, oh, ow = model.n_classes, self.plan.out_h, self.plan.out_w
+        self.logits = torch.empty((batch, k, oh, ow), dtype=torch.float32, device=dev)
+        self.dlogits = torch.empty_like(self.logits)
+        self.loss = torch.empty((), dtype=torch.float32, device=dev)
+        self.acc = torch.empty(8, dtype=torch.float64, device=dev)
+        self.first_step = True
+        self.lib = _lib.load()
+
+    @property
+    def out_hw(self):
+        return self.plan.out_h, self.plan.out_w
+
+    def forward_loss(self, x, targets, weights):
+        self.plan.forward(self.param_tab, x, self.logits, self.ws, True)
+        n, k, h, w = self.logits.shape
+        ts = (ctypes.c_int64 * 3)(*targets.stride())
+        wsd = (ctypes.c_int64 * 3)(*weights.stride())
+        _lib.check(self.lib.unet_wce_fwd_bwd(self.logits.data_ptr(), targets.data_ptr(), weights.data_ptr(), n, k, h,
+                                             w, ts, wsd, self.loss.data_ptr(), self.dlogits.data_ptr(),
+                                             ctypes.c_float(1.0), self.acc.data_ptr(), _lib.stream_of(x.device)),
+                   "unet_wce_fwd_bwd")
+        return self.loss
+
+    def backward_and_reduce(self, x):
+        works = []
+        if self.pg is None or not self.overlap:
+            self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, 0, N_SEGMENTS)
+            if self.pg is not None:
+                works.append(torch.distributed.all_reduce(self.flat.grad, group=self.pg, async_op=True))
+        else:
+            for s in range(N_SEGMENTS):
+                self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, s, s + 1)
+                f, k = self.plan.segment_grads(s)
+                works.append(torch.distributed.all_reduce(self.flat.slice_for(f, k), group=self.pg,
+                                                          async_op=True))
+        for w in works:
+            w.wait()
+
+    def optimizer_step(self):
+        fp = self.flat
+        _lib.check(self.lib.unet_sgd_momentum(fp.flat.data_ptr(), fp.grad.data_ptr(), fp.momentum.data_ptr(),
+                                              fp.numel, ctypes.c_float(self.lr), ctypes.c_float(self.mom),
+                                              ctypes.c_float(1.0 / self.world), int(self.first_step),
+                                              _lib.stream_of(fp.flat.device)), "unet_sgd_momentum")
+        self.first_step = False
+
+    def step(self, x, targets, weights):
+        """One train.py step; returns the (device) loss without synchronising."""
+        if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()):
+            raise RuntimeError("x must be a contiguous float32 HIP tensor")
+        loss = self.forward_loss(x, targets, weights)
+        self.backward_and_reduce(x)
+        self.optimizer_step()
+        return loss
+
+    def sync_buffers(self, src=0):
+        """DDP buffer semantics: broadcast rank-src BatchNorm running stats."""
+        if self.pg is None:
+            return
+        for name, t in self.model.named_buffers():
+            torch.distributed.broadcast(t, src, group=self.pg)
