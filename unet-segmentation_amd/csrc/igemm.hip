@@ -12,7 +12,9 @@
 // 64 contiguous bytes per row per K-step), with the consumer-side BatchNorm+ReLU
 // transform and the skip/upsample channel concat folded into the gather.
 // LDS tiles are [rows][16+4] floats (80-B row stride: ds_read_b128 conflict-free),
-// double buffered, register-prefetched one K-step ahead (one barrier per step).
+// double buffered.  The next K-step's global loads are issued before the MFMA
+// block and consumed (transform + ds_write) after it, so each wave's HBM/L2
+// latency hides under its own 32 MFMAs (2048 cycles) plus its SIMD partners'.
 #include "unet_internal.h"
 
 namespace unet {
@@ -22,8 +24,7 @@ typedef float floatx16 __attribute__((ext_vector_type(16)));
 __device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 __device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
-__device__ __forceinline__ float4 affine_relu4(float4 v, const float* sc, const float* sh, int c) {
-  float4 a = ld4(sc + c), b = ld4(sh + c);
+__device__ __forceinline__ float4 affine_relu4(float4 v, float4 a, float4 b) {
   v.x = fmaxf(fmaf(v.x, a.x, b.x), 0.f);
   v.y = fmaxf(fmaf(v.y, a.y, b.y), 0.f);
   v.z = fmaxf(fmaf(v.z, a.z, b.z), 0.f);
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
   constexpr int BK = 16, LDK = BK + 4;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   constexpr int AV = BM / 64, BV = BN / 64;   // float4 loads per thread per K-step
-  static_assert(WM * WN == 4, "4 waves");
+  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
   __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -65,7 +66,8 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
     m = m < M ? m : M - 1;
     int n = m / HWg, r = m - n * HWg;
     int y = r / g.Wg, x = r - y * g.Wg;
-    y *= g.stride; x *= g.stride;
+    y *= g.stride;
+    x *= g.stride;
     rb0[q] = (n * g.s[0].H + y + g.s[0].oy) * g.s[0].W + x + g.s[0].ox;
     rb1[q] = (n * g.s[1].H + y + g.s[1].oy) * g.s[1].W + x + g.s[1].ox;
   }
@@ -73,30 +75,38 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
 #pragma unroll
   for (int q = 0; q < BV; ++q) bptr[q] = args.b + (size_t)(n0 + (tid >> 2) + 64 * q) * K + col4 * 4;
 
-  float4 ra[AV], rb[BV];
-  auto load_regs = [&](int k0) {
-    const int tap = k0 / g.Cg;
-    const int c0 = k0 - tap * g.Cg;
-    const int ty = tap / g.taps_w, tx = tap - ty * g.taps_w;
-    const bool second = c0 >= g.c_split;
+  // K iterator (uniform): chunk -> (tap_y, tap_x, c0)
+  int it_ty = 0, it_tx = 0, it_c = 0;
+  float4 ra[AV], rb[BV], rsc, rsh;
+  bool rtf = false;
+  auto issue = [&](int k0) {
+    const bool second = it_c >= g.c_split;
     const Src& s = second ? g.s[1] : g.s[0];
-    const int c = (second ? c0 - g.c_split : c0) + col4 * 4;
-    const int toff = ty * s.W + tx;
+    const int c = (second ? it_c - g.c_split : it_c) + col4 * 4;
+    const int toff = it_ty * s.W + it_tx;
 #pragma unroll
-    for (int q = 0; q < AV; ++q) {
-      const int pix = (second ? rb1[q] : rb0[q]) + toff;
-      ra[q] = ld4(s.ptr + (size_t)pix * s.C + c);
-    }
-    if (s.scale) {
-#pragma unroll
-      for (int q = 0; q < AV; ++q) ra[q] = affine_relu4(ra[q], s.scale, s.shift, c);
-    }
+    for (int q = 0; q < AV; ++q) ra[q] = ld4(s.ptr + (size_t)((second ? rb1[q] : rb0[q]) + toff) * s.C + c);
 #pragma unroll
     for (int q = 0; q < BV; ++q) rb[q] = ld4(bptr[q] + k0);
+    rtf = s.scale != nullptr;
+    if (rtf) {
+      rsc = ld4(s.scale + c);
+      rsh = ld4(s.shift + c);
+    }
+    // advance the iterator to the next chunk
+    it_c += BK;
+    if (it_c == g.Cg) {
+      it_c = 0;
+      if (++it_tx == g.taps_w) { it_tx = 0; ++it_ty; }
+    }
   };
-  auto store_lds = [&](int buf) {
+  auto commit = [&](int buf) {
     float* As = lds + buf * (BM + BN) * LDK;
     float* Bs = As + BM * LDK;
+    if (rtf) {
+#pragma unroll
+      for (int q = 0; q < AV; ++q) ra[q] = affine_relu4(ra[q], rsc, rsh);
+    }
 #pragma unroll
     for (int q = 0; q < AV; ++q) st4(As + ((tid >> 2) + 64 * q) * LDK + col4 * 4, ra[q]);
 #pragma unroll
@@ -113,12 +123,13 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
 
   const int h = lane >> 5, li = lane & 31;
   const int nk = K / BK;
-  load_regs(0);
-  store_lds(0);
+  issue(0);
+  commit(0);
   __syncthreads();
   for (int kc = 0; kc < nk; ++kc) {
     const int cur = kc & 1;
-    if (kc + 1 < nk) load_regs((kc + 1) * BK);
+    const bool more = kc + 1 < nk;
+    if (more) issue((kc + 1) * BK);
     const float* As = lds + cur * (BM + BN) * LDK;
     const float* Bs = As + BM * LDK;
     float4 a0[TM], a1[TM], b0[TN], b1[TN];
@@ -142,14 +153,13 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(a0[i], a1[i], s), comp(b0[j], b1[j], s),
                                                            acc[i][j], 0, 0, 0);
-    if (kc + 1 < nk) store_lds(cur ^ 1);
+    if (more) commit(cur ^ 1);
     __syncthreads();
   }
 
   // ------------------------------ epilogue ---------------------------------
   const Epilogue& e = args.e;
   const int N = args.N;
-  // column statistics accumulated per lane (one column per lane per tile j)
   float s1[TN], s2[TN], t1[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; t1[j] = 0.f; }
@@ -164,6 +174,7 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
     float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
     const bool bwd_mask = (e.yref != nullptr) && !second;
     if (bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
+    const bool linear = !e.shuffle_co && d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg;
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
 #pragma unroll
@@ -173,13 +184,13 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
         if (m >= M) continue;
         float v = acc[i][j][r] + bias;
         size_t idx;
-        if (e.shuffle_co) {
+        if (linear) {
+          idx = (size_t)m * d.C + dcol;
+        } else if (e.shuffle_co) {
           const int ab = dcol / e.shuffle_co, co = dcol - ab * e.shuffle_co;
           const int n = m / HWg, rr = m - n * HWg;
           const int y = rr / g.Wg, x = rr - y * g.Wg;
           idx = ((size_t)(n * d.H + 2 * y + (ab >> 1) + d.oy) * d.W + 2 * x + (ab & 1) + d.ox) * d.C + co;
-        } else if (d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg) {
-          idx = (size_t)m * d.C + dcol;
         } else {
           const int n = m / HWg, rr = m - n * HWg;
           const int y = rr / g.Wg, x = rr - y * g.Wg;
@@ -202,15 +213,13 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
   }
   const bool want_stats = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
   if (!want_stats) return;
-  // reduce lanes l and l+32 (same column), then the WM waves sharing columns
-  __shared__ float red[4][3][BN];
+  __shared__ float red[WM][3][BN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     s1[j] += __shfl_xor(s1[j], 32);
     s2[j] += __shfl_xor(s2[j], 32);
     t1[j] += __shfl_xor(t1[j], 32);
   }
-  __syncthreads();
   if (h == 0) {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
@@ -244,15 +253,38 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
 // ---------------------------------------------------------------------------
 // k_wgrad: C[i][j] = sum_p A_p[i] * B_p[j], p = pixels (split over blockIdx.z).
 // LDS tiles are [16 pixels][BM] and [16 pixels][BN] (channel contiguous).
+// Each thread owns fixed columns (channel slice of A; (tap, channel) of B) and
+// walks its staged pixel rows incrementally (no divisions in the loop).
 // ---------------------------------------------------------------------------
+struct PixIt {
+  int n, y, x;
+  __device__ __forceinline__ void init(int p, int Hg, int Wg) {
+    const int hw = Hg * Wg;
+    n = p / hw;
+    const int r = p - n * hw;
+    y = r / Wg;
+    x = r - y * Wg;
+  }
+  __device__ __forceinline__ void advance(int d, int Hg, int Wg) {
+    x += d;
+    while (x >= Wg) {
+      x -= Wg;
+      if (++y == Hg) { y = 0; ++n; }
+    }
+  }
+};
+
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
   constexpr int BK = 16;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   constexpr int AR = BM / 4, BR = BN / 4;            // float4 per staged pixel row
-  constexpr int AP = BK * AR / 256, BP = BK * BR / 256;  // rows per thread
-  static_assert(AP >= 1 && BP >= 1, "tile too small");
+  constexpr int ASTEP = 256 / AR, BSTEP = 256 / BR;  // rows covered per pass
+  constexpr int AP = (BK + ASTEP - 1) / ASTEP, BP = (BK + BSTEP - 1) / BSTEP;
+  static_assert(AR <= 256 && BR <= 256, "tile widths");
   __shared__ __attribute__((aligned(16))) float lds[2 * BK * (BM + BN)];
+  // threads beyond the last full pass of a row group stage nothing (BN = 192: 240 of 256)
+  const bool aact = threadIdx.x < ASTEP * AR, bact = threadIdx.x < BSTEP * BR;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -261,15 +293,13 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
   const int pend = min(args.P, pbeg + args.pix_per_split);
   const Gather& ga = args.ga;
   const Gather& gb = args.gb;
-  const int HWg = ga.Hg * ga.Wg;
 
   // A: fixed channel slice of the (single) source of ga.
-  const int acol4 = tid % AR;
-  const int arow = tid / AR;                  // + (256/AR)*q
+  const int acol4 = tid % AR, arow = tid / AR;
   const int ac = i0 + acol4 * 4;
+  const Src& as = ga.s[0];
   // B: fixed (tap, channel) per thread.
-  const int bcol4 = tid % BR;
-  const int brow = tid / BR;
+  const int bcol4 = tid % BR, brow = tid / BR;
   const int bj = j0 + bcol4 * 4;
   const int btap = bj / gb.Cg;
   const int bc0 = bj - btap * gb.Cg;
@@ -277,46 +307,52 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
   const Src& bs = bsecond ? gb.s[1] : gb.s[0];
   const int bc = bsecond ? bc0 - gb.c_split : bc0;
   const int bty = btap / gb.taps_w, btx = btap - bty * gb.taps_w;
-  const Src& as = ga.s[0];
+
+  float4 asc = make_float4(0, 0, 0, 0), ash = asc, bsc = asc, bsh = asc;
+  if (as.scale) { asc = ld4(as.scale + ac); ash = ld4(as.shift + ac); }
+  if (bs.scale) { bsc = ld4(bs.scale + bc); bsh = ld4(bs.shift + bc); }
+
+  PixIt ait[AP], bit[BP];
+  bool ain[AP], bin[BP];
+#pragma unroll
+  for (int q = 0; q < AP; ++q) ait[q].init(min(pbeg + arow + ASTEP * q, args.P - 1), ga.Hg, ga.Wg);
+#pragma unroll
+  for (int q = 0; q < BP; ++q) bit[q].init(min(pbeg + brow + BSTEP * q, args.P - 1), gb.Hg, gb.Wg);
 
   float4 ra[AP], rb[BP];
-  auto load_regs = [&](int p0) {
+  auto issue = [&](int p0) {
 #pragma unroll
     for (int q = 0; q < AP; ++q) {
-      const int p = p0 + arow + (256 / AR) * q;
-      if (p < pend) {
-        const int n = p / HWg, r = p - n * HWg;
-        const int y = r / ga.Wg, x = r - y * ga.Wg;
-        const int pix = (n * as.H + y * ga.stride + as.oy) * as.W + x * ga.stride + as.ox;
-        float4 v = ld4(as.ptr + (size_t)pix * as.C + ac);
-        if (as.scale) v = affine_relu4(v, as.scale, as.shift, ac);
-        ra[q] = v;
-      } else {
-        ra[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      const int p = p0 + arow + ASTEP * q;
+      ain[q] = p < pend && (arow + ASTEP * q) < BK;
+      const int pix = (ait[q].n * as.H + ait[q].y * ga.stride + as.oy) * as.W + ait[q].x * ga.stride + as.ox;
+      ra[q] = ld4(as.ptr + (size_t)pix * as.C + ac);
+      if (p + BK < pend) ait[q].advance(BK, ga.Hg, ga.Wg);
     }
 #pragma unroll
     for (int q = 0; q < BP; ++q) {
-      const int p = p0 + brow + (256 / BR) * q;
-      if (p < pend) {
-        const int n = p / HWg, r = p - n * HWg;
-        const int y = r / gb.Wg, x = r - y * gb.Wg;
-        const int pix = (n * bs.H + y * gb.stride + bty + bs.oy) * bs.W + x * gb.stride + btx + bs.ox;
-        float4 v = ld4(bs.ptr + (size_t)pix * bs.C + bc);
-        if (bs.scale) v = affine_relu4(v, bs.scale, bs.shift, bc);
-        rb[q] = v;
-      } else {
-        rb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
-      }
+      const int p = p0 + brow + BSTEP * q;
+      bin[q] = p < pend && (brow + BSTEP * q) < BK;
+      const int pix = (bit[q].n * bs.H + bit[q].y * gb.stride + bty + bs.oy) * bs.W + bit[q].x * gb.stride + btx +
+                      bs.ox;
+      rb[q] = ld4(bs.ptr + (size_t)pix * bs.C + bc);
+      if (p + BK < pend) bit[q].advance(BK, gb.Hg, gb.Wg);
     }
   };
-  auto store_lds = [&](int buf) {
+  auto commit = [&](int buf) {
     float* As = lds + buf * BK * (BM + BN);
     float* Bs = As + BK * BM;
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-    for (int q = 0; q < AP; ++q) st4(As + (arow + (256 / AR) * q) * BM + acol4 * 4, ra[q]);
+    for (int q = 0; q < AP; ++q) {
+      float4 v = as.scale ? affine_relu4(ra[q], asc, ash) : ra[q];
+      if (aact && arow + ASTEP * q < BK) st4(As + (arow + ASTEP * q) * BM + acol4 * 4, ain[q] ? v : z);
+    }
 #pragma unroll
-    for (int q = 0; q < BP; ++q) st4(Bs + (brow + (256 / BR) * q) * BN + bcol4 * 4, rb[q]);
+    for (int q = 0; q < BP; ++q) {
+      float4 v = bs.scale ? affine_relu4(rb[q], bsc, bsh) : rb[q];
+      if (bact && brow + BSTEP * q < BK) st4(Bs + (brow + BSTEP * q) * BN + bcol4 * 4, bin[q] ? v : z);
+    }
   };
 
   floatx16 acc[TM][TN];
@@ -329,14 +365,14 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
 
   const int h = lane >> 5, li = lane & 31;
   const int nk = (pend - pbeg + BK - 1) / BK;
-  if (nk > 0) {
-    load_regs(pbeg);
-    store_lds(0);
-  }
+  if (nk <= 0) return;
+  issue(pbeg);
+  commit(0);
   __syncthreads();
   for (int kc = 0; kc < nk; ++kc) {
     const int cur = kc & 1;
-    if (kc + 1 < nk) load_regs(pbeg + (kc + 1) * BK);
+    const bool more = kc + 1 < nk;
+    if (more) issue(pbeg + (kc + 1) * BK);
     const float* As = lds + cur * BK * (BM + BN);
     const float* Bs = As + BK * BM;
 #pragma unroll
@@ -352,11 +388,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
     }
-    if (kc + 1 < nk) store_lds(cur ^ 1);
+    if (more) commit(cur ^ 1);
     __syncthreads();
   }
-  if (nk == 0) return;
-  // accumulate the tile into out (fp32 atomics; output is small vs the reduction)
+  // accumulate the tile into out (fp32 atomics; the output is small next to the reduction)
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -372,13 +407,32 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
 // ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
+static int g_num_cus = 0;
+static int num_cus() {
+  if (g_num_cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
+                                                hipSuccess && n > 0)
+      g_num_cus = n;
+    else
+      g_num_cus = 256;
+  }
+  return g_num_cus;
+}
+
 hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s) {
-  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.K % 16) != 0 || (a.a.Cg % 16) != 0 ||
-      (a.a.c_split % 16) != 0)
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.K % 16) != 0 || (a.a.Cg % 16) != 0 || (a.a.c_split % 16) != 0)
     return hipErrorInvalidValue;
+  const long long cus = num_cus();
   if (a.N % 128 == 0) {
-    dim3 grid((a.M + 127) / 128, a.N / 128);
-    hipLaunchKernelGGL((k_igemm<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
+    const long long big = ((a.M + 127) / 128) * (long long)(a.N / 128);
+    if (big >= 4 * cus) {
+      dim3 grid((a.M + 127) / 128, a.N / 128);
+      hipLaunchKernelGGL((k_igemm<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
+    } else {  // small-M layers (bottleneck): twice the workgroups
+      dim3 grid((a.M + 63) / 64, a.N / 128);
+      hipLaunchKernelGGL((k_igemm<64, 128, 2, 2>), grid, dim3(256), 0, s, a);
+    }
   } else if (a.N % 64 == 0) {
     dim3 grid((a.M + 255) / 256, a.N / 64);
     hipLaunchKernelGGL((k_igemm<256, 64, 4, 1>), grid, dim3(256), 0, s, a);
@@ -390,13 +444,19 @@ hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s) {
 
 hipError_t launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   WgradArgs a = a0;
-  if (a.Mo % 64 != 0 || a.No % 64 != 0 || a.P <= 0) return hipErrorInvalidValue;
-  if (a.gb.Cg % 64 != 0 || a.gb.c_split % 4 != 0) return hipErrorInvalidValue;
-  const bool big = (a.Mo % 128 == 0) && (a.No % 128 == 0) && (a.gb.Cg % 128 == 0);
-  const int bm = big ? 128 : 64, bn = big ? 128 : 64;
+  if (a.Mo % 64 != 0 || a.P <= 0 || a.gb.Cg % 4 != 0 || a.gb.c_split % 4 != 0 || a.ga.Cg % 4 != 0)
+    return hipErrorInvalidValue;
+  int bm, bn;
+  if (a.Mo % 128 == 0 && a.No % 128 == 0) { bm = 128; bn = 128; }
+  else if (a.Mo % 128 == 0 && a.No % 192 == 0) { bm = 128; bn = 192; }
+  else if (a.No % 192 == 0) { bm = 64; bn = 192; }
+  else if (a.No % 128 == 0) { bm = 64; bn = 128; }
+  else if (a.No % 64 == 0) { bm = 64; bn = 64; }
+  else return hipErrorInvalidValue;
   const int tiles = (a.Mo / bm) * (a.No / bn);
-  // split the pixel reduction so that the grid has ~2048 workgroups
-  int splits = (2048 + tiles - 1) / tiles;
+  // split the pixel reduction so that the grid has ~8 workgroups per CU
+  const int target = 8 * num_cus();
+  int splits = (target + tiles - 1) / tiles;
   int max_splits = (a.P + 255) / 256;
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
@@ -405,8 +465,14 @@ hipError_t launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   splits = (a.P + pps - 1) / pps;
   a.pix_per_split = pps;
   dim3 grid(a.Mo / bm, a.No / bn, splits);
-  if (big)
+  if (bm == 128 && bn == 128)
     hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
+  else if (bm == 128)
+    hipLaunchKernelGGL((k_wgrad<128, 192, 2, 2>), grid, dim3(256), 0, s, a);
+  else if (bn == 192)
+    hipLaunchKernelGGL((k_wgrad<64, 192, 2, 2>), grid, dim3(256), 0, s, a);
+  else if (bn == 128)
+    hipLaunchKernelGGL((k_wgrad<64, 128, 2, 2>), grid, dim3(256), 0, s, a);
   else
     hipLaunchKernelGGL((k_wgrad<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
   return hipGetLastError();
