@@ -122,6 +122,11 @@ int unet_iou_counts(const uint8_t* pred, const uint8_t* gt, size_t n, unsigned l
 int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int w,
                           unet_stream_t stream);
 
+/* Tuning hook for A/B measurements: "igemm_variant" (-1 = heuristic, 1..9 =
+ * forced tile shape) and "wgrad_variant" (-1 = heuristic, 1 = 64x64 tile,
+ * >=2 = workgroups per CU for the pixel split).  Process-global. */
+int unet_set_tuning(const char* key, int value);
+
 /* ------------------------------------------------------------------------
  * Per-op entry points (used by the op-level parity tests and by tools).
  * Shapes: x (N,H,W,Ci) NHWC; W OIHW as in PyTorch; outputs NHWC.

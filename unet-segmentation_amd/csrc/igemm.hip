@@ -15,6 +15,8 @@
 // double buffered.  The next K-step's global loads are issued before the MFMA
 // block and consumed (transform + ds_write) after it, so each wave's HBM/L2
 // latency hides under its own 32 MFMAs (2048 cycles) plus its SIMD partners'.
+#include <cstdlib>
+
 #include "unet_internal.h"
 
 namespace unet {
@@ -32,22 +34,38 @@ __device__ __forceinline__ float4 affine_relu4(float4 v, float4 a, float4 b) {
   return v;
 }
 
-__device__ __forceinline__ float comp(const float4& a, const float4& b, int s) {
-  switch (s) {
-    case 0: return a.x; case 1: return a.y; case 2: return a.z; case 3: return a.w;
-    case 4: return b.x; case 5: return b.y; case 6: return b.z; default: return b.w;
-  }
-}
-
 // ---------------------------------------------------------------------------
 // k_igemm: C[m][n] = sum_k A[m][k] * B[n][k];  A gathered, B packed [N][K].
+// WM x WN waves, each owning a (TM*32) x (TN*32) block of 32x32 MFMA tiles;
+// BK = 16 or 32 k per LDS stage.  MFMA step s of a stage takes k = s (lanes
+// 0-31) and k = BK/2 + s (lanes 32-63) on both operands, so each lane reads
+// its BK/2 consecutive k of a row with ds_read_b128.
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
-  constexpr int BK = 16, LDK = BK + 4;
+__device__ __forceinline__ float getc(const float4& v, int c) {
+  return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+}
+
+// Occupancy the register allocator must preserve: as many workgroups as the
+// LDS footprint admits per CU (without it hipcc moves the accumulators to
+// AGPRs and drops a wave per SIMD).
+constexpr int igemm_minw(int BM, int BN, int WM, int WN, int BK) {
+  const int lds = 2 * (BM + BN) * (BK + 4) * 4 + WM * 3 * BN * 4;
+  int blocks = 163840 / lds;
+  if (blocks > 8) blocks = 8;
+  int w = blocks * WM * WN * 64 / 256;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
+template <int BM, int BN, int WM, int WN, int BK>
+__global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void k_igemm(const IgemmArgs args) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int LDK = BK + 4;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-  constexpr int AV = BM / 64, BV = BN / 64;   // float4 loads per thread per K-step
-  static_assert(WM * WN == 4 && TM >= 1 && TN >= 1, "4 waves");
+  constexpr int C4 = BK / 4;           // float4 per staged row
+  constexpr int RPP = NT / C4;         // rows per staging pass
+  constexpr int AV = BM / RPP, BV = BN / RPP;
+  constexpr int KH = BK / 2, KF = KH / 4;
+  static_assert(TM >= 1 && TN >= 1 && AV >= 1 && BV >= 1 && BM % RPP == 0 && BN % RPP == 0, "tile");
   __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -55,14 +73,14 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
   const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const Gather& g = args.a;
   const int M = args.M, K = args.K;
-  const int col4 = tid & 3;
+  const int col4 = tid % C4, row0 = tid / C4;
 
   // Per staged A row: pixel base in each source grid (before the tap offset).
   int rb0[AV], rb1[AV];
   const int HWg = g.Hg * g.Wg;
 #pragma unroll
   for (int q = 0; q < AV; ++q) {
-    int m = m0 + (tid >> 2) + 64 * q;
+    int m = m0 + row0 + RPP * q;
     m = m < M ? m : M - 1;
     int n = m / HWg, r = m - n * HWg;
     int y = r / g.Wg, x = r - y * g.Wg;
@@ -73,9 +91,10 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
   }
   const float* bptr[BV];
 #pragma unroll
-  for (int q = 0; q < BV; ++q) bptr[q] = args.b + (size_t)(n0 + (tid >> 2) + 64 * q) * K + col4 * 4;
+  for (int q = 0; q < BV; ++q) bptr[q] = args.b + (size_t)(n0 + row0 + RPP * q) * K + col4 * 4;
 
-  // K iterator (uniform): chunk -> (tap_y, tap_x, c0)
+  // K iterator (uniform): chunk -> (tap_y, tap_x, c0).  A chunk never straddles
+  // a tap or the concat split (Cg and c_split are multiples of BK).
   int it_ty = 0, it_tx = 0, it_c = 0;
   float4 ra[AV], rb[BV], rsc, rsh;
   bool rtf = false;
@@ -93,7 +112,6 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
       rsc = ld4(s.scale + c);
       rsh = ld4(s.shift + c);
     }
-    // advance the iterator to the next chunk
     it_c += BK;
     if (it_c == g.Cg) {
       it_c = 0;
@@ -108,9 +126,9 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
       for (int q = 0; q < AV; ++q) ra[q] = affine_relu4(ra[q], rsc, rsh);
     }
 #pragma unroll
-    for (int q = 0; q < AV; ++q) st4(As + ((tid >> 2) + 64 * q) * LDK + col4 * 4, ra[q]);
+    for (int q = 0; q < AV; ++q) st4(As + (row0 + RPP * q) * LDK + col4 * 4, ra[q]);
 #pragma unroll
-    for (int q = 0; q < BV; ++q) st4(Bs + ((tid >> 2) + 64 * q) * LDK + col4 * 4, rb[q]);
+    for (int q = 0; q < BV; ++q) st4(Bs + (row0 + RPP * q) * LDK + col4 * 4, rb[q]);
   };
 
   floatx16 acc[TM][TN];
@@ -132,26 +150,26 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
     if (more) issue((kc + 1) * BK);
     const float* As = lds + cur * (BM + BN) * LDK;
     const float* Bs = As + BM * LDK;
-    float4 a0[TM], a1[TM], b0[TN], b1[TN];
+    float4 fa[TM][KF], fb[TN][KF];
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
-      const float* p = As + (wm * TM * 32 + i * 32 + li) * LDK + h * 8;
-      a0[i] = ld4(p);
-      a1[i] = ld4(p + 4);
+      const float* p = As + (wm * TM * 32 + i * 32 + li) * LDK + h * KH;
+#pragma unroll
+      for (int f = 0; f < KF; ++f) fa[i][f] = ld4(p + 4 * f);
     }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const float* p = Bs + (wn * TN * 32 + j * 32 + li) * LDK + h * 8;
-      b0[j] = ld4(p);
-      b1[j] = ld4(p + 4);
+      const float* p = Bs + (wn * TN * 32 + j * 32 + li) * LDK + h * KH;
+#pragma unroll
+      for (int f = 0; f < KF; ++f) fb[j][f] = ld4(p + 4 * f);
     }
 #pragma unroll
-    for (int s = 0; s < 8; ++s)
+    for (int s = 0; s < KH; ++s)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(comp(a0[i], a1[i], s), comp(b0[j], b1[j], s),
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(getc(fa[i][s >> 2], s & 3), getc(fb[j][s >> 2], s & 3),
                                                            acc[i][j], 0, 0, 0);
     if (more) commit(cur ^ 1);
     __syncthreads();
@@ -232,7 +250,7 @@ __global__ __launch_bounds__(256, 2) void k_igemm(const IgemmArgs args) {
   __syncthreads();
   const int grp = blockIdx.x % kStatGroups;
   const int nsplit = min(e.n_split, N);
-  for (int lc = tid; lc < BN; lc += 256) {
+  for (int lc = tid; lc < BN; lc += NT) {
     float a = 0.f, b = 0.f, c = 0.f;
 #pragma unroll
     for (int w = 0; w < WM; ++w) { a += red[w][0][lc]; b += red[w][1][lc]; c += red[w][2][lc]; }
@@ -420,26 +438,46 @@ static int num_cus() {
   return g_num_cus;
 }
 
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+// unet_set_tuning("igemm_variant", v) or UNET_IGEMM_VARIANT; -1 = heuristic
+int g_tune_igemm = env_int("UNET_IGEMM_VARIANT", -1);
+int g_tune_wgrad = env_int("UNET_WGRAD_VARIANT", -1);
+
+template <int BM, int BN, int WM, int WN, int BK>
+static hipError_t go_igemm(const IgemmArgs& a, hipStream_t s) {
+  if (a.N % BN != 0 || a.K % BK != 0 || a.a.Cg % BK != 0 || a.a.c_split % BK != 0) return hipErrorInvalidValue;
+  dim3 grid((a.M + BM - 1) / BM, a.N / BN);
+  hipLaunchKernelGGL((k_igemm<BM, BN, WM, WN, BK>), grid, dim3(WM * WN * 64), 0, s, a);
+  return hipGetLastError();
+}
+
 hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.K % 16) != 0 || (a.a.Cg % 16) != 0 || (a.a.c_split % 16) != 0)
     return hipErrorInvalidValue;
+  hipError_t forced = hipErrorInvalidValue;  // a forced variant that does not fit falls back
+  switch (g_tune_igemm) {
+    case 1: forced = go_igemm<128, 128, 2, 2, 16>(a, s); break;
+    case 2: forced = go_igemm<64, 128, 2, 2, 16>(a, s); break;
+    case 3: forced = go_igemm<128, 128, 2, 2, 32>(a, s); break;
+    case 4: forced = go_igemm<256, 128, 4, 2, 16>(a, s); break;
+    case 6: forced = go_igemm<256, 64, 4, 1, 16>(a, s); break;
+    case 7: forced = go_igemm<256, 64, 4, 1, 32>(a, s); break;
+    case 8: forced = go_igemm<128, 64, 2, 2, 16>(a, s); break;
+    case 9: forced = go_igemm<64, 128, 2, 2, 32>(a, s); break;
+    default: break;
+  }
+  if (forced != hipErrorInvalidValue) return forced;
   const long long cus = num_cus();
   if (a.N % 128 == 0) {
     const long long big = ((a.M + 127) / 128) * (long long)(a.N / 128);
-    if (big >= 4 * cus) {
-      dim3 grid((a.M + 127) / 128, a.N / 128);
-      hipLaunchKernelGGL((k_igemm<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
-    } else {  // small-M layers (bottleneck): twice the workgroups
-      dim3 grid((a.M + 63) / 64, a.N / 128);
-      hipLaunchKernelGGL((k_igemm<64, 128, 2, 2>), grid, dim3(256), 0, s, a);
-    }
-  } else if (a.N % 64 == 0) {
-    dim3 grid((a.M + 255) / 256, a.N / 64);
-    hipLaunchKernelGGL((k_igemm<256, 64, 4, 1>), grid, dim3(256), 0, s, a);
-  } else {
-    return hipErrorInvalidValue;
+    if (big >= 4 * cus) return go_igemm<128, 128, 2, 2, 16>(a, s);
+    return go_igemm<64, 128, 2, 2, 16>(a, s);  // small-M layers (bottleneck): twice the workgroups
   }
-  return hipGetLastError();
+  if (a.N % 64 == 0) return go_igemm<256, 64, 4, 1, 16>(a, s);
+  return hipErrorInvalidValue;
 }
 
 hipError_t launch_wgrad(const WgradArgs& a0, hipStream_t s) {
@@ -455,7 +493,7 @@ hipError_t launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   else return hipErrorInvalidValue;
   const int tiles = (a.Mo / bm) * (a.No / bn);
   // split the pixel reduction so that the grid has ~8 workgroups per CU
-  const int target = 8 * num_cus();
+  const int target = (g_tune_wgrad >= 2 ? g_tune_wgrad : 8) * num_cus();
   int splits = (target + tiles - 1) / tiles;
   int max_splits = (a.P + 255) / 256;
   if (splits > max_splits) splits = max_splits;
@@ -465,6 +503,11 @@ hipError_t launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   splits = (a.P + pps - 1) / pps;
   a.pix_per_split = pps;
   dim3 grid(a.Mo / bm, a.No / bn, splits);
+  if (g_tune_wgrad == 1 && a.Mo % 64 == 0 && a.No % 64 == 0) {  // force the small tile (A/B tests)
+    dim3 g2(a.Mo / 64, a.No / 64, splits);
+    hipLaunchKernelGGL((k_wgrad<64, 64, 2, 2>), g2, dim3(256), 0, s, a);
+    return hipGetLastError();
+  }
   if (bm == 128 && bn == 128)
     hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
   else if (bm == 128)

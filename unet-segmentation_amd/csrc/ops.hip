@@ -11,6 +11,7 @@
 using namespace unet;
 
 namespace unet {
+extern int g_tune_igemm, g_tune_wgrad;
 hipError_t launch_fill(float* p, size_t n, float v, hipStream_t s);
 hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream_t s);
 }  // namespace unet
@@ -309,6 +310,15 @@ int unet_sgd_momentum(float* p, const float* g, float* buf, size_t n, float lr, 
 
 int unet_iou_counts(const uint8_t* a, const uint8_t* b, size_t n, unsigned long long* out, unet_stream_t st) {
   OPCK(launch_iou(a, b, n, out, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_set_tuning(const char* key, int value) {
+  if (!key) return -EINVAL;
+  const std::string k(key);
+  if (k == "igemm_variant") g_tune_igemm = value;
+  else if (k == "wgrad_variant") g_tune_wgrad = value;
+  else return -EINVAL;
   return 0;
 }
 

@@ -49,6 +49,7 @@ SIGNATURES = {
     "unet_bn_train_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "unet_bn_train_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "unet_bn_ws_bytes": (_sz, [_i]),
+    "unet_set_tuning": (_i, [ctypes.c_char_p, _i]),
 }
 
 _lib = None
