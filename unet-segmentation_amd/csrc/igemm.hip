@@ -470,13 +470,21 @@ hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s) {
     default: break;
   }
   if (forced != hipErrorInvalidValue) return forced;
+  // Tile choice measured per U-Net layer shape on MI355X (tools/layer_report.py
+  // over a rocprofv3 trace per forced variant, profiles/r01_tuning.txt):
+  //  N = 64 (Co or Ci = 64): 128x64, 5 waves/SIMD            (+19 % on inc.c1 dgrad)
+  //  N >= 256, >= 1.5 x CUs 256x128 tiles: 8-wave 256x128    (+5..10 % on down1-3, up2)
+  //  N = 128 with large M: 128x128
+  //  otherwise (bottleneck, M <= ~20k pixels): 64x128 to fill the CUs
   const long long cus = num_cus();
   if (a.N % 128 == 0) {
-    const long long big = ((a.M + 127) / 128) * (long long)(a.N / 128);
-    if (big >= 4 * cus) return go_igemm<128, 128, 2, 2, 16>(a, s);
-    return go_igemm<64, 128, 2, 2, 16>(a, s);  // small-M layers (bottleneck): twice the workgroups
+    const long long t256 = ((a.M + 255) / 256) * (long long)(a.N / 128);
+    const long long t128 = ((a.M + 127) / 128) * (long long)(a.N / 128);
+    if (a.N >= 256 && t256 >= 3 * cus / 2) return go_igemm<256, 128, 4, 2, 16>(a, s);
+    if (t128 >= 4 * cus) return go_igemm<128, 128, 2, 2, 16>(a, s);
+    return go_igemm<64, 128, 2, 2, 16>(a, s);
   }
-  if (a.N % 64 == 0) return go_igemm<256, 64, 4, 1, 16>(a, s);
+  if (a.N % 64 == 0) return go_igemm<128, 64, 2, 2, 16>(a, s);
   return hipErrorInvalidValue;
 }
 
