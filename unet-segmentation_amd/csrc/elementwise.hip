@@ -99,53 +99,109 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict_
 }
 
 // inc.c0 weight gradient: dW[co][ci][ky][kx] = sum_p dY[p][co] * x[ci][p+(ky,kx)].
-// Grid-stride over (image, row, 64-pixel segment); per-thread register sums,
-// one fp32 atomic per weight per workgroup.
+// HBM-bound reduction over every output pixel (dY is 64 ch x 510^2 x N floats).
+// Work item = a strip of RB rows x 64 columns; thread = (4-channel group,
+// pixel slot): 16 lanes read one pixel's 64 channels as float4 (a wave moves
+// 1 KiB of contiguous dY per load), 8 loads in flight per thread; the x strip
+// is staged in LDS.  Per-thread register sums, one fp32 atomic per weight per
+// workgroup at the end.
 template <int CI>
 __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restrict__ x, int nimg, int h, int w,
                                                           Src dy, float* __restrict__ dw) {
+  constexpr int RB = 4, PX = 64, TW = PX + 2;
   const int ho = h - 2, wo = w - 2;
-  const int nseg = (wo + 63) / 64;
-  const long long items = (long long)nimg * ho * nseg;
-  __shared__ float tile[CI][3][66];
-  const int tid = threadIdx.x, c = tid & 63, q = tid >> 6;
-  float acc[CI * 9];
+  const int nseg = (wo + PX - 1) / PX, nstrip = (ho + RB - 1) / RB;
+  const long long items = (long long)nimg * nstrip * nseg;
+  __shared__ float tile[CI][RB + 2][TW];
+  const int tid = threadIdx.x, cg = tid & 15, slot = tid >> 4;  // 16 channel groups x 16 pixel slots
+  float acc[4][CI * 9];
 #pragma unroll
-  for (int k = 0; k < CI * 9; ++k) acc[k] = 0.f;
+  for (int c = 0; c < 4; ++c)
+#pragma unroll
+    for (int k = 0; k < CI * 9; ++k) acc[c][k] = 0.f;
   for (long long it = blockIdx.x; it < items; it += gridDim.x) {
     const int seg = (int)(it % nseg);
     const long long t2 = it / nseg;
-    const int row = (int)(t2 % ho), n = (int)(t2 / ho);
-    const int x0 = seg * 64;
+    const int strip = (int)(t2 % nstrip), n = (int)(t2 / nstrip);
+    const int x0 = seg * PX, r0 = strip * RB;
     __syncthreads();
-    for (int i = tid; i < CI * 3 * 66; i += 256) {
-      const int ci = i / 198, rem = i - ci * 198, r = rem / 66, cx = rem - r * 66;
-      const int gx = min(x0 + cx, w - 1);
-      tile[ci][r][cx] = x[((size_t)(n * CI + ci) * h + row + r) * w + gx];
+    for (int i = tid; i < CI * (RB + 2) * TW; i += 256) {
+      const int ci = i / ((RB + 2) * TW), rem = i - ci * (RB + 2) * TW, r = rem / TW, cx = rem - r * TW;
+      const int gx = min(x0 + cx, w - 1), gy = min(r0 + r, h - 1);
+      tile[ci][r][cx] = x[((size_t)(n * CI + ci) * h + gy) * w + gx];
     }
     __syncthreads();
-    for (int j = 0; j < 16; ++j) {
-      const int px = q + 4 * j;
-      const int gx = x0 + px;
-      if (gx >= wo) break;
-      const float g = dy.ptr[((size_t)(n * dy.H + row + dy.oy) * dy.W + gx + dy.ox) * dy.C + c];
+    // RB*PX = 256 pixels, 16 per slot, in two batches of 8 loads
 #pragma unroll
-      for (int ci = 0; ci < CI; ++ci)
+    for (int b = 0; b < 2; ++b) {
+      float4 g[8];
+      int pr[8], pc[8];
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+      for (int j = 0; j < 8; ++j) {
+        const int pix = slot + 16 * (8 * b + j);  // 0..255
+        pr[j] = pix / PX;
+        pc[j] = pix - pr[j] * PX;
+        const bool ok = (r0 + pr[j] < ho) && (x0 + pc[j] < wo);
+        const int yy = min(r0 + pr[j], ho - 1), xx = min(x0 + pc[j], wo - 1);
+        g[j] = *reinterpret_cast<const float4*>(
+            dy.ptr + ((size_t)(n * dy.H + yy + dy.oy) * dy.W + xx + dy.ox) * dy.C + cg * 4);
+        if (!ok) g[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) acc[(ci * 3 + ky) * 3 + kx] = fmaf(g, tile[ci][ky][px + kx], acc[(ci * 3 + ky) * 3 + kx]);
+      for (int j = 0; j < 8; ++j) {
+#pragma unroll
+        for (int ci = 0; ci < CI; ++ci)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              const float xv = tile[ci][pr[j] + ky][pc[j] + kx];
+              const int k = (ci * 3 + ky) * 3 + kx;
+              acc[0][k] = fmaf(g[j].x, xv, acc[0][k]);
+              acc[1][k] = fmaf(g[j].y, xv, acc[1][k]);
+              acc[2][k] = fmaf(g[j].z, xv, acc[2][k]);
+              acc[3][k] = fmaf(g[j].w, xv, acc[3][k]);
+            }
+      }
     }
   }
-  __shared__ float red[4][CI * 9][64];
+  // reduce the 16 pixel slots that share a channel group, one weight index at a
+  // time through a small LDS buffer, then write this workgroup's partial slab
+  // (no atomics: 2048 workgroups adding into the same 576 words serialise at
+  // the memory side; k_reduce_slabs sums the slabs)
+  __shared__ float red[16][65];
+  float* slab = dw + (size_t)blockIdx.x * CI * 9 * 64;
 #pragma unroll
-  for (int k = 0; k < CI * 9; ++k) red[q][k][c] = acc[k];
+  for (int k = 0; k < CI * 9; ++k) {
+    __syncthreads();
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[slot][cg * 4 + c] = acc[c][k];
+    __syncthreads();
+    if (tid < 64) {
+      float v = 0.f;
+#pragma unroll
+      for (int s2 = 0; s2 < 16; ++s2) v += red[s2][tid];
+      slab[(size_t)tid * CI * 9 + k] = v;
+    }
+  }
+}
+
+// out[i] += sum_{b in chunk} slabs[b][i]: block (word group of 64, chunk of
+// 64 slabs); 4 waves each sum 16 slabs of the same 64 words (256-B coalesced
+// rows), then one atomic per word per block (out zeroed by the launcher).
+__global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ slabs, int nslab, int n,
+                                                      float* __restrict__ out) {
+  const int w = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int b0 = blockIdx.y * 64;
+  const int b1 = min(nslab, b0 + 64);
+  float s = 0.f;
+  if (w < n)
+    for (int b = b0 + (threadIdx.x >> 6); b < b1; b += 4) s += slabs[(size_t)b * n + w];
+  __shared__ float red[4][64];
+  red[threadIdx.x >> 6][threadIdx.x & 63] = s;
   __syncthreads();
-  for (int i = tid; i < CI * 9 * 64; i += 256) {
-    const int k = i / 64, cc = i - k * 64;
-    const float v = red[0][k][cc] + red[1][k][cc] + red[2][k][cc] + red[3][k][cc];
-    atomicAdd(dw + (size_t)cc * CI * 9 + k, v);
-  }
+  if (threadIdx.x < 64 && w < n) atomicAdd(out + w, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                                        red[3][threadIdx.x]);
 }
 
 hipError_t launch_conv_first_fwd(const float* x, int n, int ci, int h, int w, const float* wt,
@@ -161,17 +217,23 @@ hipError_t launch_conv_first_fwd(const float* x, int n, int ci, int h, int w, co
   return hipGetLastError();
 }
 
+size_t conv_first_wgrad_ws_bytes(int ci) { return sizeof(float) * (size_t)kFirstWgradSlabs * ci * 9 * 64; }
+
 hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, const Src& dy, int co,
-                                   float* dw, hipStream_t s) {
+                                   float* dw, float* slabs, hipStream_t s) {
   if (co != 64 || ci < 1 || ci > 4) return hipErrorInvalidValue;
-  const long long items = (long long)n * (h - 2) * cdiv(w - 2, 64);
-  const int grid = (int)(items < 1024 ? items : 1024);
+  const long long items = (long long)n * cdiv(h - 2, 4) * cdiv(w - 2, 64);
+  const int grid = (int)(items < kFirstWgradSlabs ? items : kFirstWgradSlabs);
   switch (ci) {
-    case 1: hipLaunchKernelGGL(k_conv_first_wgrad<1>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, dw); break;
-    case 2: hipLaunchKernelGGL(k_conv_first_wgrad<2>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, dw); break;
-    case 3: hipLaunchKernelGGL(k_conv_first_wgrad<3>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, dw); break;
-    default: hipLaunchKernelGGL(k_conv_first_wgrad<4>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, dw); break;
+    case 1: hipLaunchKernelGGL(k_conv_first_wgrad<1>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
+    case 2: hipLaunchKernelGGL(k_conv_first_wgrad<2>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
+    case 3: hipLaunchKernelGGL(k_conv_first_wgrad<3>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
+    default: hipLaunchKernelGGL(k_conv_first_wgrad<4>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
   }
+  const int nw = ci * 9 * 64;
+  hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * nw, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(nw, 64), cdiv(grid, 64)), dim3(256), 0, s, slabs, grid, nw, dw);
   return hipGetLastError();
 }
 

@@ -72,7 +72,7 @@ struct unet_plan {
   ConvT T[4];
   Pool P[4];
   Skip S[4];
-  Buf stat_region, dwp_region, head_acc, wce_acc, dz_head;
+  Buf stat_region, dwp_region, head_acc, wce_acc, first_slabs;
   size_t ws_bytes = 0;
   // timing
   bool timing = false;
@@ -323,10 +323,9 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     dy.C = L.co;
     dy.oy = dy.ox = 2;
     if (l == 0) {
-      CK(hipMemsetAsync(P<float>(grd, L.gw), 0, sizeof(float) * L.co * L.ci * 9, s));
       Timer t(p, s, UNET_KC_STAGE1, 2.0 * M * L.co * L.ci * 9,
               4.0 * n * ((double)p->cin * p->h * p->w + (double)L.ho * L.wo * L.co));
-      CK(launch_conv_first_wgrad(x, n, p->cin, p->h, p->w, dy, L.co, P<float>(grd, L.gw), s));
+      CK(launch_conv_first_wgrad(x, n, p->cin, p->h, p->w, dy, L.co, P<float>(grd, L.gw), c.f(p->first_slabs), s));
       continue;
     }
     // weight gradient
@@ -577,6 +576,7 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
     p->T[k].colsum = al.take(sizeof(double) * kStatGroups * p->T[k].co);
   p->head_acc = al.take(sizeof(double) * (64 * 4 + 4));
   p->wce_acc = al.take(64);
+  p->first_slabs = al.take(conv_first_wgrad_ws_bytes(c_in));
   p->stat_region.off = stat_start;
   p->stat_region.bytes = al.top - stat_start;
   const size_t dwp_start = al.top;

@@ -88,8 +88,12 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s);
 hipError_t launch_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w,
                                  const float* wt_oihw, const float* bias, int co, float* y,
                                  double* stats, hipStream_t s);
+// Written per workgroup into `slabs` (conv_first_wgrad_ws_bytes) then reduced
+// into dw_oihw (overwritten, not accumulated).
+constexpr int kFirstWgradSlabs = 2048;
+size_t conv_first_wgrad_ws_bytes(int ci);
 hipError_t launch_conv_first_wgrad(const float* x_nchw, int n, int ci, int h, int w,
-                                   const Src& dy, int co, float* dw_oihw, hipStream_t s);
+                                   const Src& dy, int co, float* dw_oihw, float* slabs, hipStream_t s);
 
 // BN finalize (train): stats[G][C][2] -> mean, invstd, scale, shift; running update.
 hipError_t launch_bn_finalize(const double* stats, int c, double count, const float* gamma,

@@ -19,6 +19,7 @@ import ctypes
 import torch
 
 from . import _lib
+from .dist import GradBucketReducer
 from .plan import N_SEGMENTS, Plan
 
 
@@ -49,11 +50,11 @@ class FlatParams:
                 p.data = view
         self.grad_views = [self.grad[o:o + p.numel()].view_as(p) for p, o in zip(params, offs)]
 
-    def slice_for(self, first, count):
-        """Flat-buffer slice holding parameters [first, first+count)."""
+    def range_for(self, first, count):
+        """Flat-buffer element range holding parameters [first, first+count)."""
         a = self.offsets[first]
         b = self.offsets[first + count] if first + count < len(self.offsets) else self.numel
-        return self.grad[a:b]
+        return a, b
 
 
 class Trainer:
@@ -81,6 +82,9 @@ class Trainer:
         self.acc = torch.empty(8, dtype=torch.float64, device=dev)
         self.first_step = True
         self.lib = _lib.load()
+        buckets = [self.flat.range_for(*self.plan.segment_grads(s)) for s in range(N_SEGMENTS)]
+        self.reducer = GradBucketReducer(self.flat.grad, buckets, process_group)
+        self.reducer_whole = GradBucketReducer(self.flat.grad, [(0, self.flat.numel)], process_group)
 
     @property
     def out_hw(self):
@@ -98,19 +102,16 @@ class Trainer:
         return self.loss
 
     def backward_and_reduce(self, x):
-        works = []
         if self.pg is None or not self.overlap:
             self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, 0, N_SEGMENTS)
             if self.pg is not None:
-                works.append(torch.distributed.all_reduce(self.flat.grad, group=self.pg, async_op=True))
-        else:
-            for s in range(N_SEGMENTS):
-                self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, s, s + 1)
-                f, k = self.plan.segment_grads(s)
-                works.append(torch.distributed.all_reduce(self.flat.slice_for(f, k), group=self.pg,
-                                                          async_op=True))
-        for w in works:
-            w.wait()
+                self.reducer_whole.reduce_all()
+                self.reducer_whole.wait()
+            return
+        for s in range(N_SEGMENTS):
+            self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, s, s + 1)
+            self.reducer.reduce(s)  # bucket s is final: all-reduce it while segment s+1 computes
+        self.reducer.wait()
 
     def optimizer_step(self):
         fp = self.flat
