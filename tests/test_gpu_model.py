@@ -229,3 +229,29 @@ def test_sgd_trajectory_vs_reference_fixture():
         d = float(torch.linalg.norm(v.detach() - p0[k]))
         r = float(z[f"dnorm/{k}"])
         assert abs(d - r) <= 3e-2 * r, (k, d, r)
+
+
+def test_trainer_fast_path_matches_dropin_autograd_path():
+    """unet_amd.train.Trainer (flat buffers, fused SGD, segmented backward: the
+    bench path) == UNet + WeightedCrossEntropyLoss + torch.optim.SGD."""
+    from unet_amd import WeightedCrossEntropyLoss
+    from unet_amd.train import Trainer
+    params = O.hash_init(1, 2, seed=41, bn_random=True)
+    x, tgt, wmap = F.make_inputs(41, 2, 1, 204)
+    xd, td, wd = (torch.from_numpy(a).cuda() for a in (x, tgt, wmap))
+    a = make_model(params)
+    opt = torch.optim.SGD(a.parameters(), lr=1e-4, momentum=0.99)
+    crit = WeightedCrossEntropyLoss()
+    b = make_model(params)
+    tr = Trainer(b, 2, 204, 204, lr=1e-4, momentum=0.99)
+    for _ in range(3):
+        opt.zero_grad()
+        la = crit(a(xd), td, wd)
+        la.backward()
+        opt.step()
+        lb = tr.step(xd, td, wd)
+        assert abs(la.item() - lb.item()) <= 1e-5 * abs(la.item())
+    sa, sb = a.state_dict(), b.state_dict()
+    for k in sa:
+        va, vb = sa[k].double().cpu().numpy(), sb[k].double().cpu().numpy()
+        assert np.abs(va - vb).max() <= 1e-6 * max(1.0, np.abs(va).max()), k

@@ -1,0 +1,75 @@
+"""Overlap-tile inference (unet_amd.tiling): geometry and stitching on CPU,
+parity of the GPU tile farm against per-tile oracle eval forwards."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import unet_oracle as O
+
+
+def test_margin_rule_matches_predict1():
+    from unet_amd.tiling import TileGeometry, output_size
+    # scripts/predict1.py:45-46: margin = tile_in - tile_out = 188 for 512
+    assert 512 - output_size(512) == 188
+    g = TileGeometry(1024, 1024, 512)
+    assert (g.tile_out, g.margin, len(g)) == (324, 94, 16)
+    assert g.pads[0] == 94 and g.pads[2] == 94
+    # padded image exactly covers all input tiles
+    assert 1024 + g.pads[0] + g.pads[1] == (g.ny - 1) * g.tile_out + g.tile_in
+
+
+@pytest.mark.parametrize("hw,tile", [((1024, 1024), 512), ((700, 333), 512), ((100, 90), 220), ((37, 41), 204)])
+def test_tiles_stitch_back_to_the_image(hw, tile):
+    from unet_amd.tiling import TileGeometry, mirror_pad, extract_tiles, stitch
+    H, W = hw
+    img = torch.arange(H * W, dtype=torch.float32).reshape(1, H, W)
+    g = TileGeometry(H, W, tile)
+    padded = mirror_pad(img, g.pads)
+    np.testing.assert_array_equal(padded.numpy(), O.mirror_pad(img.numpy(), g.pads))
+    tiles = extract_tiles(padded, g, list(range(len(g))))
+    m, t = g.margin, g.tile_out
+    # an "identity U-Net": the valid output of a tile is its centre
+    res = {i: tiles[i][:, m:m + t, m:m + t] for i in range(len(g))}
+    np.testing.assert_array_equal(stitch(res, g, 1).numpy(), img.numpy())
+
+
+def test_rank_share_partitions_tiles():
+    from unet_amd.tiling import TileGeometry, rank_share
+    g = TileGeometry(1024, 1024, 512)
+    for world in (1, 2, 8):
+        got = sorted(i for r in range(world) for i in rank_share(g, r, world))
+        assert got == list(range(len(g)))
+
+
+@pytest.mark.gpu
+def test_tile_farm_vs_oracle():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from unet_amd import UNet
+    from unet_amd.tiling import TileFarm, TileGeometry, mask_from_logits
+    params = O.hash_init(1, 2, seed=31, bn_random=True)
+    rng = np.random.default_rng(0)
+    for k in params:  # plausible running statistics
+        if k.endswith("running_mean"):
+            params[k] = (0.2 * rng.standard_normal(params[k].shape)).astype(np.float32)
+        if k.endswith("running_var"):
+            params[k] = (0.5 + rng.uniform(size=params[k].shape)).astype(np.float32)
+    m = UNet(1, 2)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    H, W, tile = 100, 90, 220
+    img = (rng.uniform(size=(H, W)) * 2 - 1).astype(np.float32)
+    farm = TileFarm(m, devices=[0], tile_in=tile, batch=4)
+    logits = farm.predict(torch.from_numpy(img)).numpy()
+    # oracle: mirror pad, eval forward per tile, stitch
+    g = TileGeometry(H, W, tile)
+    padded = O.mirror_pad(img[None], g.pads)
+    net = O.UNetOracle(params)
+    ref = np.zeros((2, g.ny * g.tile_out, g.nx * g.tile_out))
+    for (y, x) in g.origins:
+        lg, _, _ = net.forward(padded[None, :, y:y + tile, x:x + tile], train=False)
+        ref[:, y:y + g.tile_out, x:x + g.tile_out] = lg[0]
+    ref = ref[:, :H, :W]
+    assert np.abs(logits - ref).max() <= 1e-3
+    mk = mask_from_logits(torch.from_numpy(logits)).numpy()
+    sure = np.abs(ref[1] - ref[0]) > 1e-3
+    np.testing.assert_array_equal(mk[sure], ((ref[1] > ref[0]) * 255).astype(np.uint8)[sure])
