@@ -242,17 +242,38 @@ hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, 
 // variance, invstd; consumer transform scale = gamma*invstd, shift = beta -
 // mean*scale; running stats: momentum 0.1, unbiased variance; nbt += 1.
 // ---------------------------------------------------------------------------
-__global__ void k_bn_finalize(const double* __restrict__ st, int C, double count, const float* gamma,
-                              const float* beta, float* rmean, float* rvar, int64_t* nbt, float* mean,
-                              float* invstd, float* scale, float* shift, float mom, float eps) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c == 0 && nbt) *nbt += 1;
-  if (c >= C) return;
-  double s1 = 0, s2 = 0;
-  for (int g = 0; g < kStatGroups; ++g) {
-    s1 += st[((size_t)g * C + c) * 2 + 0];
-    s2 += st[((size_t)g * C + c) * 2 + 1];
+// Sum the kStatGroups group partials of (a, b) for 64 channels per block: the
+// 4 waves each take a quarter of the groups, then combine through LDS.
+// Returns true for the 64 threads that hold a channel's totals.
+__device__ __forceinline__ bool group_sum(const double* __restrict__ st, int C, double& s1, double& s2, int& c) {
+  __shared__ double red[4][64][2];
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  c = blockIdx.x * 64 + lane;
+  double a = 0, b = 0;
+  if (c < C) {
+#pragma unroll 4
+    for (int g = q; g < kStatGroups; g += 4) {
+      a += st[((size_t)g * C + c) * 2 + 0];
+      b += st[((size_t)g * C + c) * 2 + 1];
+    }
   }
+  red[q][lane][0] = a;
+  red[q][lane][1] = b;
+  __syncthreads();
+  if (q != 0 || c >= C) return false;
+  s1 = red[0][lane][0] + red[1][lane][0] + red[2][lane][0] + red[3][lane][0];
+  s2 = red[0][lane][1] + red[1][lane][1] + red[2][lane][1] + red[3][lane][1];
+  return true;
+}
+
+__global__ __launch_bounds__(256) void k_bn_finalize(const double* __restrict__ st, int C, double count,
+                                                     const float* gamma, const float* beta, float* rmean,
+                                                     float* rvar, int64_t* nbt, float* mean, float* invstd,
+                                                     float* scale, float* shift, float mom, float eps) {
+  if (blockIdx.x == 0 && threadIdx.x == 0 && nbt) *nbt += 1;
+  double s1, s2;
+  int c;
+  if (!group_sum(st, C, s1, s2, c)) return;
   const double mu = s1 / count;
   double var = s2 / count - mu * mu;
   if (var < 0) var = 0;
@@ -282,16 +303,12 @@ __global__ void k_bn_eval_prepare(int C, const float* gamma, const float* beta, 
 //      = k0*dz' + k1*(y - mean) + k2,  k0 = g*is, k1 = -g*is^2*B2/M, k2 = -g*is*B1/M.
 // The conv bias that precedes the BN gets sum_p dY = k0*B1 + k2*M (+ k1*0),
 // which is zero up to rounding (BN-cancelled biases).
-__global__ void k_bnb_finalize(const double* __restrict__ st, int C, double M, const float* gamma,
-                               const float* mean, const float* invstd, float* dgamma, float* dbeta,
-                               float* dbias, float* coef) {
-  const int c = blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= C) return;
-  double b1 = 0, b2 = 0;
-  for (int g = 0; g < kStatGroups; ++g) {
-    b1 += st[((size_t)g * C + c) * 2 + 0];
-    b2 += st[((size_t)g * C + c) * 2 + 1];
-  }
+__global__ __launch_bounds__(256) void k_bnb_finalize(const double* __restrict__ st, int C, double M,
+                                                      const float* gamma, const float* mean, const float* invstd,
+                                                      float* dgamma, float* dbeta, float* dbias, float* coef) {
+  double b1, b2;
+  int c;
+  if (!group_sum(st, C, b1, b2, c)) return;
   const double gi = (double)gamma[c] * (double)invstd[c];
   const double k0 = gi, k1 = -gi * (double)invstd[c] * b2 / M, k2 = -gi * b1 / M;
   if (dgamma) dgamma[c] = (float)b2;
@@ -337,7 +354,7 @@ __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restric
 hipError_t launch_bn_finalize(const double* stats, int c, double count, const float* gamma, const float* beta,
                               float* rmean, float* rvar, int64_t* nbt, float* mean, float* invstd, float* scale,
                               float* shift, float momentum, float eps, hipStream_t s) {
-  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(c, 256)), dim3(256), 0, s, stats, c, count, gamma, beta, rmean, rvar,
+  hipLaunchKernelGGL(k_bn_finalize, dim3(cdiv(c, 64)), dim3(256), 0, s, stats, c, count, gamma, beta, rmean, rvar,
                      nbt, mean, invstd, scale, shift, momentum, eps);
   return hipGetLastError();
 }
@@ -350,7 +367,7 @@ hipError_t launch_bn_eval_prepare(int c, const float* gamma, const float* beta, 
 hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const float* gamma, const float* mean,
                                const float* invstd, float* dgamma, float* dbeta, float* dbias, float* coef,
                                hipStream_t s) {
-  hipLaunchKernelGGL(k_bnb_finalize, dim3(cdiv(c, 256)), dim3(256), 0, s, bstats, c, count, gamma, mean, invstd,
+  hipLaunchKernelGGL(k_bnb_finalize, dim3(cdiv(c, 64)), dim3(256), 0, s, bstats, c, count, gamma, mean, invstd,
                      dgamma, dbeta, dbias, coef);
   return hipGetLastError();
 }
@@ -778,16 +795,23 @@ hipError_t launch_scale_by_dev(float* x, size_t n, const float* g, hipStream_t s
 //   convT fwd  B[ab*Co+co][ci] = W[ci][co][ab]
 //   convT dgrad B[ci][ab*Co+co] = W[ci][co][ab]
 // ---------------------------------------------------------------------------
-__global__ void k_permute_last2(const float* __restrict__ in, int A, int B, int C, float* __restrict__ out) {
-  const long long total = (long long)A * B * C;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    // i indexes out[a][c][b]
-    const int b = (int)(i % B);
-    const long long t = i / B;
-    const int c = (int)(t % C);
-    const long long a = t / C;
-    out[i] = in[(a * B + b) * C + c];
+// out[a][c][b] = in[a][b][c], 32x32 (b, c) tiles through LDS so both the reads
+// (rows of c) and the writes (rows of b) are contiguous.  grid = (ceil(C/32),
+// ceil(B/32), A).
+__global__ __launch_bounds__(256) void k_permute_last2(const float* __restrict__ in, int A, int B, int C,
+                                                       float* __restrict__ out) {
+  __shared__ float tile[32][33];
+  const int c0 = blockIdx.x * 32, b0 = blockIdx.y * 32;
+  const size_t a = blockIdx.z;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  for (int k = ty; k < 32; k += 8) {
+    const int b = b0 + k, c = c0 + tx;
+    if (b < B && c < C) tile[k][tx] = in[(a * B + b) * C + c];
+  }
+  __syncthreads();
+  for (int k = ty; k < 32; k += 8) {
+    const int c = c0 + k, b = b0 + tx;
+    if (b < B && c < C) out[(a * C + c) * B + b] = tile[tx][k];
   }
 }
 
@@ -814,9 +838,41 @@ __global__ void k_transpose_taps(const float* __restrict__ in, int R, int T, int
   }
 }
 
+// Small inner dim C (taps, packing OIHW -> [co][tap][ci]): thread per (a, b)
+// reads its C contiguous words, lanes write consecutive b (coalesced).
+__global__ void k_permute_small_c(const float* __restrict__ in, long long AB, int B, int C, float* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < AB; i += (long long)gridDim.x * blockDim.x) {
+    const long long a = i / B;
+    const int b = (int)(i - a * B);
+    const float* src = in + i * C;
+    float* dst = out + a * (long long)C * B + b;
+    for (int c = 0; c < C; ++c) dst[(long long)c * B] = src[c];
+  }
+}
+// Small middle dim B (taps, unpacking [co][tap][ci] -> OIHW): thread per (a, c)
+// reads lanes-consecutive c for every b, writes its B contiguous words.
+__global__ void k_permute_small_b(const float* __restrict__ in, long long AC, int B, int C, float* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < AC; i += (long long)gridDim.x * blockDim.x) {
+    const long long a = i / C;
+    const int c = (int)(i - a * C);
+    const float* src = in + a * (long long)B * C + c;
+    float* dst = out + i * B;
+    for (int b = 0; b < B; ++b) dst[b] = src[(long long)b * C];
+  }
+}
+
 hipError_t launch_permute_last2(const float* in, int A, int B, int C, float* out, hipStream_t s) {
-  const long long total = (long long)A * B * C;
-  hipLaunchKernelGGL(k_permute_last2, dim3(grid_cap(total, 256, 8192)), dim3(256), 0, s, in, A, B, C, out);
+  if (A <= 0 || B <= 0 || C <= 0) return hipErrorInvalidValue;
+  if (C <= 16) {
+    const long long ab = (long long)A * B;
+    hipLaunchKernelGGL(k_permute_small_c, dim3(grid_cap(ab, 256, 8192)), dim3(256), 0, s, in, ab, B, C, out);
+  } else if (B <= 16) {
+    const long long ac = (long long)A * C;
+    hipLaunchKernelGGL(k_permute_small_b, dim3(grid_cap(ac, 256, 8192)), dim3(256), 0, s, in, ac, B, C, out);
+  } else {
+    if (A > 65535) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_permute_last2, dim3(cdiv(C, 32), cdiv(B, 32), A), dim3(256), 0, s, in, A, B, C, out);
+  }
   return hipGetLastError();
 }
 

@@ -194,7 +194,10 @@ Gather input_gather(const Ctx& c, int l) {
 int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, char* ws, int train, hipStream_t s) {
   Ctx c{p, ws, s};
   const int n = p->n;
-  CK(hipMemsetAsync(ws + p->stat_region.off, 0, p->stat_region.bytes, s));
+  // One memset for every accumulator of this forward AND of the backward that
+  // follows it (BN stats, BN-bwd stats, convT bias sums, head/loss sums, and in
+  // train mode the packed weight-gradient region, laid out right after).
+  CK(hipMemsetAsync(ws + p->stat_region.off, 0, p->stat_region.bytes + (train ? p->dwp_region.bytes : 0), s));
   // ---- repack weights (per call: the optimizer moves them every step) ----
   {
     Timer t(p, s, UNET_KC_ELEMWISE, 0, 0);
@@ -296,10 +299,8 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
   const int n = p->n;
   auto in_seg = [&](int sg) { return sg >= seg_b && sg < seg_e; };
   if (seg_b == 0) {
-    // bstats live in the stat region next to the forward stats: clear only them
-    for (int l = 0; l < 18; ++l) CK(hipMemsetAsync(c.d(p->L[l].bstats), 0, p->L[l].bstats.bytes, s));
-    for (int k = 0; k < 4; ++k) CK(hipMemsetAsync(c.d(p->T[k].colsum), 0, sizeof(double) * kStatGroups * p->T[k].co, s));
-    CK(hipMemsetAsync(ws + p->dwp_region.off, 0, p->dwp_region.bytes, s));
+    // accumulators (bstats, colsums, packed weight grads) were zeroed by the
+    // train-mode forward that filled this workspace
     Conv& L = p->L[17];
     Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * L.ho * L.wo * (2 * L.co + p->ncls));
     CK(launch_head_bwd(src_of(c, L, true), dlogits, n, L.ho, L.wo, L.co, P<float>(prm, 134), p->ncls, c.f(L.y),

@@ -91,6 +91,17 @@ class _Runner:
         self.plans = {}
         self.lock = threading.Lock()
 
+    # plans hold a native handle and a lock: copies (deepcopy, pickling of the
+    # module) start with an empty cache
+    def __deepcopy__(self, memo):
+        return _Runner()
+
+    def __getstate__(self):
+        return {}
+
+    def __setstate__(self, state):
+        self.__init__()
+
     def plan(self, n, c, h, w, k):
         key = (n, c, h, w, k)
         with self.lock:
