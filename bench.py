@@ -83,6 +83,17 @@ def cpu_baseline(seconds_hint=20.0):
                       f"restatement in oracle/, {dt:.1f} s"}
 
 
+def pmc_traffic(args):
+    """HBM bytes per launch per kernel family, from the committed PMC passes of
+    this same command (tools/pmc_report.py --json); counters cannot be read in
+    the timed run itself (separate rocprofv3 --pmc passes)."""
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
+    if args.size != 512 or args.batch != 8 or not os.path.exists(path):
+        return {}
+    fams = json.load(open(path))["families"]
+    return {k: int(v["bytes_per_launch"]) for k, v in fams.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -148,6 +159,7 @@ def main():
     tim = trainer.plan.timing()
 
     if rank == 0:
+        pmc = pmc_traffic(args)
         imgs = world * args.batch * args.steps
         value = imgs / elapsed
         conv = [tim[k] for k in ("conv_fwd", "conv_dgrad", "conv_wgrad")]
@@ -180,12 +192,14 @@ def main():
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv family (k_igemm fwd/dgrad + k_wgrad)",
                          "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc.get("conv"),
+                         "traffic_unit": "HBM bytes/launch (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, "
+                                         "profiles/pmc_traffic.json)",
                          "flops_per_step": conv_fl, "launches_per_step": launches,
                          "avg_launch_ms": round(conv_ms / max(launches, 1), 4)},
             "stage1": {"bound": "hbm", "ms": round(st[0], 3),
                        "achieved_gbs": round(st[2] / (st[0] * 1e-3) / 1e9, 1) if st[0] > 0 else None,
-                       "peak_gbs": HBM_PEAK_GBS},
+                       "peak_gbs": HBM_PEAK_GBS, "traffic": pmc.get("stage1")},
             "kernels": kernels,
             "final_loss": round(final_loss, 5),
         }
