@@ -103,6 +103,7 @@ def main():
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--tuning-report", default=None, help="write the GEMM autotuner's choices to this file")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -203,6 +204,10 @@ def main():
             "kernels": kernels,
             "final_loss": round(final_loss, 5),
         }
+        if args.tuning_report:
+            from unet_amd import _lib as _ulib
+            with open(args.tuning_report, "w") as f:
+                f.write(_ulib.tuning_report())
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))

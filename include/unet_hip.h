@@ -122,10 +122,22 @@ int unet_iou_counts(const uint8_t* pred, const uint8_t* gt, size_t n, unsigned l
 int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int w,
                           unet_stream_t stream);
 
-/* Tuning hook for A/B measurements: "igemm_variant" (-1 = heuristic, 1..9 =
- * forced tile shape) and "wgrad_variant" (-1 = heuristic, 1 = 64x64 tile,
- * >=2 = workgroups per CU for the pixel split).  Process-global. */
+/* Tuning hooks, process-global:
+ *  "autotune"      1 (default, or env UNET_AUTOTUNE) = the plan times the
+ *                  applicable GEMM variants (tile shape, split-K, wgrad pixel
+ *                  split) the first time it meets a GEMM shape and caches the
+ *                  fastest per shape; 0 = built-in heuristic only.
+ *  "igemm_variant" heuristic override for A/B measurements (-1 = off, 1..9 =
+ *                  forced tile shape); "wgrad_variant" (-1 = off, 1 = 64x64
+ *                  tile, >=2 = workgroups per CU for the pixel split);
+ *  "force_split"   k > 1: every plan igemm runs split-K k (tests), 0 = off. */
 int unet_set_tuning(const char* key, int value);
+/* Text report of the tuned GEMM choices (one line per shape: key, heuristic
+ * time, chosen variant and time).  Copies up to len-1 bytes + NUL into buf
+ * (buf may be NULL); returns the full report size including the NUL. */
+size_t unet_tuning_report(char* buf, size_t len);
+/* Forget every tuned choice (the next plan run re-tunes). */
+int unet_tuning_reset(void);
 
 /* ------------------------------------------------------------------------
  * Per-op entry points (used by the op-level parity tests and by tools).

@@ -86,7 +86,7 @@ def _worker(rank, world, port, q):
 
 @pytest.mark.timeout(600)
 def test_dp_allreduce_matches_shard_average():
-    ctx = mp.get_context("fork")
+    ctx = mp.get_context("spawn")  # fork would inherit the parent's OpenMP/BLAS pools (deadlock)
     q = ctx.Queue()
     port = _free_port()
     procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]

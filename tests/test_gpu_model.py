@@ -4,8 +4,9 @@ fixtures produced by the reference itself (tests/golden/make_golden.py).
 
 Tolerances (from the measured fp32 noise floor):
   logits <= 1e-3 abs; loss <= 1e-4 rel; argmax masks exact where the oracle
-  margin |l1-l0| > 1e-3; parameter grads rel-L2 <= 1e-2 per tensor except the
-  22 BN-cancelled biases (abs <= 1e-3 * max|grad of their weight|).
+  margin |l1-l0| > 1e-3; parameter grads rel-L2 <= max(1e-2, 2 x the fp32
+  oracle's own rel-L2 error vs fp64) per tensor, except the 22 BN-cancelled
+  biases (abs <= 1e-3 * max|grad of their weight|).
 """
 import os
 
@@ -64,6 +65,29 @@ def check_grads(gpu, ref, ref32=None, tol=1e-2):
         worst = max(worst, e / max(tol, floor))
         assert e <= max(tol, floor), (name, e, floor)
     return worst
+
+
+@pytest.fixture
+def gemm_mode(request):
+    """Select how the plan resolves its GEMM variants, restore autotuning after."""
+    from unet_amd import _lib
+    lib = _lib.load()
+    mode = getattr(request, "param", "autotune")
+    lib.unet_tuning_reset()
+    if mode == "heuristic":
+        lib.unet_set_tuning(b"autotune", 0)
+    elif mode.startswith("split"):
+        lib.unet_set_tuning(b"force_split", int(mode[5:]))
+    yield mode
+    lib.unet_set_tuning(b"autotune", 1)
+    lib.unet_set_tuning(b"force_split", 0)
+    lib.unet_tuning_reset()
+
+
+@pytest.mark.parametrize("gemm_mode", ["heuristic", "split3", "split8"], indirect=True)
+def test_train_step_gemm_variants_vs_oracle(gemm_mode):
+    """Built-in tiles and split-K (k_splitk_epi epilogue) against the oracle."""
+    test_train_step_vs_oracle(2, 188, 21)
 
 
 @pytest.mark.parametrize("n,h,seed", [(2, 188, 11), (2, 204, 12), (1, 220, 13)])

@@ -93,9 +93,24 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
 #pragma unroll
   for (int q = 0; q < BV; ++q) bptr[q] = args.b + (size_t)(n0 + row0 + RPP * q) * K + col4 * 4;
 
+  // K range of this workgroup (split-K slices chunks over blockIdx.z)
+  const int nk_all = K / BK;
+  int kc0 = 0, kc1 = nk_all;
+  if (args.ksplit > 1) {
+    const int per = (nk_all + args.ksplit - 1) / args.ksplit;
+    kc0 = blockIdx.z * per;
+    kc1 = min(nk_all, kc0 + per);
+  }
   // K iterator (uniform): chunk -> (tap_y, tap_x, c0).  A chunk never straddles
   // a tap or the concat split (Cg and c_split are multiples of BK).
   int it_ty = 0, it_tx = 0, it_c = 0;
+  {
+    const int cpt = g.Cg / BK;
+    const int tap = kc0 / cpt;
+    it_c = (kc0 - tap * cpt) * BK;
+    it_ty = tap / g.taps_w;
+    it_tx = tap - it_ty * g.taps_w;
+  }
   float4 ra[AV], rb[BV], rsc, rsh;
   bool rtf = false;
   auto issue = [&](int k0) {
@@ -140,13 +155,14 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int h = lane >> 5, li = lane & 31;
-  const int nk = K / BK;
-  issue(0);
-  commit(0);
-  __syncthreads();
-  for (int kc = 0; kc < nk; ++kc) {
-    const int cur = kc & 1;
-    const bool more = kc + 1 < nk;
+  if (kc0 < kc1) {
+    issue(kc0 * BK);
+    commit(0);
+    __syncthreads();
+  }
+  for (int kc = kc0; kc < kc1; ++kc) {
+    const int cur = (kc - kc0) & 1;
+    const bool more = kc + 1 < kc1;
     if (more) issue((kc + 1) * BK);
     const float* As = lds + cur * (BM + BN) * LDK;
     const float* Bs = As + BM * LDK;
@@ -175,9 +191,25 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
     __syncthreads();
   }
 
+  const int N = args.N;
+  if (args.ksplit > 1) {  // raw partial tile; k_splitk_epi finishes
+    float* sl = args.slab + (size_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * TN * 32 + j * 32 + li;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (m < M) sl[(size_t)m * N + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+
   // ------------------------------ epilogue ---------------------------------
   const Epilogue& e = args.e;
-  const int N = args.N;
   float s1[TN], s2[TN], t1[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; t1[j] = 0.f; }
@@ -264,6 +296,108 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
     } else if (e.colsum1) {
       const int n2 = N - nsplit;
       atomicAdd(e.colsum1 + (size_t)grp * n2 + (col - nsplit), (double)c);
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// k_splitk_epi: out = sum_z slab[z] + the k_igemm epilogue (bias, pixel-shuffle
+// or cropped destination, ReLU-mask + BN-bwd stats, BN stats, concat colsum).
+// 256 threads = 16 column quads x 16 row lanes over a 128-row x 64-column
+// block; every Dst channel count, n_split and shuffle_co is a multiple of 4, so
+// a column quad maps to 4 contiguous destination floats.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_splitk_epi(const IgemmArgs args) {
+  const int tid = threadIdx.x, cq = tid & 15, rl = tid >> 4;
+  const int col = blockIdx.y * 64 + cq * 4;
+  const int mbeg = blockIdx.x * 128, mend = min(args.M, mbeg + 128);
+  const Epilogue& e = args.e;
+  const Gather& g = args.a;
+  const int M = args.M, N = args.N, HWg = g.Hg * g.Wg;
+  const bool second = col >= e.n_split;
+  const Dst& d = second ? e.d[1] : e.d[0];
+  const int dcol = second ? col - e.n_split : col;
+  float4 bias = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (e.bias) bias = ld4(e.bias + (e.shuffle_co ? col % e.shuffle_co : col));
+  const bool bwd_mask = (e.yref != nullptr) && !second;
+  float4 bsc = bias, bsh = bias, bmu = bias, bis = bias;
+  if (bwd_mask) {
+    bsc = ld4(e.bn_scale + col);
+    bsh = ld4(e.bn_shift + col);
+    bmu = ld4(e.bn_mean + col);
+    bis = ld4(e.bn_invstd + col);
+  }
+  const bool linear = !e.shuffle_co && d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int m = mbeg + rl; m < mend; m += 16) {
+    float4 v = bias;
+    for (int z = 0; z < args.ksplit; ++z) {
+      const float4 p = ld4(args.slab + ((size_t)z * M + m) * N + col);
+      v.x += p.x;
+      v.y += p.y;
+      v.z += p.z;
+      v.w += p.w;
+    }
+    size_t idx;
+    if (linear) {
+      idx = (size_t)m * d.C + dcol;
+    } else {
+      const int n = m / HWg, rr = m - n * HWg;
+      const int y = rr / g.Wg, x = rr - y * g.Wg;
+      if (e.shuffle_co) {
+        const int ab = dcol / e.shuffle_co, co = dcol - ab * e.shuffle_co;
+        idx = ((size_t)(n * d.H + 2 * y + (ab >> 1) + d.oy) * d.W + 2 * x + (ab & 1) + d.ox) * d.C + co;
+      } else {
+        idx = ((size_t)(n * d.H + y + d.oy) * d.W + x + d.ox) * d.C + dcol;
+      }
+    }
+    float vv[4] = {v.x, v.y, v.z, v.w};
+    if (bwd_mask) {
+      const float4 y4 = ld4(e.yref + idx);
+      const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float sc = getc(bsc, q), sh = getc(bsh, q), mu = getc(bmu, q), is = getc(bis, q);
+        vv[q] = (fmaf(yv[q], sc, sh) > 0.f) ? vv[q] : 0.f;
+        s1[q] += vv[q];
+        s2[q] += vv[q] * ((yv[q] - mu) * is);
+      }
+    } else if (e.stats || (second && e.colsum1)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        s1[q] += vv[q];
+        s2[q] += vv[q] * vv[q];
+      }
+    }
+    st4(d.ptr + idx, make_float4(vv[0], vv[1], vv[2], vv[3]));
+  }
+  const bool want = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
+  if (!want) return;
+  __shared__ float red[2][16][65];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    red[0][rl][cq * 4 + q] = s1[q];
+    red[1][rl][cq * 4 + q] = s2[q];
+  }
+  __syncthreads();
+  if (tid < 64) {
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      a += red[0][r][tid];
+      b += red[1][r][tid];
+    }
+    const int c = blockIdx.y * 64 + tid;
+    const int grp = blockIdx.x % kStatGroups;
+    const int nsplit = min(e.n_split, N);
+    if (c < nsplit) {
+      double* st = e.yref ? e.bstats : e.stats;
+      if (st) {
+        atomicAdd(st + ((size_t)grp * nsplit + c) * 2 + 0, (double)a);
+        atomicAdd(st + ((size_t)grp * nsplit + c) * 2 + 1, (double)b);
+      }
+    } else if (e.colsum1) {
+      atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (c - nsplit), (double)a);
     }
   }
 }
@@ -426,7 +560,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
 // launchers
 // ---------------------------------------------------------------------------
 static int g_num_cus = 0;
-static int num_cus() {
+int num_cus() {
   if (g_num_cus == 0) {
     int dev = 0, n = 0;
     if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) ==
@@ -446,62 +580,143 @@ static int env_int(const char* name, int dflt) {
 int g_tune_igemm = env_int("UNET_IGEMM_VARIANT", -1);
 int g_tune_wgrad = env_int("UNET_WGRAD_VARIANT", -1);
 
+// igemm tile table: id -> (BM, BN, waves M x N, BK), resident workgroups per CU
+// (min of the LDS and VGPR limits of the built kernels).
+struct TileInfo {
+  int bm, bn, bk, slots;
+};
+static TileInfo tile_info(int id) {
+  switch (id) {
+    case 1: return {128, 128, 16, 3};
+    case 2: return {64, 128, 16, 4};
+    case 3: return {128, 128, 32, 2};
+    case 4: return {256, 128, 16, 2};
+    case 6: return {256, 64, 16, 2};
+    case 7: return {256, 64, 32, 1};
+    case 8: return {128, 64, 16, 4};
+    case 9: return {64, 128, 32, 2};
+    default: return {0, 0, 0, 0};
+  }
+}
+
+bool igemm_tile_fits(const IgemmArgs& a, int tile) {
+  const TileInfo t = tile_info(tile);
+  return t.bm > 0 && a.N % t.bn == 0 && a.K % t.bk == 0 && a.a.Cg % t.bk == 0 && a.a.c_split % t.bk == 0;
+}
+long long igemm_tile_count(const IgemmArgs& a, int tile) {
+  const TileInfo t = tile_info(tile);
+  if (t.bm == 0) return 0;
+  return (long long)((a.M + t.bm - 1) / t.bm) * (a.N / t.bn);
+}
+int igemm_tile_slots(int tile) { return tile_info(tile).slots; }
+size_t igemm_slab_bytes(const IgemmArgs& a, int ksplit) {
+  return ksplit > 1 ? (size_t)ksplit * a.M * a.N * sizeof(float) : 0;
+}
+
 template <int BM, int BN, int WM, int WN, int BK>
 static hipError_t go_igemm(const IgemmArgs& a, hipStream_t s) {
   if (a.N % BN != 0 || a.K % BK != 0 || a.a.Cg % BK != 0 || a.a.c_split % BK != 0) return hipErrorInvalidValue;
-  dim3 grid((a.M + BM - 1) / BM, a.N / BN);
+  dim3 grid((a.M + BM - 1) / BM, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
   hipLaunchKernelGGL((k_igemm<BM, BN, WM, WN, BK>), grid, dim3(WM * WN * 64), 0, s, a);
   return hipGetLastError();
 }
 
-hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s) {
-  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || (a.K % 16) != 0 || (a.a.Cg % 16) != 0 || (a.a.c_split % 16) != 0)
-    return hipErrorInvalidValue;
-  hipError_t forced = hipErrorInvalidValue;  // a forced variant that does not fit falls back
-  switch (g_tune_igemm) {
-    case 1: forced = go_igemm<128, 128, 2, 2, 16>(a, s); break;
-    case 2: forced = go_igemm<64, 128, 2, 2, 16>(a, s); break;
-    case 3: forced = go_igemm<128, 128, 2, 2, 32>(a, s); break;
-    case 4: forced = go_igemm<256, 128, 4, 2, 16>(a, s); break;
-    case 6: forced = go_igemm<256, 64, 4, 1, 16>(a, s); break;
-    case 7: forced = go_igemm<256, 64, 4, 1, 32>(a, s); break;
-    case 8: forced = go_igemm<128, 64, 2, 2, 16>(a, s); break;
-    case 9: forced = go_igemm<64, 128, 2, 2, 32>(a, s); break;
-    default: break;
+static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
+  switch (tile) {
+    case 1: return go_igemm<128, 128, 2, 2, 16>(a, s);
+    case 2: return go_igemm<64, 128, 2, 2, 16>(a, s);
+    case 3: return go_igemm<128, 128, 2, 2, 32>(a, s);
+    case 4: return go_igemm<256, 128, 4, 2, 16>(a, s);
+    case 6: return go_igemm<256, 64, 4, 1, 16>(a, s);
+    case 7: return go_igemm<256, 64, 4, 1, 32>(a, s);
+    case 8: return go_igemm<128, 64, 2, 2, 16>(a, s);
+    case 9: return go_igemm<64, 128, 2, 2, 32>(a, s);
+    default: return hipErrorInvalidValue;
   }
-  if (forced != hipErrorInvalidValue) return forced;
-  // Tile choice measured per U-Net layer shape on MI355X (tools/layer_report.py
-  // over a rocprofv3 trace per forced variant, profiles/r01_tuning.txt):
-  //  N = 64 (Co or Ci = 64): 128x64, 5 waves/SIMD            (+19 % on inc.c1 dgrad)
-  //  N >= 256, >= 1.5 x CUs 256x128 tiles: 8-wave 256x128    (+5..10 % on down1-3, up2)
-  //  N = 128 with large M: 128x128
-  //  otherwise (bottleneck, M <= ~20k pixels): 64x128 to fill the CUs
+}
+
+static bool igemm_args_ok(const IgemmArgs& a) {
+  return a.M > 0 && a.N > 0 && a.K > 0 && (a.K % 16) == 0 && (a.a.Cg % 16) == 0 && (a.a.c_split % 16) == 0;
+}
+
+// Built-in tile choice (used when no tuned choice exists), measured per U-Net
+// layer shape on MI355X (profiles/r01_tuning.txt):
+//  N = 64 (Co or Ci = 64): 128x64, 5 waves/SIMD            (+19 % on inc.c1 dgrad)
+//  N >= 256, >= 1.5 x CUs 256x128 tiles: 8-wave 256x128    (+5..10 % on down1-3, up2)
+//  N = 128 with large M: 128x128
+//  otherwise (bottleneck, M <= ~20k pixels): 64x128 to fill the CUs
+static int heuristic_tile(const IgemmArgs& a) {
+  if (g_tune_igemm > 0 && igemm_tile_fits(a, g_tune_igemm)) return g_tune_igemm;
   const long long cus = num_cus();
   if (a.N % 128 == 0) {
     const long long t256 = ((a.M + 255) / 256) * (long long)(a.N / 128);
     const long long t128 = ((a.M + 127) / 128) * (long long)(a.N / 128);
-    if (a.N >= 256 && t256 >= 3 * cus / 2) return go_igemm<256, 128, 4, 2, 16>(a, s);
-    if (t128 >= 4 * cus) return go_igemm<128, 128, 2, 2, 16>(a, s);
-    return go_igemm<64, 128, 2, 2, 16>(a, s);
+    if (a.N >= 256 && t256 >= 3 * cus / 2) return 4;
+    if (t128 >= 4 * cus) return 1;
+    return 2;
   }
-  if (a.N % 64 == 0) return go_igemm<128, 64, 2, 2, 16>(a, s);
-  return hipErrorInvalidValue;
+  if (a.N % 64 == 0) return 8;
+  return -1;
 }
 
-hipError_t launch_wgrad(const WgradArgs& a0, hipStream_t s) {
+hipError_t launch_igemm(const IgemmArgs& a0, hipStream_t s) {
+  if (!igemm_args_ok(a0)) return hipErrorInvalidValue;
+  IgemmArgs a = a0;
+  a.ksplit = 1;
+  return go_tile(a, s, heuristic_tile(a));
+}
+
+hipError_t launch_igemm_v(const IgemmArgs& a0, hipStream_t s, GemmChoice c) {
+  if (c.tile < 0) return launch_igemm(a0, s);
+  if (!igemm_args_ok(a0) || !igemm_tile_fits(a0, c.tile)) return hipErrorInvalidValue;
+  IgemmArgs a = a0;
+  const int nk = a.K / tile_info(c.tile).bk;
+  int ks = c.split < 1 ? 1 : (c.split > nk ? nk : c.split);
+  if (ks > 1) {  // no empty slice: ks = ceil(nk / ceil(nk / ks))
+    const int per = (nk + ks - 1) / ks;
+    ks = (nk + per - 1) / per;
+  }
+  a.ksplit = ks;
+  if (ks > 1 && (a.slab == nullptr || a.N % 64 != 0)) return hipErrorInvalidValue;
+  hipError_t e = go_tile(a, s, c.tile);
+  if (e != hipSuccess || ks == 1) return e;
+  dim3 grid((a.M + 127) / 128, a.N / 64);
+  hipLaunchKernelGGL(k_splitk_epi, grid, dim3(256), 0, s, a);
+  return hipGetLastError();
+}
+
+// wgrad tile table: id -> (BM, BN)
+static void wgrad_tile(int id, int& bm, int& bn) {
+  static const int t[5][2] = {{128, 128}, {128, 192}, {64, 192}, {64, 128}, {64, 64}};
+  bm = (id >= 0 && id < 5) ? t[id][0] : 0;
+  bn = (id >= 0 && id < 5) ? t[id][1] : 0;
+}
+bool wgrad_tile_fits(const WgradArgs& a, int tile) {
+  int bm, bn;
+  wgrad_tile(tile, bm, bn);
+  return bm > 0 && a.Mo % bm == 0 && a.No % bn == 0;
+}
+
+hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   WgradArgs a = a0;
   if (a.Mo % 64 != 0 || a.P <= 0 || a.gb.Cg % 4 != 0 || a.gb.c_split % 4 != 0 || a.ga.Cg % 4 != 0)
     return hipErrorInvalidValue;
+  int tile = c.tile;
+  if (tile < 0) {
+    if (g_tune_wgrad == 1) tile = 4;  // force the small tile (A/B tests)
+    else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 0;
+    else if (a.Mo % 128 == 0 && a.No % 192 == 0) tile = 1;
+    else if (a.No % 192 == 0) tile = 2;
+    else if (a.No % 128 == 0) tile = 3;
+    else tile = 4;
+  }
+  if (!wgrad_tile_fits(a, tile)) return hipErrorInvalidValue;
   int bm, bn;
-  if (a.Mo % 128 == 0 && a.No % 128 == 0) { bm = 128; bn = 128; }
-  else if (a.Mo % 128 == 0 && a.No % 192 == 0) { bm = 128; bn = 192; }
-  else if (a.No % 192 == 0) { bm = 64; bn = 192; }
-  else if (a.No % 128 == 0) { bm = 64; bn = 128; }
-  else if (a.No % 64 == 0) { bm = 64; bn = 64; }
-  else return hipErrorInvalidValue;
+  wgrad_tile(tile, bm, bn);
   const int tiles = (a.Mo / bm) * (a.No / bn);
-  // split the pixel reduction so that the grid has ~8 workgroups per CU
-  const int target = (g_tune_wgrad >= 2 ? g_tune_wgrad : 8) * num_cus();
+  // split the pixel reduction so that the grid has ~`per_cu` workgroups per CU
+  const int per_cu = c.tile >= 0 ? (c.split > 0 ? c.split : 8) : (g_tune_wgrad >= 2 ? g_tune_wgrad : 8);
+  const int target = per_cu * num_cus();
   int splits = (target + tiles - 1) / tiles;
   int max_splits = (a.P + 255) / 256;
   if (splits > max_splits) splits = max_splits;
@@ -511,22 +726,16 @@ hipError_t launch_wgrad(const WgradArgs& a0, hipStream_t s) {
   splits = (a.P + pps - 1) / pps;
   a.pix_per_split = pps;
   dim3 grid(a.Mo / bm, a.No / bn, splits);
-  if (g_tune_wgrad == 1 && a.Mo % 64 == 0 && a.No % 64 == 0) {  // force the small tile (A/B tests)
-    dim3 g2(a.Mo / 64, a.No / 64, splits);
-    hipLaunchKernelGGL((k_wgrad<64, 64, 2, 2>), g2, dim3(256), 0, s, a);
-    return hipGetLastError();
+  switch (tile) {
+    case 0: hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
+    case 1: hipLaunchKernelGGL((k_wgrad<128, 192, 2, 2>), grid, dim3(256), 0, s, a); break;
+    case 2: hipLaunchKernelGGL((k_wgrad<64, 192, 2, 2>), grid, dim3(256), 0, s, a); break;
+    case 3: hipLaunchKernelGGL((k_wgrad<64, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL((k_wgrad<64, 64, 2, 2>), grid, dim3(256), 0, s, a); break;
   }
-  if (bm == 128 && bn == 128)
-    hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a);
-  else if (bm == 128)
-    hipLaunchKernelGGL((k_wgrad<128, 192, 2, 2>), grid, dim3(256), 0, s, a);
-  else if (bn == 192)
-    hipLaunchKernelGGL((k_wgrad<64, 192, 2, 2>), grid, dim3(256), 0, s, a);
-  else if (bn == 128)
-    hipLaunchKernelGGL((k_wgrad<64, 128, 2, 2>), grid, dim3(256), 0, s, a);
-  else
-    hipLaunchKernelGGL((k_wgrad<64, 64, 2, 2>), grid, dim3(256), 0, s, a);
   return hipGetLastError();
 }
+
+hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad_v(a, s, GemmChoice{}); }
 
 }  // namespace unet

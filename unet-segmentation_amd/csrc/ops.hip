@@ -11,7 +11,7 @@
 using namespace unet;
 
 namespace unet {
-extern int g_tune_igemm, g_tune_wgrad;
+extern int g_tune_igemm, g_tune_wgrad, g_autotune, g_force_split;
 hipError_t launch_fill(float* p, size_t n, float v, hipStream_t s);
 hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream_t s);
 }  // namespace unet
@@ -318,6 +318,8 @@ int unet_set_tuning(const char* key, int value) {
   const std::string k(key);
   if (k == "igemm_variant") g_tune_igemm = value;
   else if (k == "wgrad_variant") g_tune_wgrad = value;
+  else if (k == "autotune") g_autotune = value;
+  else if (k == "force_split") g_force_split = value;
   else return -EINVAL;
   return 0;
 }

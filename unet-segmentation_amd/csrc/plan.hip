@@ -12,7 +12,11 @@
 // collects the next BN-bwd statistics.
 #include <cerrno>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
+#include <algorithm>
+#include <map>
+#include <mutex>
 #include <string>
 #include <vector>
 
@@ -20,6 +24,13 @@
 #include "unet_internal.h"
 
 using namespace unet;
+
+namespace unet {
+// unet_set_tuning("autotune", v) or UNET_AUTOTUNE (default on)
+int g_autotune = getenv("UNET_AUTOTUNE") ? atoi(getenv("UNET_AUTOTUNE")) : 1;
+// unet_set_tuning("force_split", k): every igemm site runs split-K k (tests)
+int g_force_split = 0;
+}  // namespace unet
 
 namespace {
 
@@ -73,6 +84,8 @@ struct unet_plan {
   Pool P[4];
   Skip S[4];
   Buf stat_region, dwp_region, head_acc, wce_acc, first_slabs;
+  Buf slab;          // split-K partial tiles (igemm sites the tuner splits)
+  Buf tune_scratch;  // atomic targets of the autotuner's trial launches
   size_t ws_bytes = 0;
   // timing
   bool timing = false;
@@ -133,6 +146,170 @@ struct Timer {
     }
   }
 };
+
+
+// ---------------- GEMM variant autotuner ------------------------------------
+// Every implicit-GEMM launch site is resolved to a (tile, split) variant by
+// timing the applicable candidates once, on the live operands, the first time
+// its GEMM shape is met (the way MIOpen's find step picks a conv solver).
+// Choices are cached process-wide per shape key, so plans of equal shapes (the
+// Trainer and a drop-in module, DP replicas in one process) run identical
+// kernels.  Trial launches redirect their atomic accumulators to scratch; their
+// plain stores are overwritten by the real launch that follows.
+std::mutex g_tune_mu;
+std::map<std::string, GemmChoice> g_tuned;
+std::map<std::string, std::string> g_tune_log;
+
+int env_autotune() { return unet::g_autotune; }
+
+constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
+
+std::string igemm_key(const IgemmArgs& a) {
+  char b[192];
+  const Epilogue& e = a.e;
+  const int epi = (e.shuffle_co ? 1 : 0) | (e.stats ? 2 : 0) | (e.yref ? 4 : 0) | (e.colsum1 ? 8 : 0) |
+                  (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0);
+  snprintf(b, sizeof b, "igemm M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d", a.M, a.N, a.K, a.a.Cg,
+           a.a.taps_h, a.a.taps_w, a.a.stride, a.a.Hg, a.a.Wg, epi);
+  return b;
+}
+
+std::string wgrad_key(const WgradArgs& a) {
+  char b[192];
+  snprintf(b, sizeof b, "wgrad Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d", a.Mo, a.No, a.P, a.gb.Cg,
+           a.gb.taps_h, a.gb.taps_w, a.gb.stride, a.gb.Hg, a.gb.Wg);
+  return b;
+}
+
+std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) {
+  std::vector<GemmChoice> v;
+  const long long cus = num_cus();
+  for (int t : {4, 1, 2, 8, 6, 3, 9, 7}) {
+    if (!igemm_tile_fits(a, t)) continue;
+    v.push_back({t, 1});
+    const long long cnt = igemm_tile_count(a, t);
+    const long long slots = (long long)igemm_tile_slots(t) * cus;
+    if (cnt >= 4 * slots || a.N % 64 != 0) continue;  // enough workgroup rounds already
+    for (int ks : {2, 3, 4, 6, 8}) {
+      if (igemm_slab_bytes(a, ks) > slab_bytes || a.K / ks < 256 || cnt * ks > 8 * slots) break;
+      v.push_back({t, ks});
+    }
+  }
+  return v;
+}
+
+std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
+  std::vector<GemmChoice> v;
+  for (int t = 0; t < 5; ++t) {
+    if (!wgrad_tile_fits(a, t)) continue;
+    for (int per_cu : {4, 8, 16}) v.push_back({t, per_cu});
+  }
+  return v;
+}
+
+// min over 2 timed runs after 1 warm-up; < 0 if the launch failed
+template <typename F>
+float time_launch(hipStream_t s, F&& launch) {
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess) return -1.f;
+  if (hipEventCreate(&e1) != hipSuccess) {
+    (void)hipEventDestroy(e0);
+    return -1.f;
+  }
+  float best = -1.f;
+  for (int r = 0; r < 3; ++r) {
+    (void)hipEventRecord(e0, s);
+    if (launch() != hipSuccess) {
+      (void)hipGetLastError();
+      best = -1.f;
+      break;
+    }
+    (void)hipEventRecord(e1, s);
+    if (hipEventSynchronize(e1) != hipSuccess) {
+      best = -1.f;
+      break;
+    }
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, e0, e1);
+    if (r > 0 && (best < 0.f || ms < best)) best = ms;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  return best;
+}
+
+bool capturing(hipStream_t s) {
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  return hipStreamIsCapturing(s, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+}
+
+GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
+  if (unet::g_force_split > 1) {
+    for (int t : {4, 1, 2, 8})
+      if (igemm_tile_fits(a, t) && igemm_slab_bytes(a, unet::g_force_split) <= c.p->slab.bytes)
+        return GemmChoice{t, unet::g_force_split};
+    return GemmChoice{};
+  }
+  if (!env_autotune() || capturing(c.s)) return GemmChoice{};
+  const std::string key = igemm_key(a);
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  auto it = g_tuned.find(key);
+  if (it != g_tuned.end()) return it->second;
+  IgemmArgs t = a;
+  double* scr = c.d(c.p->tune_scratch);
+  if (t.e.stats) t.e.stats = scr;
+  if (t.e.bstats) t.e.bstats = scr;
+  if (t.e.colsum1) t.e.colsum1 = scr;
+  const float th = time_launch(c.s, [&] { return launch_igemm(t, c.s); });
+  GemmChoice best{};
+  float tb = th;
+  std::string log = key + " | heuristic " + std::to_string(th * 1e3f) + " us";
+  for (const GemmChoice& g : igemm_candidates(a, c.p->slab.bytes)) {
+    const float tm = time_launch(c.s, [&] { return launch_igemm_v(t, c.s, g); });
+    if (tm > 0.f && (tb < 0.f || tm < tb)) {
+      tb = tm;
+      best = g;
+    }
+  }
+  log += " | best tile " + std::to_string(best.tile) + " split " + std::to_string(best.split) + " " +
+         std::to_string(tb * 1e3f) + " us";
+  g_tuned[key] = best;
+  g_tune_log[key] = log;
+  return best;
+}
+
+GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
+  if (!env_autotune() || capturing(c.s)) return GemmChoice{};
+  const std::string key = wgrad_key(a);
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  auto it = g_tuned.find(key);
+  if (it != g_tuned.end()) return it->second;
+  WgradArgs t = a;
+  t.out = c.f(c.p->tune_scratch);
+  const float th = time_launch(c.s, [&] { return launch_wgrad(t, c.s); });
+  GemmChoice best{};
+  float tb = th;
+  std::string log = key + " | heuristic " + std::to_string(th * 1e3f) + " us";
+  for (const GemmChoice& g : wgrad_candidates(a)) {
+    const float tm = time_launch(c.s, [&] { return launch_wgrad_v(t, c.s, g); });
+    if (tm > 0.f && (tb < 0.f || tm < tb)) {
+      tb = tm;
+      best = g;
+    }
+  }
+  log += " | best tile " + std::to_string(best.tile) + " per_cu " + std::to_string(best.split) + " " +
+         std::to_string(tb * 1e3f) + " us";
+  g_tuned[key] = best;
+  g_tune_log[key] = log;
+  return best;
+}
+
+hipError_t run_igemm(const Ctx& c, IgemmArgs a) {
+  a.slab = c.f(c.p->slab);
+  return launch_igemm_v(a, c.s, choose_igemm(c, a));
+}
+
+hipError_t run_wgrad(const Ctx& c, const WgradArgs& a) { return launch_wgrad_v(a, c.s, choose_wgrad(c, a)); }
 
 Src src_of(const Ctx& c, const Conv& L, bool transform) {
   Src s;
@@ -255,7 +432,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       a.e.shuffle_co = T.co;
       a.e.d[0] = Dst{c.f(T.u), 2 * T.h, 2 * T.w, T.co, 0, 0};
       Timer t(p, s, UNET_KC_CONV_FWD, 2.0 * a.M * a.N * a.K, 0);
-      CK(launch_igemm(a, s));
+      CK(run_igemm(c, a));
     }
     IgemmArgs a;
     a.a = input_gather(c, l);
@@ -268,7 +445,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
     a.e.stats = train ? c.d(L.stats) : nullptr;
     {
       Timer t(p, s, UNET_KC_CONV_FWD, conv_flops(L, n), 0);
-      CK(launch_igemm(a, s));
+      CK(run_igemm(c, a));
     }
     if (int r = finalize(l)) return r;
     if (l <= 7 && l % 2 == 1) {  // encoder output -> MaxPool2d(2)
@@ -344,7 +521,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       w.P = n * L.ho * L.wo;
       w.out = c.f(L.dwp);
       Timer t(p, s, UNET_KC_CONV_WGRAD, conv_flops(L, n), 0);
-      CK(launch_wgrad(w, s));
+      CK(run_wgrad(c, w));
     }
     CK(launch_permute_last2(c.f(L.dwp), L.co, 9, L.ci, P<float>(grd, L.gw), s));
     // input gradient
@@ -371,14 +548,14 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       a.e.bn_invstd = c.f(Q.invstd);
       a.e.bstats = c.d(Q.bstats);
       Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
-      CK(launch_igemm(a, s));
+      CK(run_igemm(c, a));
     } else if (l <= 8) {  // -> gradient of the pooled tensor, then pool backward
       const int k = l / 2 - 1;
       Pool& pl = p->P[k];
       a.e.d[0] = Dst{c.f(pl.dp), pl.h / 2, pl.w / 2, pl.c, 0, 0};
       {
         Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
-        CK(launch_igemm(a, s));
+        CK(run_igemm(c, a));
       }
       Conv& Q = p->L[l - 1];  // encoder output feeding this pool (and a skip)
       const Skip& sk = p->S[3 - k];
@@ -396,7 +573,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       a.e.colsum1 = c.d(T.colsum);
       {
         Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
-        CK(launch_igemm(a, s));
+        CK(run_igemm(c, a));
       }
       CK(launch_colsum(c.d(T.colsum), kStatGroups, T.co, P<float>(grd, T.gw + 1), s));
       // ConvTranspose2d weight grad: C[ci][ab*Co+co] = sum_p z[p][ci] * du[2p+ab][co]
@@ -427,7 +604,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
         w.P = n * T.h * T.w;
         w.out = c.f(T.dwp);
         Timer t(p, s, UNET_KC_CONV_WGRAD, 2.0 * w.P * (double)w.Mo * w.No, 0);
-        CK(launch_wgrad(w, s));
+        CK(run_wgrad(c, w));
       }
       CK(launch_permute_last2(c.f(T.dwp), T.ci, 4, T.co, P<float>(grd, T.gw), s));
       // ConvTranspose2d input grad -> dz of layer l-1
@@ -457,7 +634,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       b.e.bn_invstd = c.f(Q.invstd);
       b.e.bstats = c.d(Q.bstats);
       Timer t(p, s, UNET_KC_CONV_DGRAD, 2.0 * b.M * (double)b.N * b.K, 0);
-      CK(launch_igemm(b, s));
+      CK(run_igemm(c, b));
     }
   }
   return 0;
@@ -585,6 +762,18 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
   for (int k = 0; k < 4; ++k) p->T[k].dwp = al.take(fsz(4LL * p->T[k].co * p->T[k].ci));
   p->dwp_region.off = dwp_start;
   p->dwp_region.bytes = al.top - dwp_start;
+  {
+    // split-K partials: the budget, or the largest 8-way split of any conv GEMM if smaller
+    size_t mx = 0, wmax = (size_t)kStatGroups * 1024 * 2 * sizeof(double);
+    for (int l = 1; l < 18; ++l) {
+      const Conv& L = p->L[l];
+      mx = std::max(mx, 8 * (size_t)n * L.ho * L.wo * L.co * sizeof(float));
+      mx = std::max(mx, 8 * (size_t)n * L.hi * L.wi * L.ci * sizeof(float));
+      wmax = std::max(wmax, (size_t)9 * L.co * L.ci * sizeof(float));
+    }
+    p->slab = al.take(std::min(mx, kSlabBudget));
+    p->tune_scratch = al.take(wmax);
+  }
   for (int l = 0; l < 18; ++l) {
     Conv& L = p->L[l];
     const long long pix = (long long)n * L.ho * L.wo;
@@ -674,6 +863,27 @@ int unet_plan_backward(unet_plan* p, void* const* prm, void* const* grd, const f
   }
   return run_backward(p, prm, grd, x, dlogits, reinterpret_cast<char*>(ws), sb, se,
                       reinterpret_cast<hipStream_t>(stream));
+}
+
+size_t unet_tuning_report(char* buf, size_t len) {
+  std::string r;
+  {
+    std::lock_guard<std::mutex> lk(g_tune_mu);
+    for (const auto& kv : g_tune_log) r += kv.second + "\n";
+  }
+  if (buf && len > 0) {
+    const size_t k = std::min(len - 1, r.size());
+    memcpy(buf, r.data(), k);
+    buf[k] = 0;
+  }
+  return r.size() + 1;
+}
+
+int unet_tuning_reset(void) {
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  g_tuned.clear();
+  g_tune_log.clear();
+  return 0;
 }
 
 int unet_plan_set_timing(unet_plan* p, int enable) {

@@ -68,6 +68,10 @@ struct IgemmArgs {
   const float* b;    // packed B[N][K] (k contiguous)
   int M, N, K;
   Epilogue e;
+  // split-K: > 1 slices the K chunks over blockIdx.z; raw partial tiles go to
+  // slab[z][M][N] and k_splitk_epi sums them and runs the epilogue
+  int ksplit = 1;
+  float* slab = nullptr;
 };
 
 struct WgradArgs {
@@ -81,8 +85,24 @@ struct WgradArgs {
 };
 
 // ---------------- launchers (kernels.hip) ----------------
-hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s);
-hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s);
+// Variant of a GEMM launch.  igemm: tile id (1-4, 6-9, see igemm.hip) and K
+// split; wgrad: tile id (0-4) and target workgroups per CU of the pixel split.
+// tile < 0 = built-in heuristic.  Chosen per launch site by the plan's autotuner.
+struct GemmChoice {
+  int tile = -1;
+  int split = 1;
+};
+int num_cus();
+hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s);  // heuristic
+hipError_t launch_igemm_v(const IgemmArgs& a, hipStream_t s, GemmChoice c);
+bool igemm_tile_fits(const IgemmArgs& a, int tile);
+// workgroups of one K slice and resident workgroups per CU for a tile
+long long igemm_tile_count(const IgemmArgs& a, int tile);
+int igemm_tile_slots(int tile);
+size_t igemm_slab_bytes(const IgemmArgs& a, int ksplit);
+hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s);  // heuristic
+hipError_t launch_wgrad_v(const WgradArgs& a, hipStream_t s, GemmChoice c);
+bool wgrad_tile_fits(const WgradArgs& a, int tile);
 
 // inc.c0: Ci in {1,2,3,4} direct conv from an NCHW input; y NHWC (Co = 64 multiple).
 hipError_t launch_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w,

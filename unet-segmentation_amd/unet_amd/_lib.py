@@ -50,6 +50,8 @@ SIGNATURES = {
     "unet_bn_train_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "unet_bn_ws_bytes": (_sz, [_i]),
     "unet_set_tuning": (_i, [ctypes.c_char_p, _i]),
+    "unet_tuning_report": (_sz, [ctypes.c_char_p, _sz]),
+    "unet_tuning_reset": (_i, []),
 }
 
 _lib = None
@@ -102,3 +104,12 @@ def ptr_array(tensors):
 def stream_of(device=None):
     import torch
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+def tuning_report() -> str:
+    """The GEMM autotuner's choices (one line per GEMM shape)."""
+    lib = load()
+    n = lib.unet_tuning_report(None, 0)
+    buf = ctypes.create_string_buffer(n)
+    lib.unet_tuning_report(buf, n)
+    return buf.value.decode()
