@@ -130,7 +130,9 @@ int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int 
  *  "igemm_variant" heuristic override for A/B measurements (-1 = off, 1..9 =
  *                  forced tile shape); "wgrad_variant" (-1 = off, 1 = 64x64
  *                  tile, >=2 = workgroups per CU for the pixel split);
- *  "force_split"   k > 1: every plan igemm runs split-K k (tests), 0 = off. */
+ *  "force_split"   k > 1: every plan igemm runs split-K k (tests), 0 = off.
+ *  "force_tile"    id > 0: every plan igemm whose shape admits tile id runs
+ *                  it (tests; 1-4, 6-9 register-staged, 11-14 LDS-DMA). */
 int unet_set_tuning(const char* key, int value);
 /* Text report of the tuned GEMM choices (one line per shape: key, heuristic
  * time, chosen variant and time).  Copies up to len-1 bytes + NUL into buf

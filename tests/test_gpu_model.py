@@ -74,19 +74,25 @@ def gemm_mode(request):
     lib = _lib.load()
     mode = getattr(request, "param", "autotune")
     lib.unet_tuning_reset()
-    if mode == "heuristic":
-        lib.unet_set_tuning(b"autotune", 0)
-    elif mode.startswith("split"):
-        lib.unet_set_tuning(b"force_split", int(mode[5:]))
+    for part in mode.split("+"):
+        if part == "heuristic":
+            lib.unet_set_tuning(b"autotune", 0)
+        elif part.startswith("split"):
+            lib.unet_set_tuning(b"force_split", int(part[5:]))
+        elif part.startswith("tile"):
+            lib.unet_set_tuning(b"force_tile", int(part[4:]))
     yield mode
     lib.unet_set_tuning(b"autotune", 1)
     lib.unet_set_tuning(b"force_split", 0)
+    lib.unet_set_tuning(b"force_tile", 0)
     lib.unet_tuning_reset()
 
 
-@pytest.mark.parametrize("gemm_mode", ["heuristic", "split3", "split8"], indirect=True)
+@pytest.mark.parametrize("gemm_mode", ["heuristic", "split3", "split8", "tile11", "tile12", "tile13", "tile14",
+                                       "tile12+split4", "tile14+split3", "tile3", "tile6"], indirect=True)
 def test_train_step_gemm_variants_vs_oracle(gemm_mode):
-    """Built-in tiles and split-K (k_splitk_epi epilogue) against the oracle."""
+    """Built-in tiles, the LDS-DMA staged tiles (11-14) and split-K (k_splitk_epi
+    epilogue) on every conv / convT / dgrad GEMM of a train step, against the oracle."""
     test_train_step_vs_oracle(2, 188, 21)
 
 

@@ -56,141 +56,18 @@ constexpr int igemm_minw(int BM, int BN, int WM, int WN, int BK) {
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
-template <int BM, int BN, int WM, int WN, int BK>
-__global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void k_igemm(const IgemmArgs args) {
-  constexpr int NT = WM * WN * 64;
-  constexpr int LDK = BK + 4;
+// Split-K partial store or the full epilogue of a k_igemm-family tile: bias,
+// destination mapping (linear / pixel shuffle / cropped), ReLU mask + BN-bwd
+// statistics, BN statistics, concat column sums.  `red` is WM*3*BN floats of
+// LDS that no wave reads or writes any more (a barrier precedes its use).
+template <int BM, int BN, int WM, int WN, int NT>
+__device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&acc)[BM / (WM * 32)][BN / (WN * 32)],
+                                             int m0, int n0, int wm, int wn, int tid, float* red) {
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-  constexpr int C4 = BK / 4;           // float4 per staged row
-  constexpr int RPP = NT / C4;         // rows per staging pass
-  constexpr int AV = BM / RPP, BV = BN / RPP;
-  constexpr int KH = BK / 2, KF = KH / 4;
-  static_assert(TM >= 1 && TN >= 1 && AV >= 1 && BV >= 1 && BM % RPP == 0 && BN % RPP == 0, "tile");
-  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
-
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
   const Gather& g = args.a;
-  const int M = args.M, K = args.K;
-  const int col4 = tid % C4, row0 = tid / C4;
-
-  // Per staged A row: pixel base in each source grid (before the tap offset).
-  int rb0[AV], rb1[AV];
+  const int M = args.M;
+  const int lane = tid & 63, h = lane >> 5, li = lane & 31;
   const int HWg = g.Hg * g.Wg;
-#pragma unroll
-  for (int q = 0; q < AV; ++q) {
-    int m = m0 + row0 + RPP * q;
-    m = m < M ? m : M - 1;
-    int n = m / HWg, r = m - n * HWg;
-    int y = r / g.Wg, x = r - y * g.Wg;
-    y *= g.stride;
-    x *= g.stride;
-    rb0[q] = (n * g.s[0].H + y + g.s[0].oy) * g.s[0].W + x + g.s[0].ox;
-    rb1[q] = (n * g.s[1].H + y + g.s[1].oy) * g.s[1].W + x + g.s[1].ox;
-  }
-  const float* bptr[BV];
-#pragma unroll
-  for (int q = 0; q < BV; ++q) bptr[q] = args.b + (size_t)(n0 + row0 + RPP * q) * K + col4 * 4;
-
-  // K range of this workgroup (split-K slices chunks over blockIdx.z)
-  const int nk_all = K / BK;
-  int kc0 = 0, kc1 = nk_all;
-  if (args.ksplit > 1) {
-    const int per = (nk_all + args.ksplit - 1) / args.ksplit;
-    kc0 = blockIdx.z * per;
-    kc1 = min(nk_all, kc0 + per);
-  }
-  // K iterator (uniform): chunk -> (tap_y, tap_x, c0).  A chunk never straddles
-  // a tap or the concat split (Cg and c_split are multiples of BK).
-  int it_ty = 0, it_tx = 0, it_c = 0;
-  {
-    const int cpt = g.Cg / BK;
-    const int tap = kc0 / cpt;
-    it_c = (kc0 - tap * cpt) * BK;
-    it_ty = tap / g.taps_w;
-    it_tx = tap - it_ty * g.taps_w;
-  }
-  float4 ra[AV], rb[BV], rsc, rsh;
-  bool rtf = false;
-  auto issue = [&](int k0) {
-    const bool second = it_c >= g.c_split;
-    const Src& s = second ? g.s[1] : g.s[0];
-    const int c = (second ? it_c - g.c_split : it_c) + col4 * 4;
-    const int toff = it_ty * s.W + it_tx;
-#pragma unroll
-    for (int q = 0; q < AV; ++q) ra[q] = ld4(s.ptr + (size_t)((second ? rb1[q] : rb0[q]) + toff) * s.C + c);
-#pragma unroll
-    for (int q = 0; q < BV; ++q) rb[q] = ld4(bptr[q] + k0);
-    rtf = s.scale != nullptr;
-    if (rtf) {
-      rsc = ld4(s.scale + c);
-      rsh = ld4(s.shift + c);
-    }
-    it_c += BK;
-    if (it_c == g.Cg) {
-      it_c = 0;
-      if (++it_tx == g.taps_w) { it_tx = 0; ++it_ty; }
-    }
-  };
-  auto commit = [&](int buf) {
-    float* As = lds + buf * (BM + BN) * LDK;
-    float* Bs = As + BM * LDK;
-    if (rtf) {
-#pragma unroll
-      for (int q = 0; q < AV; ++q) ra[q] = affine_relu4(ra[q], rsc, rsh);
-    }
-#pragma unroll
-    for (int q = 0; q < AV; ++q) st4(As + (row0 + RPP * q) * LDK + col4 * 4, ra[q]);
-#pragma unroll
-    for (int q = 0; q < BV; ++q) st4(Bs + (row0 + RPP * q) * LDK + col4 * 4, rb[q]);
-  };
-
-  floatx16 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int h = lane >> 5, li = lane & 31;
-  if (kc0 < kc1) {
-    issue(kc0 * BK);
-    commit(0);
-    __syncthreads();
-  }
-  for (int kc = kc0; kc < kc1; ++kc) {
-    const int cur = (kc - kc0) & 1;
-    const bool more = kc + 1 < kc1;
-    if (more) issue((kc + 1) * BK);
-    const float* As = lds + cur * (BM + BN) * LDK;
-    const float* Bs = As + BM * LDK;
-    float4 fa[TM][KF], fb[TN][KF];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const float* p = As + (wm * TM * 32 + i * 32 + li) * LDK + h * KH;
-#pragma unroll
-      for (int f = 0; f < KF; ++f) fa[i][f] = ld4(p + 4 * f);
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const float* p = Bs + (wn * TN * 32 + j * 32 + li) * LDK + h * KH;
-#pragma unroll
-      for (int f = 0; f < KF; ++f) fb[j][f] = ld4(p + 4 * f);
-    }
-#pragma unroll
-    for (int s = 0; s < KH; ++s)
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(getc(fa[i][s >> 2], s & 3), getc(fb[j][s >> 2], s & 3),
-                                                           acc[i][j], 0, 0, 0);
-    if (more) commit(cur ^ 1);
-    __syncthreads();
-  }
-
   const int N = args.N;
   if (args.ksplit > 1) {  // raw partial tile; k_splitk_epi finishes
     float* sl = args.slab + (size_t)blockIdx.z * M * N;
@@ -263,7 +140,6 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   }
   const bool want_stats = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
   if (!want_stats) return;
-  __shared__ float red[WM][3][BN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     s1[j] += __shfl_xor(s1[j], 32);
@@ -274,9 +150,9 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int lc = wn * TN * 32 + j * 32 + li;
-      red[wm][0][lc] = s1[j];
-      red[wm][1][lc] = s2[j];
-      red[wm][2][lc] = t1[j];
+      red[(wm * 3 + 0) * BN + lc] = s1[j];
+      red[(wm * 3 + 1) * BN + lc] = s2[j];
+      red[(wm * 3 + 2) * BN + lc] = t1[j];
     }
   }
   __syncthreads();
@@ -285,7 +161,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   for (int lc = tid; lc < BN; lc += NT) {
     float a = 0.f, b = 0.f, c = 0.f;
 #pragma unroll
-    for (int w = 0; w < WM; ++w) { a += red[w][0][lc]; b += red[w][1][lc]; c += red[w][2][lc]; }
+    for (int w = 0; w < WM; ++w) { a += red[(w * 3 + 0) * BN + lc]; b += red[(w * 3 + 1) * BN + lc]; c += red[(w * 3 + 2) * BN + lc]; }
     const int col = n0 + lc;
     if (col < nsplit) {
       double* st = e.yref ? e.bstats : e.stats;
@@ -298,6 +174,416 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
       atomicAdd(e.colsum1 + (size_t)grp * n2 + (col - nsplit), (double)c);
     }
   }
+}
+
+// ABL: ablation switches for tools/igemm_bench.cpp only (0 in the library):
+// 1 no global loads, 2 no in-loop barrier, 4 no BN transform, 8 no LDS
+// fragment reads, 16 no LDS stores, 32 BN transform with constant scale/shift
+// (no scale/shift loads), 64 no A loads, 128 no B loads, 256 A loads from
+// contiguous addresses, 512 global loads for the first two K-steps only (the
+// LDS keeps real, non-zero data: MFMA power and clock stay representative).
+// Results are meaningless when set.
+// PF: K-steps of operands in flight in registers (1 or 2).
+template <int BM, int BN, int WM, int WN, int BK, int ABL = 0, int PF = 1>
+__global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void k_igemm(const IgemmArgs args) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int LDK = BK + 4;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  constexpr int C4 = BK / 4;           // float4 per staged row
+  constexpr int RPP = NT / C4;         // rows per staging pass
+  constexpr int AV = BM / RPP, BV = BN / RPP;
+  constexpr int KH = BK / 2, KF = KH / 4;
+  static_assert(TM >= 1 && TN >= 1 && AV >= 1 && BV >= 1 && BM % RPP == 0 && BN % RPP == 0, "tile");
+  __shared__ __attribute__((aligned(16))) float lds[2 * (BM + BN) * LDK];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const Gather& g = args.a;
+  const int M = args.M, K = args.K;
+  const int col4 = tid % C4, row0 = tid / C4;
+
+  // Per staged A row: pixel base in each source grid (before the tap offset).
+  int rb0[AV], rb1[AV];
+  const int HWg = g.Hg * g.Wg;
+#pragma unroll
+  for (int q = 0; q < AV; ++q) {
+    int m = m0 + row0 + RPP * q;
+    m = m < M ? m : M - 1;
+    int n = m / HWg, r = m - n * HWg;
+    int y = r / g.Wg, x = r - y * g.Wg;
+    y *= g.stride;
+    x *= g.stride;
+    rb0[q] = (n * g.s[0].H + y + g.s[0].oy) * g.s[0].W + x + g.s[0].ox;
+    rb1[q] = (n * g.s[1].H + y + g.s[1].oy) * g.s[1].W + x + g.s[1].ox;
+  }
+  const float* bptr[BV];
+#pragma unroll
+  for (int q = 0; q < BV; ++q) bptr[q] = args.b + (size_t)(n0 + row0 + RPP * q) * K + col4 * 4;
+
+  // K range of this workgroup (split-K slices chunks over blockIdx.z)
+  const int nk_all = K / BK;
+  int kc0 = 0, kc1 = nk_all;
+  if (args.ksplit > 1) {
+    const int per = (nk_all + args.ksplit - 1) / args.ksplit;
+    kc0 = blockIdx.z * per;
+    kc1 = min(nk_all, kc0 + per);
+  }
+  // K iterator (uniform): chunk -> (tap_y, tap_x, c0).  A chunk never straddles
+  // a tap or the concat split (Cg and c_split are multiples of BK).
+  int it_ty = 0, it_tx = 0, it_c = 0;
+  {
+    const int cpt = g.Cg / BK;
+    const int tap = kc0 / cpt;
+    it_c = (kc0 - tap * cpt) * BK;
+    it_ty = tap / g.taps_w;
+    it_tx = tap - it_ty * g.taps_w;
+  }
+  // One K-step of staged operands in registers (PF of them in flight).
+  struct Stage {
+    float4 ra[AV], rb[BV], sc, sh;
+    bool tf;
+  };
+  Stage S0, S1;
+  if (ABL & (1 | 64 | 128)) {
+#pragma unroll
+    for (int q = 0; q < AV; ++q) S0.ra[q] = S1.ra[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+    for (int q = 0; q < BV; ++q) S0.rb[q] = S1.rb[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+    S0.sc = S0.sh = S1.sc = S1.sh = S0.ra[0];
+  }
+  int nissued = 0;
+  auto issue = [&](Stage& st, int k0) {
+    const bool second = it_c >= g.c_split;
+    const Src& s = second ? g.s[1] : g.s[0];
+    const int c = (second ? it_c - g.c_split : it_c) + col4 * 4;
+    const int toff = it_ty * s.W + it_tx;
+    if (!(ABL & 1) && (!(ABL & 512) || nissued++ < 2)) {
+      if (ABL & 256) {  // contiguous 1 KiB per wave-instruction (layout experiment)
+#pragma unroll
+        for (int q = 0; q < AV; ++q)
+          st.ra[q] = ld4(s.ptr + (((size_t)(m0 + RPP * q) * BK + k0 * 64) % ((size_t)s.C * s.H * s.W)) + tid * 4);
+      } else if (!(ABL & 64)) {
+#pragma unroll
+        for (int q = 0; q < AV; ++q) st.ra[q] = ld4(s.ptr + (size_t)((second ? rb1[q] : rb0[q]) + toff) * s.C + c);
+      }
+      if (!(ABL & 128)) {
+#pragma unroll
+        for (int q = 0; q < BV; ++q) st.rb[q] = ld4(bptr[q] + k0);
+      }
+    }
+    st.tf = !(ABL & 4) && s.scale != nullptr;
+    if (ABL & 32) {
+      st.sc = make_float4(1.f, 1.f, 1.f, 1.f);
+      st.sh = make_float4(0.f, 0.f, 0.f, 0.f);
+    } else if (st.tf && !(ABL & 1)) {
+      st.sc = ld4(s.scale + c);
+      st.sh = ld4(s.shift + c);
+    }
+    it_c += BK;
+    if (it_c == g.Cg) {
+      it_c = 0;
+      if (++it_tx == g.taps_w) { it_tx = 0; ++it_ty; }
+    }
+  };
+  auto commit = [&](Stage& st, int buf) {
+    if (ABL & 16) return;
+    float* As = lds + buf * (BM + BN) * LDK;
+    float* Bs = As + BM * LDK;
+    if (st.tf) {
+#pragma unroll
+      for (int q = 0; q < AV; ++q) st.ra[q] = affine_relu4(st.ra[q], st.sc, st.sh);
+    }
+#pragma unroll
+    for (int q = 0; q < AV; ++q) st4(As + (row0 + RPP * q) * LDK + col4 * 4, st.ra[q]);
+#pragma unroll
+    for (int q = 0; q < BV; ++q) st4(Bs + (row0 + RPP * q) * LDK + col4 * 4, st.rb[q]);
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int h = lane >> 5, li = lane & 31;
+  auto compute = [&](int buf, int kc) {
+    const float* As = lds + buf * (BM + BN) * LDK;
+    const float* Bs = As + BM * LDK;
+    float4 fa[TM][KF], fb[TN][KF];
+    if (ABL & 8) {
+      const float v = (float)(lane + kc);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int f = 0; f < KF; ++f) fa[i][f] = make_float4(v, v + i, v + f, v);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int f = 0; f < KF; ++f) fb[j][f] = make_float4(v, v + j, v + f, v);
+    } else {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* p = As + (wm * TM * 32 + i * 32 + li) * LDK + h * KH;
+#pragma unroll
+        for (int f = 0; f < KF; ++f) fa[i][f] = ld4(p + 4 * f);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* p = Bs + (wn * TN * 32 + j * 32 + li) * LDK + h * KH;
+#pragma unroll
+        for (int f = 0; f < KF; ++f) fb[j][f] = ld4(p + 4 * f);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < KH; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(getc(fa[i][s >> 2], s & 3), getc(fb[j][s >> 2], s & 3),
+                                                           acc[i][j], 0, 0, 0);
+  };
+  auto barrier = [&] {
+    if (!(ABL & 2)) __syncthreads();
+  };
+
+  if constexpr (PF == 1) {
+    // one K-step in flight: loads for kc+1 issued before kc's MFMAs, stored after
+    if (kc0 < kc1) {
+      issue(S0, kc0 * BK);
+      commit(S0, 0);
+      barrier();
+    }
+    for (int kc = kc0; kc < kc1; ++kc) {
+      const int cur = (kc - kc0) & 1;
+      const bool more = kc + 1 < kc1;
+      if (more) issue(S0, (kc + 1) * BK);
+      compute(cur, kc);
+      if (more) commit(S0, cur ^ 1);
+      barrier();
+    }
+  } else {
+    // two K-steps in flight (register sets S0/S1 alternate; loop unrolled by 2)
+    if (kc0 < kc1) {
+      issue(S0, kc0 * BK);
+      commit(S0, 0);
+      if (kc0 + 1 < kc1) issue(S1, (kc0 + 1) * BK);
+      barrier();
+    }
+    for (int kc = kc0; kc < kc1; kc += 2) {
+      if (kc + 2 < kc1) issue(S0, (kc + 2) * BK);
+      compute(0, kc);
+      if (kc + 1 < kc1) commit(S1, 1);
+      barrier();
+      if (kc + 1 >= kc1) break;
+      if (kc + 3 < kc1) issue(S1, (kc + 3) * BK);
+      compute(1, kc + 1);
+      if (kc + 2 < kc1) commit(S0, 0);
+      barrier();
+    }
+  }
+
+  __shared__ float red[WM * 3 * BN];
+  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, red);
+}
+
+
+// ---------------------------------------------------------------------------
+// k_igemm_g: the same implicit GEMM with LDS-DMA staging.  Every K-step's A
+// and B tiles go global -> LDS by global_load_lds_dwordx4 (no staging VGPRs,
+// no ds_write), through a 3-slot LDS ring: the loads of step k+2 are in flight
+// while step k computes.  LDS rows are 16 floats (64 B) unpadded; the 16-B
+// chunk c of row r sits at slot c ^ ((r >> 2) & 3) (the source address carries
+// the permutation, the fragment read applies it), which keeps every
+// ds_read_b128 lane group on distinct bank quads.  The consumer-side BN+ReLU
+// of the A operand is applied to the fragments after the LDS read, with
+// scale/shift preloaded into LDS once per workgroup.
+// ---------------------------------------------------------------------------
+typedef __attribute__((address_space(3))) float lds_float_t;
+
+// One global_load_lds_dwordx4: 16 B per lane from `src` into LDS at the
+// wave-uniform `dst` + lane*16.  Inline asm, so that hipcc neither waits for it
+// before unrelated ds_reads (it cannot tell ring slots apart) nor counts it:
+// the caller retires it with an explicit vmcnt.
+__device__ __forceinline__ void glds16(const float* src, float* dst) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane((unsigned)(size_t)(lds_float_t*)dst);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+
+constexpr int igemm_g_lds_floats(int BM, int BN) { return 3 * (BM + BN) * 16; }
+constexpr int igemm_g_minw(int BM, int BN, int WM, int WN) {
+  int blocks = 163840 / (igemm_g_lds_floats(BM, BN) * 4 + 2048);
+  if (blocks > 8) blocks = 8;
+  int w = blocks * WM * WN * 64 / 256;
+  return w < 1 ? 1 : (w > 8 ? 8 : w);
+}
+
+// s_waitcnt vmcnt(n) leaving expcnt/lgkmcnt unconstrained (gfx9 encoding)
+#define UNET_WAIT_VMCNT(n) __builtin_amdgcn_s_waitcnt(((n)&15) | (7 << 4) | (15 << 8) | ((((n) >> 4) & 3) << 14))
+
+template <int BM, int BN, int WM, int WN>
+__global__ __launch_bounds__(WM * WN * 64, igemm_g_minw(BM, BN, WM, WN)) void k_igemm_g(const IgemmArgs args) {
+  constexpr int NT = WM * WN * 64, NW = WM * WN, BK = 16, NS = 3;
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  constexpr int STAGE = (BM + BN) * BK;
+  constexpr int PA = BM / (16 * NW), PB = BN / (16 * NW);  // 1-KiB pieces per wave per step
+  static_assert(PA >= 1 && PB >= 1 && BM % (16 * NW) == 0 && BN % (16 * NW) == 0, "tile");
+  extern __shared__ __attribute__((aligned(16))) float dl[];
+  float* ssc = dl + NS * STAGE;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const Gather& g = args.a;
+  const int M = args.M, K = args.K, Cg = g.Cg;
+  const int lrow = lane >> 2, lslot = lane & 3;
+
+  // per-lane source rows of this wave's pieces (row r of the tile = piece*16 + lrow)
+  int rb0[PA], rb1[PA], ca[PA];
+  const int HWg = g.Hg * g.Wg;
+#pragma unroll
+  for (int p = 0; p < PA; ++p) {
+    const int r = (wave * PA + p) * 16 + lrow;
+    int m = m0 + r;
+    m = m < M ? m : M - 1;
+    const int n = m / HWg, rr = m - n * HWg;
+    int y = rr / g.Wg, x = rr - y * g.Wg;
+    y *= g.stride;
+    x *= g.stride;
+    rb0[p] = (n * g.s[0].H + y + g.s[0].oy) * g.s[0].W + x + g.s[0].ox;
+    rb1[p] = (n * g.s[1].H + y + g.s[1].oy) * g.s[1].W + x + g.s[1].ox;
+    ca[p] = (lslot ^ ((r >> 2) & 3)) * 4;
+  }
+  const float* bptr[PB];
+#pragma unroll
+  for (int p = 0; p < PB; ++p) {
+    const int r = (wave * PB + p) * 16 + lrow;
+    bptr[p] = args.b + (size_t)(n0 + r) * K + (lslot ^ ((r >> 2) & 3)) * 4;
+  }
+  // consumer BN+ReLU parameters of the concatenated channel range
+  const bool any_tf = g.s[0].scale != nullptr || (g.c_split < Cg && g.s[1].scale != nullptr);
+  if (any_tf) {
+    for (int c = tid; c < Cg; c += NT) {
+      const bool sec = c >= g.c_split;
+      const Src& sr = sec ? g.s[1] : g.s[0];
+      const int cl = sec ? c - g.c_split : c;
+      ssc[c] = sr.scale ? sr.scale[cl] : 1.f;
+      ssc[Cg + c] = sr.scale ? sr.shift[cl] : 0.f;
+    }
+    __syncthreads();
+  }
+
+  const int nk_all = K / BK;
+  int kc0 = 0, kc1 = nk_all;
+  if (args.ksplit > 1) {
+    const int per = (nk_all + args.ksplit - 1) / args.ksplit;
+    kc0 = blockIdx.z * per;
+    kc1 = min(nk_all, kc0 + per);
+  }
+  // producer-side K iterator (issue runs two steps ahead of compute)
+  int it_ty, it_tx, it_c;
+  {
+    const int cpt = Cg / BK;
+    const int tap = kc0 / cpt;
+    it_c = (kc0 - tap * cpt) * BK;
+    it_ty = tap / g.taps_w;
+    it_tx = tap - it_ty * g.taps_w;
+  }
+  int cc = it_c;  // consumer-side channel offset of the step being computed
+
+  auto issue = [&](int slot, int k0) {
+    const bool second = it_c >= g.c_split;
+    const Src& s = second ? g.s[1] : g.s[0];
+    const int c = second ? it_c - g.c_split : it_c;
+    const int toff = it_ty * s.W + it_tx;
+    float* As = dl + slot * STAGE;
+    float* Bs = As + BM * BK;
+#pragma unroll
+    for (int p = 0; p < PA; ++p)
+      glds16(s.ptr + (size_t)((second ? rb1[p] : rb0[p]) + toff) * s.C + c + ca[p], As + (wave * PA + p) * 16 * BK);
+#pragma unroll
+    for (int p = 0; p < PB; ++p) glds16(bptr[p] + k0, Bs + (wave * PB + p) * 16 * BK);
+    it_c += BK;
+    if (it_c == Cg) {
+      it_c = 0;
+      if (++it_tx == g.taps_w) { it_tx = 0; ++it_ty; }
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int h = lane >> 5, li = lane & 31;
+  const int sw = (li >> 2) & 3;  // row swizzle of this lane's fragment rows (row bases are multiples of 32)
+  auto compute = [&](int slot) {
+    const float* As = dl + slot * STAGE;
+    const float* Bs = As + BM * BK;
+    float4 fa[TM][2], fb[TN][2];
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const float* pr = As + (wm * TM * 32 + i * 32 + li) * BK;
+#pragma unroll
+      for (int f = 0; f < 2; ++f) fa[i][f] = ld4(pr + (((2 * h + f) ^ sw) << 2));
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const float* pr = Bs + (wn * TN * 32 + j * 32 + li) * BK;
+#pragma unroll
+      for (int f = 0; f < 2; ++f) fb[j][f] = ld4(pr + (((2 * h + f) ^ sw) << 2));
+    }
+    const bool tf = cc < g.c_split ? g.s[0].scale != nullptr : g.s[1].scale != nullptr;
+    if (tf) {
+#pragma unroll
+      for (int f = 0; f < 2; ++f) {
+        const float4 sc = ld4(ssc + cc + 8 * h + 4 * f), sh = ld4(ssc + Cg + cc + 8 * h + 4 * f);
+#pragma unroll
+        for (int i = 0; i < TM; ++i) fa[i][f] = affine_relu4(fa[i][f], sc, sh);
+      }
+    }
+#pragma unroll
+    for (int s = 0; s < 8; ++s)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(getc(fa[i][s >> 2], s & 3), getc(fb[j][s >> 2], s & 3),
+                                                           acc[i][j], 0, 0, 0);
+    cc += BK;
+    if (cc == Cg) cc = 0;
+  };
+
+  if (kc0 < kc1) issue(0, kc0 * BK);
+  if (kc0 + 1 < kc1) issue(1, (kc0 + 1) * BK);
+  int slot = 0;
+  for (int kc = kc0; kc < kc1; ++kc) {
+    // this wave's loads of step kc have landed (step kc+1's may still fly) ...
+    if (kc + 1 < kc1) UNET_WAIT_VMCNT(PA + PB);
+    else UNET_WAIT_VMCNT(0);
+    // ... and every wave's (also: every wave is done reading the slot refilled next)
+    __builtin_amdgcn_s_barrier();
+    if (kc + 2 < kc1) issue(slot == 0 ? 2 : slot - 1, (kc + 2) * BK);
+    compute(slot);
+    slot = slot == 2 ? 0 : slot + 1;
+  }
+  __syncthreads();  // the ring is reused as the epilogue's reduction buffer
+  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, dl);
+}
+
+template <int BM, int BN>
+constexpr size_t igemm_g_smem(int cg) {
+  return (size_t)igemm_g_lds_floats(BM, BN) * 4 + (size_t)2 * cg * 4;
 }
 
 // ---------------------------------------------------------------------------
@@ -595,6 +881,11 @@ static TileInfo tile_info(int id) {
     case 7: return {256, 64, 32, 1};
     case 8: return {128, 64, 16, 4};
     case 9: return {64, 128, 32, 2};
+    // LDS-DMA staged (k_igemm_g)
+    case 11: return {256, 128, 16, 2};
+    case 12: return {128, 128, 16, 3};
+    case 13: return {64, 128, 16, 4};
+    case 14: return {128, 64, 16, 4};
     default: return {0, 0, 0, 0};
   }
 }
@@ -621,6 +912,25 @@ static hipError_t go_igemm(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int BM, int BN, int WM, int WN>
+static hipError_t go_igemm_g(const IgemmArgs& a, hipStream_t s) {
+  if (a.N % BN != 0 || a.K % 16 != 0 || a.a.Cg % 16 != 0 || a.a.c_split % 16 != 0) return hipErrorInvalidValue;
+  static bool attr = false;
+  const size_t full = igemm_g_smem<BM, BN>(1024);
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_igemm_g<BM, BN, WM, WN>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)full);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const bool tf = a.a.s[0].scale != nullptr || (a.a.c_split < a.a.Cg && a.a.s[1].scale != nullptr);
+  if (tf && a.a.Cg > 1024) return hipErrorInvalidValue;
+  const size_t smem = igemm_g_smem<BM, BN>(tf ? a.a.Cg : 0);
+  dim3 grid((a.M + BM - 1) / BM, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
+  hipLaunchKernelGGL((k_igemm_g<BM, BN, WM, WN>), grid, dim3(WM * WN * 64), smem, s, a);
+  return hipGetLastError();
+}
+
 static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
   switch (tile) {
     case 1: return go_igemm<128, 128, 2, 2, 16>(a, s);
@@ -631,6 +941,10 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 7: return go_igemm<256, 64, 4, 1, 32>(a, s);
     case 8: return go_igemm<128, 64, 2, 2, 16>(a, s);
     case 9: return go_igemm<64, 128, 2, 2, 32>(a, s);
+    case 11: return go_igemm_g<256, 128, 4, 2>(a, s);
+    case 12: return go_igemm_g<128, 128, 2, 2>(a, s);
+    case 13: return go_igemm_g<64, 128, 2, 2>(a, s);
+    case 14: return go_igemm_g<128, 64, 2, 2>(a, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -28,8 +28,10 @@ using namespace unet;
 namespace unet {
 // unet_set_tuning("autotune", v) or UNET_AUTOTUNE (default on)
 int g_autotune = getenv("UNET_AUTOTUNE") ? atoi(getenv("UNET_AUTOTUNE")) : 1;
-// unet_set_tuning("force_split", k): every igemm site runs split-K k (tests)
+// unet_set_tuning("force_split", k) / ("force_tile", id): every igemm site
+// runs split-K k and/or tile id where they apply (tests)
 int g_force_split = 0;
+int g_force_tile = 0;
 }  // namespace unet
 
 namespace {
@@ -184,7 +186,7 @@ std::string wgrad_key(const WgradArgs& a) {
 std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) {
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
-  for (int t : {4, 1, 2, 8, 6, 3, 9, 7}) {
+  for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14}) {
     if (!igemm_tile_fits(a, t)) continue;
     v.push_back({t, 1});
     const long long cnt = igemm_tile_count(a, t);
@@ -244,10 +246,14 @@ bool capturing(hipStream_t s) {
 }
 
 GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
-  if (unet::g_force_split > 1) {
+  if (unet::g_force_split > 1 || unet::g_force_tile > 0) {
+    const int ks = unet::g_force_split > 1 ? unet::g_force_split : 1;
+    if (igemm_slab_bytes(a, ks) > c.p->slab.bytes) return GemmChoice{};
+    if (unet::g_force_tile > 0) {
+      if (igemm_tile_fits(a, unet::g_force_tile)) return GemmChoice{unet::g_force_tile, ks};
+    }
     for (int t : {4, 1, 2, 8})
-      if (igemm_tile_fits(a, t) && igemm_slab_bytes(a, unet::g_force_split) <= c.p->slab.bytes)
-        return GemmChoice{t, unet::g_force_split};
+      if (igemm_tile_fits(a, t)) return GemmChoice{t, ks};
     return GemmChoice{};
   }
   if (!env_autotune() || capturing(c.s)) return GemmChoice{};

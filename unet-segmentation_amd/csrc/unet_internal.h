@@ -85,7 +85,8 @@ struct WgradArgs {
 };
 
 // ---------------- launchers (kernels.hip) ----------------
-// Variant of a GEMM launch.  igemm: tile id (1-4, 6-9, see igemm.hip) and K
+// Variant of a GEMM launch.  igemm: tile id (1-4, 6-9 register-staged,
+// 11-14 LDS-DMA staged; see igemm.hip) and K
 // split; wgrad: tile id (0-4) and target workgroups per CU of the pixel split.
 // tile < 0 = built-in heuristic.  Chosen per launch site by the plan's autotuner.
 struct GemmChoice {
