@@ -130,6 +130,9 @@ int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int 
  *  "igemm_variant" heuristic override for A/B measurements (-1 = off, 1..9 =
  *                  forced tile shape); "wgrad_variant" (-1 = off, 1 = 64x64
  *                  tile, >=2 = workgroups per CU for the pixel split);
+ *  "concurrent"    1 (default, or env UNET_CONCURRENT) = a plan's backward
+ *                  runs the weight-gradient GEMMs on a side stream beside the
+ *                  dX chain (joined before the call returns); 0 = one stream.
  *  "force_split"   k > 1: every plan igemm runs split-K k (tests), 0 = off.
  *  "force_tile"    id > 0: every plan igemm whose shape admits tile id runs
  *                  it (tests; 1-4, 6-9 register-staged, 11-14 LDS-DMA). */

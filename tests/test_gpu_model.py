@@ -297,3 +297,33 @@ def test_trainer_fast_path_matches_dropin_autograd_path():
         # later steps start from weights that differ by rounding; the network is
         # sensitive enough (small-sample BN) that only the losses are compared
         assert abs(la.item() - lb.item()) <= 1e-4 * abs(la.item())
+
+
+def test_side_stream_weight_grads_match_serial():
+    """Weight-gradient GEMMs on the side stream (after the plan's first, tuning,
+    backward) give the serial result: same kernels, only fp32 atomic order differs."""
+    from unet_amd import WeightedCrossEntropyLoss, _lib
+    lib = _lib.load()
+    params = O.hash_init(1, 2, seed=31, bn_random=True)
+    x, tgt, wmap = (torch.from_numpy(a).cuda() for a in F.make_inputs(31, 2, 1, 204))
+    m = make_model(params)
+    m.train()
+    crit = WeightedCrossEntropyLoss()
+
+    def grads():
+        m.zero_grad()
+        crit(m(x), tgt, wmap).backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.double().cpu().numpy() for n, p in m.named_parameters()}
+
+    try:
+        lib.unet_set_tuning(b"concurrent", 0)
+        grads()               # first backward of the plan: tunes, serial
+        ref = grads()
+        lib.unet_set_tuning(b"concurrent", 1)
+        got = grads()
+    finally:
+        lib.unet_set_tuning(b"concurrent", 1)
+    for name, g in ref.items():
+        scale = max(np.abs(g).max(), 1e-30)
+        assert np.abs(got[name] - g).max() <= 1e-5 * scale + 1e-12, name

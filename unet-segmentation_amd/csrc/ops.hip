@@ -11,7 +11,7 @@
 using namespace unet;
 
 namespace unet {
-extern int g_tune_igemm, g_tune_wgrad, g_autotune, g_force_split, g_force_tile;
+extern int g_tune_igemm, g_tune_wgrad, g_autotune, g_force_split, g_force_tile, g_concurrent;
 hipError_t launch_fill(float* p, size_t n, float v, hipStream_t s);
 hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream_t s);
 }  // namespace unet
@@ -321,6 +321,7 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "autotune") g_autotune = value;
   else if (k == "force_split") g_force_split = value;
   else if (k == "force_tile") g_force_tile = value;
+  else if (k == "concurrent") g_concurrent = value;
   else return -EINVAL;
   return 0;
 }

@@ -28,6 +28,9 @@ using namespace unet;
 namespace unet {
 // unet_set_tuning("autotune", v) or UNET_AUTOTUNE (default on)
 int g_autotune = getenv("UNET_AUTOTUNE") ? atoi(getenv("UNET_AUTOTUNE")) : 1;
+// unet_set_tuning("concurrent", v) or UNET_CONCURRENT (default on): weight
+// gradients on a side stream
+int g_concurrent = getenv("UNET_CONCURRENT") ? atoi(getenv("UNET_CONCURRENT")) : 1;
 // unet_set_tuning("force_split", k) / ("force_tile", id): every igemm site
 // runs split-K k and/or tile id where they apply (tests)
 int g_force_split = 0;
@@ -86,6 +89,11 @@ struct unet_plan {
   Pool P[4];
   Skip S[4];
   Buf stat_region, dwp_region, head_acc, wce_acc, first_slabs;
+  // weight-gradient GEMMs run on a side stream beside the dY -> dX chain of the
+  // backward (joined at the end of every backward call)
+  hipStream_t side = nullptr;
+  hipEvent_t ev_dy[18] = {}, ev_du[4] = {}, ev_join = nullptr;
+  int bwd_full = 0;  // completed whole backward passes (the first one tunes, serially)
   Buf slab;          // split-K partial tiles (igemm sites the tuner splits)
   Buf tune_scratch;  // atomic targets of the autotuner's trial launches
   size_t ws_bytes = 0;
@@ -476,10 +484,31 @@ int seg_of_layer(int l) {
   return 4 + (9 - l) / 2;            // 9,8 -> 4 ; 1,0 -> 8
 }
 
+hipError_t ensure_side_stream(unet_plan* p) {
+  if (p->side) return hipSuccess;
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  e = hipStreamCreateWithPriority(&p->side, hipStreamNonBlocking, least);
+  if (e != hipSuccess) return e;
+  for (auto& ev : p->ev_dy)
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+  for (auto& ev : p->ev_du)
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+  return hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming);
+}
+
 int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* x, const float* dlogits, char* ws,
                  int seg_b, int seg_e, hipStream_t s) {
   Ctx c{p, ws, s};
   const int n = p->n;
+  // Weight gradients of layer l need only dY(l) and forward tensors: they go to
+  // the side stream once the plan is tuned (timing runs stay serial so that
+  // per-kernel event times stay clean).
+  const bool conc = unet::g_concurrent && !p->timing && p->bwd_full > 0 && !capturing(s);
+  if (conc) CK(ensure_side_stream(p));
+  Ctx cw{p, ws, conc ? p->side : s};
+  const hipStream_t sw = cw.s;
   auto in_seg = [&](int sg) { return sg >= seg_b && sg < seg_e; };
   if (seg_b == 0) {
     // accumulators (bstats, colsums, packed weight grads) were zeroed by the
@@ -500,6 +529,10 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * ((double)(L.ho + 4) * (L.wo + 4) + 2.0 * L.ho * L.wo) * L.co);
       CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), n, L.ho, L.wo, L.co, c.f(L.dyp), 2, s));
     }
+    if (conc) {
+      CK(hipEventRecord(p->ev_dy[l], s));
+      CK(hipStreamWaitEvent(sw, p->ev_dy[l], 0));
+    }
     Src dy;  // dY interior of the padded buffer
     dy.ptr = c.f(L.dyp);
     dy.H = L.ho + 4;
@@ -507,9 +540,9 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     dy.C = L.co;
     dy.oy = dy.ox = 2;
     if (l == 0) {
-      Timer t(p, s, UNET_KC_STAGE1, 2.0 * M * L.co * L.ci * 9,
+      Timer t(p, sw, UNET_KC_STAGE1, 2.0 * M * L.co * L.ci * 9,
               4.0 * n * ((double)p->cin * p->h * p->w + (double)L.ho * L.wo * L.co));
-      CK(launch_conv_first_wgrad(x, n, p->cin, p->h, p->w, dy, L.co, P<float>(grd, L.gw), c.f(p->first_slabs), s));
+      CK(launch_conv_first_wgrad(x, n, p->cin, p->h, p->w, dy, L.co, P<float>(grd, L.gw), c.f(p->first_slabs), sw));
       continue;
     }
     // weight gradient
@@ -526,10 +559,10 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       w.No = 9 * L.ci;
       w.P = n * L.ho * L.wo;
       w.out = c.f(L.dwp);
-      Timer t(p, s, UNET_KC_CONV_WGRAD, conv_flops(L, n), 0);
-      CK(run_wgrad(c, w));
+      Timer t(p, sw, UNET_KC_CONV_WGRAD, conv_flops(L, n), 0);
+      CK(run_wgrad(cw, w));
     }
-    CK(launch_permute_last2(c.f(L.dwp), L.co, 9, L.ci, P<float>(grd, L.gw), s));
+    CK(launch_permute_last2(c.f(L.dwp), L.co, 9, L.ci, P<float>(grd, L.gw), sw));
     // input gradient
     IgemmArgs a;
     a.a.s[0] = dy;
@@ -582,6 +615,10 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
         CK(run_igemm(c, a));
       }
       CK(launch_colsum(c.d(T.colsum), kStatGroups, T.co, P<float>(grd, T.gw + 1), s));
+      if (conc) {  // du (the dgrad's second destination) feeds the convT weight grad
+        CK(hipEventRecord(p->ev_du[k], s));
+        CK(hipStreamWaitEvent(sw, p->ev_du[k], 0));
+      }
       // ConvTranspose2d weight grad: C[ci][ab*Co+co] = sum_p z[p][ci] * du[2p+ab][co]
       Conv& Q = p->L[l - 1];
       {
@@ -609,10 +646,10 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
         w.No = 4 * T.co;
         w.P = n * T.h * T.w;
         w.out = c.f(T.dwp);
-        Timer t(p, s, UNET_KC_CONV_WGRAD, 2.0 * w.P * (double)w.Mo * w.No, 0);
-        CK(run_wgrad(c, w));
+        Timer t(p, sw, UNET_KC_CONV_WGRAD, 2.0 * w.P * (double)w.Mo * w.No, 0);
+        CK(run_wgrad(cw, w));
       }
-      CK(launch_permute_last2(c.f(T.dwp), T.ci, 4, T.co, P<float>(grd, T.gw), s));
+      CK(launch_permute_last2(c.f(T.dwp), T.ci, 4, T.co, P<float>(grd, T.gw), sw));
       // ConvTranspose2d input grad -> dz of layer l-1
       IgemmArgs b;
       Src du;
@@ -643,6 +680,11 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       CK(run_igemm(c, b));
     }
   }
+  if (conc) {
+    CK(hipEventRecord(p->ev_join, sw));
+    CK(hipStreamWaitEvent(s, p->ev_join, 0));
+  }
+  if (seg_e == 9) ++p->bwd_full;
   return 0;
 }
 
@@ -819,6 +861,13 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
 
 void unet_plan_destroy(unet_plan* p) {
   if (!p) return;
+  if (p->side) {
+    (void)hipStreamSynchronize(p->side);
+    for (auto ev : p->ev_dy) (void)hipEventDestroy(ev);
+    for (auto ev : p->ev_du) (void)hipEventDestroy(ev);
+    (void)hipEventDestroy(p->ev_join);
+    (void)hipStreamDestroy(p->side);
+  }
   for (auto& e : p->evs) {
     hipEventDestroy(e.a);
     hipEventDestroy(e.b);
