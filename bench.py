@@ -104,16 +104,24 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--tuning-report", default=None, help="write the GEMM autotuner's choices to this file")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (ranks may share a GPU; rehearsal only)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
-    device = torch.device("cuda", local)
+    # one GPU per rank; "--dist-backend gloo" lets several ranks share a device
+    # (a rehearsal of the DP path on a 1-GPU box, not a measurement)
+    local_dev = local if args.dist_backend == "nccl" else local % torch.cuda.device_count()
+    torch.cuda.set_device(local_dev)
+    device = torch.device("cuda", local_dev)
     pg = None
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
         pg = dist.group.WORLD
 
     from unet_amd import UNet
@@ -188,7 +196,7 @@ def main():
             "data": "synthetic: x~U[0,1) (N,1,512,512), Bernoulli(0.4) targets, 10+1/freq(class) weight maps; "
                     "kaiming fan_out init (scripts/train.py:54-61)",
             "config": {"workload": f"U-Net train step {args.size}x{args.size}x1, batch {args.batch}/GPU, fp32: "
-                                   "fwd + weighted CE + bwd + SGD(0.99)" + (" + RCCL all-reduce" if world > 1 else ""),
+                                   "fwd + weighted CE + bwd + SGD(0.99)" + ((f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-reduce" if world > 1 else "")),
                        "global_batch": world * args.batch, "image": args.size,
                        "parallelism": f"dp{world}"},
             "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv family (k_igemm fwd/dgrad + k_wgrad)",
