@@ -1,6 +1,8 @@
 """Benchmark: U-Net training images/s at 512x512x1, batch 8 per GPU, fp32
 (BASELINE.json configs[1]; weak scaling over 1/2/4/8 MI355X with an RCCL
-gradient all-reduce over xGMI).
+gradient all-reduce over xGMI).  ``--dtype bf16`` runs the convolution GEMMs on
+bf16 operands with fp32 accumulation (configs[2] per GPU; with ``--channels 3
+--size 572`` the configs[4] stress shape); the default stays configs[1].
 
 A step = forward + WeightedCrossEntropyLoss + backward + all-reduce (N>1) +
 SGD(momentum 0.99) over one synthetic batch resident in HBM, exactly the body
@@ -28,6 +30,7 @@ import torch.distributed as dist  # noqa: E402
 
 METRIC = "training images/sec (512×512×1, batch=8) at 1/2/4/8 MI355X; IoU vs ref"
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 HBM_PEAK_GBS = 8000.0
 
 
@@ -42,12 +45,12 @@ def init_weights(m):
         torch.nn.init.constant_(m.bias, 0)
 
 
-def synthetic_batch(n, size, out, device, seed):
+def synthetic_batch(n, size, out, device, seed, channels=1):
     """x ~ U[0,1), target ~ Bernoulli(0.4), weight = 10 + 1/freq(class) per image
     (the committed HeLa weight maps have exactly this form)."""
     g = torch.Generator(device=device)
     g.manual_seed(seed)
-    x = torch.rand((n, 1, size, size), generator=g, device=device)
+    x = torch.rand((n, channels, size, size), generator=g, device=device)
     t = (torch.rand((n, out, out), generator=g, device=device) < 0.4).long()
     f1 = t.float().mean(dim=(1, 2), keepdim=True).clamp_min(1e-6)
     w = torch.where(t > 0, 10.0 + 1.0 / f1, 10.0 + 1.0 / (1.0 - f1).clamp_min(1e-6))
@@ -87,8 +90,9 @@ def pmc_traffic(args):
     """HBM bytes per launch per kernel family, from the committed PMC passes of
     this same command (tools/pmc_report.py --json); counters cannot be read in
     the timed run itself (separate rocprofv3 --pmc passes)."""
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", "pmc_traffic.json")
-    if args.size != 512 or args.batch != 8 or not os.path.exists(path):
+    name = "pmc_traffic.json" if args.dtype == "fp32" else f"pmc_traffic_{args.dtype}.json"
+    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", name)
+    if args.size != 512 or args.batch != 8 or args.channels != 1 or not os.path.exists(path):
         return {}
     fams = json.load(open(path))["families"]
     return {k: int(v["bytes_per_launch"]) for k, v in fams.items()}
@@ -101,6 +105,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=8, help="images per GPU")
     ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--channels", type=int, default=1, help="input channels (configs[4]: 3)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
+                    help="GEMM operand precision (bf16 = bf16-in / fp32-acc MFMA)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--tuning-report", default=None, help="write the GEMM autotuner's choices to this file")
@@ -128,16 +135,16 @@ def main():
     from unet_amd.train import Trainer
 
     torch.manual_seed(0)
-    model = UNet(n_channels=1, n_classes=2)
+    model = UNet(n_channels=args.channels, n_classes=2)
     model.apply(init_weights)
     model = model.to(device).train()
     if pg is not None:  # identical start on every rank
         for t in model.state_dict().values():
             dist.broadcast(t, 0)
     trainer = Trainer(model, args.batch, args.size, args.size, lr=1e-4, momentum=0.99, process_group=pg,
-                      overlap=not args.no_overlap)
+                      overlap=not args.no_overlap, precision=args.dtype)
     oh, ow = trainer.out_hw
-    x, t, w = synthetic_batch(args.batch, args.size, oh, device, seed=1234 + rank)
+    x, t, w = synthetic_batch(args.batch, args.size, oh, device, seed=1234 + rank, channels=args.channels)
 
     for _ in range(args.warmup):
         trainer.step(x, t, w)
@@ -175,6 +182,7 @@ def main():
         conv_ms = sum(c[0] for c in conv)
         conv_fl = sum(c[1] for c in conv)
         achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+        peak = BF16_MFMA_PEAK_TFLOPS if args.dtype == "bf16" else FP32_MFMA_PEAK_TFLOPS
         launches = sum(c[3] for c in conv)
         st = tim["stage1"]
         kernels = {k: {"ms": round(v[0], 3), "launches": v[3],
@@ -192,16 +200,18 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "fp32",
+            "dtype": args.dtype,
             "data": "synthetic: x~U[0,1) (N,1,512,512), Bernoulli(0.4) targets, 10+1/freq(class) weight maps; "
                     "kaiming fan_out init (scripts/train.py:54-61)",
-            "config": {"workload": f"U-Net train step {args.size}x{args.size}x1, batch {args.batch}/GPU, fp32: "
+            "config": {"workload": f"U-Net train step {args.size}x{args.size}x{args.channels}, batch {args.batch}/GPU, "
+                                   f"{'fp32' if args.dtype == 'fp32' else 'bf16-operand/fp32-acc'} GEMMs: "
                                    "fwd + weighted CE + bwd + SGD(0.99)" + ((f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-reduce" if world > 1 else "")),
                        "global_batch": world * args.batch, "image": args.size,
                        "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv family (k_igemm fwd/dgrad + k_wgrad)",
-                         "achieved": round(achieved, 2), "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                         "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": pmc.get("conv"),
+            "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv family (fwd/dgrad igemm + wgrad, "
+                                                    f"{args.dtype} operands)",
+                         "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                         "frac": round(achieved / peak, 4), "traffic": pmc.get("conv"),
                          "traffic_unit": "HBM bytes/launch (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, "
                                          "profiles/pmc_traffic.json)",
                          "flops_per_step": conv_fl, "launches_per_step": launches,
@@ -216,7 +226,7 @@ def main():
             from unet_amd import _lib as _ulib
             with open(args.tuning_report, "w") as f:
                 f.write(_ulib.tuning_report())
-        if world == 1 and not args.no_cpu_baseline:
+        if world == 1 and not args.no_cpu_baseline and args.channels == 1:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))
     if pg is not None:

@@ -49,8 +49,24 @@ const char* unet_last_error(void);
 typedef struct unet_plan unet_plan;
 
 /* Create a plan; returns NULL (and sets unet_last_error) for sizes the valid
- * U-Net cannot take (models/unet_model.py:189: out = in - 184 for clean sizes). */
+ * U-Net cannot take (models/unet_model.py:189: out = in - 184 for clean sizes).
+ * unet_plan_create() is unet_plan_create_ex(..., UNET_PREC_FP32). */
 unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes);
+
+/* Arithmetic of the implicit-GEMM convolutions (the 17 3x3 convs after the
+ * first, the 4 ConvTranspose2d, their input and weight gradients):
+ *  UNET_PREC_FP32  fp32 operands, exact fp32 MFMA (configs C1/C2, the parity
+ *                  configuration);
+ *  UNET_PREC_BF16  both operands rounded to bf16 (RNE) when staged, fp32
+ *                  accumulation (v_mfma_f32_32x32x16_bf16): the "bf16-in /
+ *                  fp32-acc" of configs C3/C5, what torch.autocast(bfloat16)
+ *                  asks of the reference's convolutions.
+ * Everything else -- stored activations, BatchNorm statistics, the first conv
+ * (Ci <= 4), the 1x1 head, the loss, gradients and the optimizer -- is fp32 in
+ * both. */
+enum { UNET_PREC_FP32 = 0, UNET_PREC_BF16 = 1 };
+unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int precision);
+int unet_plan_precision(const unet_plan* p);
 void unet_plan_destroy(unet_plan* p);
 /* Output spatial size and the workspace the caller must provide. */
 int unet_plan_out_hw(const unet_plan* p, int* out_h, int* out_w);
@@ -135,7 +151,10 @@ int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int 
  *                  dX chain (joined before the call returns); 0 = one stream.
  *  "force_split"   k > 1: every plan igemm runs split-K k (tests), 0 = off.
  *  "force_tile"    id > 0: every plan igemm whose shape admits tile id runs
- *                  it (tests; 1-4, 6-9 register-staged, 11-14 LDS-DMA). */
+ *                  it (tests; 1-4, 6-9 register-staged, 11-14 LDS-DMA, 21-26
+ *                  bf16 operands -- only in a UNET_PREC_BF16 plan).
+ *  "op_precision"  UNET_PREC_* of the per-op GEMM entry points below
+ *                  (unet_conv3x3_*, unet_convT2_*); default fp32. */
 int unet_set_tuning(const char* key, int value);
 /* Text report of the tuned GEMM choices (one line per shape: key, heuristic
  * time, chosen variant and time).  Copies up to len-1 bytes + NUL into buf

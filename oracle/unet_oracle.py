@@ -186,6 +186,19 @@ def hash_init(n_channels: int = 1, n_classes: int = 2, seed: int = 0,
 
 
 # ----------------------------------------------------------------------------
+# bf16 operand rounding (the HIP path's UNET_PREC_BF16 GEMMs).
+# ----------------------------------------------------------------------------
+def round_bf16(a):
+    """Round to the nearest bf16 (ties to even), as gfx950's v_cvt_pk_bf16_f32
+    and torch's float32 -> bfloat16 cast do; the value is taken as float32
+    first (the HIP path rounds fp32 activations).  Returns float64 values."""
+    f = np.ascontiguousarray(np.asarray(a, dtype=np.float32))
+    u = f.view(np.uint32).astype(np.uint64)
+    u = (u + np.uint64(0x7FFF) + ((u >> np.uint64(16)) & np.uint64(1))) & np.uint64(0xFFFF0000)
+    return u.astype(np.uint32).view(np.float32).astype(np.float64)
+
+
+# ----------------------------------------------------------------------------
 # Primitive ops (NHWC activations).
 # ----------------------------------------------------------------------------
 def conv_valid_fwd(x, w, b):
@@ -416,12 +429,32 @@ def output_size(h: int) -> int:
 class UNetOracle:
     """Restatement of UNet.forward (models/unet_model.py:105-146) with an explicit
     backward.  ``params`` maps reference state_dict names -> arrays (PyTorch
-    shapes); activations are NHWC in ``dtype``."""
+    shapes); activations are NHWC in ``dtype``.
 
-    def __init__(self, params, dtype=np.float64, bn_momentum=BN_MOMENTUM):
+    ``gemm="bf16"`` restates the HIP path's bf16-operand GEMMs (UNET_PREC_BF16,
+    the reference's convs under torch.autocast(bfloat16)): every 3x3 conv after
+    the first, every ConvTranspose2d and their input / weight gradients see both
+    operands rounded to bf16 (after the producer's BatchNorm+ReLU); products
+    are accumulated exactly.  The first conv (Ci <= 4), the 1x1 head, BatchNorm,
+    pooling, biases, the loss and every stored activation stay unrounded."""
+
+    def __init__(self, params, dtype=np.float64, bn_momentum=BN_MOMENTUM, gemm="fp32"):
+        if gemm not in ("fp32", "bf16"):
+            raise ValueError(gemm)
         self.p = OrderedDict((k, np.asarray(v)) for k, v in params.items())
         self.dtype = dtype
         self.bn_momentum = bn_momentum
+        self.gemm = gemm
+
+    def _q(self, a, on=True):
+        """GEMM operand as the HIP path sees it."""
+        return round_bf16(a).astype(self.dtype) if (on and self.gemm == "bf16") else a
+
+    def _conv_bwd(self, a_in, w, d, need_dx, quant):
+        if not (quant and self.gemm == "bf16"):
+            return conv_valid_bwd(a_in, w, d, need_dx=need_dx)
+        dx, dw, _ = conv_valid_bwd(self._q(a_in), self._q(w), self._q(d), need_dx=need_dx)
+        return dx, dw, d.reshape(-1, d.shape[-1]).sum(0)
 
     def _w(self, name):
         return self.p[name].astype(self.dtype)
@@ -432,7 +465,9 @@ class UNetOracle:
         outs = []
         a = x
         for conv_i, bn_i in (("0", "1"), ("3", "4")):
-            y = conv_valid_fwd(a, self._w(pre + conv_i + ".weight"), self._w(pre + conv_i + ".bias"))
+            q = not (pre == _dc_prefix("inc") and conv_i == "0")  # first conv: direct fp32 kernel
+            y = conv_valid_fwd(self._q(a, q), self._q(self._w(pre + conv_i + ".weight"), q),
+                               self._w(pre + conv_i + ".bias"))
             g, b = self._w(pre + bn_i + ".weight"), self._w(pre + bn_i + ".bias")
             if train:
                 z, bn_cache, mean, var_unb = bn_train_fwd(y, g, b)
@@ -460,7 +495,8 @@ class UNetOracle:
             grads[pre + bn_i + ".weight"] = dg
             grads[pre + bn_i + ".bias"] = dbt
             nd = need_dx or conv_i == "3"
-            d, dw, db = conv_valid_bwd(a_in, self._w(pre + conv_i + ".weight"), d, need_dx=nd)
+            q = not (pre == _dc_prefix("inc") and conv_i == "0")
+            d, dw, db = self._conv_bwd(a_in, self._w(pre + conv_i + ".weight"), d, nd, q)
             grads[pre + conv_i + ".weight"] = dw
             grads[pre + conv_i + ".bias"] = db
         return d
@@ -481,7 +517,7 @@ class UNetOracle:
         for k in range(1, 5):
             name = f"up{k}"
             cache[name + ".in"] = a
-            up = convT2_fwd(a, self._w(name + ".up.weight"), self._w(name + ".up.bias"))
+            up = convT2_fwd(self._q(a), self._q(self._w(name + ".up.weight")), self._w(name + ".up.bias"))
             skip = skips[4 - k]
             cs = center_crop_nhwc(skip, up.shape[1], up.shape[2])
             cache[name + ".crop"] = (skip.shape, crop_offsets(skip.shape[1], skip.shape[2], up.shape[1], up.shape[2]),
@@ -508,7 +544,9 @@ class UNetOracle:
             dskip[:, oy:oy + h, ox:ox + w, :] = dcat[..., :cs]
             dskips[4 - k] = dskip
             dup = np.ascontiguousarray(dcat[..., cs:])
-            d, dw, db = convT2_bwd(cache[name + ".in"], self._w(name + ".up.weight"), dup)
+            d, dw, db = convT2_bwd(self._q(cache[name + ".in"]), self._q(self._w(name + ".up.weight")), self._q(dup))
+            if self.gemm == "bf16":
+                db = dup.reshape(-1, dup.shape[-1]).sum(0)
             grads[name + ".up.weight"], grads[name + ".up.bias"] = dw, db
         for k in range(4, 0, -1):
             dpool = self._double_conv_bwd(_dc_prefix(f"down{k}"), d, cache, grads)

@@ -1,0 +1,189 @@
+// Device helpers shared by the fp32 (igemm.hip) and bf16 (igemm_bf16.hip)
+// implicit-GEMM kernel families: vector load/store, the consumer-side
+// BatchNorm+ReLU transform, bf16 packing, the pixel iterator of the
+// weight-gradient GEMMs and the common epilogue of every forward /
+// input-gradient GEMM tile.
+//
+// Accumulator layout (identical for v_mfma_f32_32x32x2_f32 and
+// v_mfma_f32_32x32x16_bf16 on gfx950): lane l holds column l&31 of a 32x32 tile,
+// register r holds row (r&3) + 8*(r>>2) + 4*(l>>5).
+#pragma once
+#include "unet_internal.h"
+
+namespace unet {
+
+typedef float floatx16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2_t __attribute__((ext_vector_type(2)));
+typedef float floatx2_t __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
+
+__device__ __forceinline__ float4 affine_relu4(float4 v, float4 a, float4 b) {
+  v.x = fmaxf(fmaf(v.x, a.x, b.x), 0.f);
+  v.y = fmaxf(fmaf(v.y, a.y, b.y), 0.f);
+  v.z = fmaxf(fmaf(v.z, a.z, b.z), 0.f);
+  v.w = fmaxf(fmaf(v.w, a.w, b.w), 0.f);
+  return v;
+}
+
+__device__ __forceinline__ float getc(const float4& v, int c) {
+  return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+}
+
+// two fp32 -> two bf16 (round to nearest even, v_cvt_pk_bf16_f32), low half = a
+__device__ __forceinline__ unsigned bf16pack(float a, float b) {
+  const bf16x2_t v = __builtin_convertvector((floatx2_t){a, b}, bf16x2_t);
+  return __builtin_bit_cast(unsigned, v);
+}
+__device__ __forceinline__ uint4 bf16pack8(float4 a, float4 b) {
+  return make_uint4(bf16pack(a.x, a.y), bf16pack(a.z, a.w), bf16pack(b.x, b.y), bf16pack(b.z, b.w));
+}
+
+// Pixel iterator over an (nimg, Hg, Wg) grid (weight-gradient GEMMs walk their
+// staged pixel rows incrementally, no divisions in the loop).
+struct PixIt {
+  int n, y, x;
+  __device__ __forceinline__ void init(int p, int Hg, int Wg) {
+    const int hw = Hg * Wg;
+    n = p / hw;
+    const int r = p - n * hw;
+    y = r / Wg;
+    x = r - y * Wg;
+  }
+  __device__ __forceinline__ void advance(int d, int Hg, int Wg) {
+    x += d;
+    while (x >= Wg) {
+      x -= Wg;
+      if (++y == Hg) { y = 0; ++n; }
+    }
+  }
+  __device__ __forceinline__ void next(int Hg, int Wg) {
+    if (++x == Wg) {
+      x = 0;
+      if (++y == Hg) { y = 0; ++n; }
+    }
+  }
+};
+
+// Split-K partial store or the full epilogue of an implicit-GEMM tile: bias,
+// destination mapping (linear / pixel shuffle / cropped), ReLU mask + BN-bwd
+// statistics, BN statistics, concat column sums.  `red` is WM*3*BN floats of
+// LDS that no wave reads or writes any more (a barrier precedes its use).
+template <int BM, int BN, int WM, int WN, int NT>
+__device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&acc)[BM / (WM * 32)][BN / (WN * 32)],
+                                             int m0, int n0, int wm, int wn, int tid, float* red) {
+  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
+  const Gather& g = args.a;
+  const int M = args.M;
+  const int lane = tid & 63, h = lane >> 5, li = lane & 31;
+  const int HWg = g.Hg * g.Wg;
+  const int N = args.N;
+  if (args.ksplit > 1) {  // raw partial tile; k_splitk_epi finishes
+    float* sl = args.slab + (size_t)blockIdx.z * M * N;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * TN * 32 + j * 32 + li;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+          if (m < M) sl[(size_t)m * N + col] = acc[i][j][r];
+        }
+    }
+    return;
+  }
+
+  // ------------------------------ epilogue ---------------------------------
+  const Epilogue& e = args.e;
+  float s1[TN], s2[TN], t1[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; t1[j] = 0.f; }
+
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * TN * 32 + j * 32 + li;
+    const float bias = e.bias ? e.bias[e.shuffle_co ? col % e.shuffle_co : col] : 0.f;
+    const bool second = col >= e.n_split;
+    const Dst& d = second ? e.d[1] : e.d[0];
+    const int dcol = second ? col - e.n_split : col;
+    float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
+    const bool bwd_mask = (e.yref != nullptr) && !second;
+    if (bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
+    const bool linear = !e.shuffle_co && d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int m = m0 + row;
+        if (m >= M) continue;
+        float v = acc[i][j][r] + bias;
+        size_t idx;
+        if (linear) {
+          idx = (size_t)m * d.C + dcol;
+        } else if (e.shuffle_co) {
+          const int ab = dcol / e.shuffle_co, co = dcol - ab * e.shuffle_co;
+          const int n = m / HWg, rr = m - n * HWg;
+          const int y = rr / g.Wg, x = rr - y * g.Wg;
+          idx = ((size_t)(n * d.H + 2 * y + (ab >> 1) + d.oy) * d.W + 2 * x + (ab & 1) + d.ox) * d.C + co;
+        } else {
+          const int n = m / HWg, rr = m - n * HWg;
+          const int y = rr / g.Wg, x = rr - y * g.Wg;
+          idx = ((size_t)(n * d.H + y + d.oy) * d.W + x + d.ox) * d.C + dcol;
+        }
+        if (bwd_mask) {
+          const float yv = e.yref[idx];
+          v = (fmaf(yv, bsc, bsh) > 0.f) ? v : 0.f;
+          s1[j] += v;
+          s2[j] += v * ((yv - bmu) * bis);
+        } else if (e.stats) {
+          s1[j] += v;
+          s2[j] += v * v;
+        } else if (second && e.colsum1) {
+          t1[j] += v;
+        }
+        d.ptr[idx] = v;
+      }
+    }
+  }
+  const bool want_stats = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
+  if (!want_stats) return;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    s1[j] += __shfl_xor(s1[j], 32);
+    s2[j] += __shfl_xor(s2[j], 32);
+    t1[j] += __shfl_xor(t1[j], 32);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int lc = wn * TN * 32 + j * 32 + li;
+      red[(wm * 3 + 0) * BN + lc] = s1[j];
+      red[(wm * 3 + 1) * BN + lc] = s2[j];
+      red[(wm * 3 + 2) * BN + lc] = t1[j];
+    }
+  }
+  __syncthreads();
+  const int grp = blockIdx.x % kStatGroups;
+  const int nsplit = min(e.n_split, N);
+  for (int lc = tid; lc < BN; lc += NT) {
+    float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) { a += red[(w * 3 + 0) * BN + lc]; b += red[(w * 3 + 1) * BN + lc]; c += red[(w * 3 + 2) * BN + lc]; }
+    const int col = n0 + lc;
+    if (col < nsplit) {
+      double* st = e.yref ? e.bstats : e.stats;
+      if (st) {
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b);
+      }
+    } else if (e.colsum1) {
+      const int n2 = N - nsplit;
+      atomicAdd(e.colsum1 + (size_t)grp * n2 + (col - nsplit), (double)c);
+    }
+  }
+}
+
+}  // namespace unet

@@ -17,33 +17,9 @@
 // latency hides under its own 32 MFMAs (2048 cycles) plus its SIMD partners'.
 #include <cstdlib>
 
-#include "unet_internal.h"
+#include "gemm_common.h"
 
 namespace unet {
-
-typedef float floatx16 __attribute__((ext_vector_type(16)));
-
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
-
-__device__ __forceinline__ float4 affine_relu4(float4 v, float4 a, float4 b) {
-  v.x = fmaxf(fmaf(v.x, a.x, b.x), 0.f);
-  v.y = fmaxf(fmaf(v.y, a.y, b.y), 0.f);
-  v.z = fmaxf(fmaf(v.z, a.z, b.z), 0.f);
-  v.w = fmaxf(fmaf(v.w, a.w, b.w), 0.f);
-  return v;
-}
-
-// ---------------------------------------------------------------------------
-// k_igemm: C[m][n] = sum_k A[m][k] * B[n][k];  A gathered, B packed [N][K].
-// WM x WN waves, each owning a (TM*32) x (TN*32) block of 32x32 MFMA tiles;
-// BK = 16 or 32 k per LDS stage.  MFMA step s of a stage takes k = s (lanes
-// 0-31) and k = BK/2 + s (lanes 32-63) on both operands, so each lane reads
-// its BK/2 consecutive k of a row with ds_read_b128.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ float getc(const float4& v, int c) {
-  return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
-}
 
 // Occupancy the register allocator must preserve: as many workgroups as the
 // LDS footprint admits per CU (without it hipcc moves the accumulators to
@@ -54,126 +30,6 @@ constexpr int igemm_minw(int BM, int BN, int WM, int WN, int BK) {
   if (blocks > 8) blocks = 8;
   int w = blocks * WM * WN * 64 / 256;
   return w < 1 ? 1 : (w > 8 ? 8 : w);
-}
-
-// Split-K partial store or the full epilogue of a k_igemm-family tile: bias,
-// destination mapping (linear / pixel shuffle / cropped), ReLU mask + BN-bwd
-// statistics, BN statistics, concat column sums.  `red` is WM*3*BN floats of
-// LDS that no wave reads or writes any more (a barrier precedes its use).
-template <int BM, int BN, int WM, int WN, int NT>
-__device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&acc)[BM / (WM * 32)][BN / (WN * 32)],
-                                             int m0, int n0, int wm, int wn, int tid, float* red) {
-  constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
-  const Gather& g = args.a;
-  const int M = args.M;
-  const int lane = tid & 63, h = lane >> 5, li = lane & 31;
-  const int HWg = g.Hg * g.Wg;
-  const int N = args.N;
-  if (args.ksplit > 1) {  // raw partial tile; k_splitk_epi finishes
-    float* sl = args.slab + (size_t)blockIdx.z * M * N;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = n0 + wn * TN * 32 + j * 32 + li;
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (m < M) sl[(size_t)m * N + col] = acc[i][j][r];
-        }
-    }
-    return;
-  }
-
-  // ------------------------------ epilogue ---------------------------------
-  const Epilogue& e = args.e;
-  float s1[TN], s2[TN], t1[TN];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; t1[j] = 0.f; }
-
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + wn * TN * 32 + j * 32 + li;
-    const float bias = e.bias ? e.bias[e.shuffle_co ? col % e.shuffle_co : col] : 0.f;
-    const bool second = col >= e.n_split;
-    const Dst& d = second ? e.d[1] : e.d[0];
-    const int dcol = second ? col - e.n_split : col;
-    float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
-    const bool bwd_mask = (e.yref != nullptr) && !second;
-    if (bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
-    const bool linear = !e.shuffle_co && d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int m = m0 + row;
-        if (m >= M) continue;
-        float v = acc[i][j][r] + bias;
-        size_t idx;
-        if (linear) {
-          idx = (size_t)m * d.C + dcol;
-        } else if (e.shuffle_co) {
-          const int ab = dcol / e.shuffle_co, co = dcol - ab * e.shuffle_co;
-          const int n = m / HWg, rr = m - n * HWg;
-          const int y = rr / g.Wg, x = rr - y * g.Wg;
-          idx = ((size_t)(n * d.H + 2 * y + (ab >> 1) + d.oy) * d.W + 2 * x + (ab & 1) + d.ox) * d.C + co;
-        } else {
-          const int n = m / HWg, rr = m - n * HWg;
-          const int y = rr / g.Wg, x = rr - y * g.Wg;
-          idx = ((size_t)(n * d.H + y + d.oy) * d.W + x + d.ox) * d.C + dcol;
-        }
-        if (bwd_mask) {
-          const float yv = e.yref[idx];
-          v = (fmaf(yv, bsc, bsh) > 0.f) ? v : 0.f;
-          s1[j] += v;
-          s2[j] += v * ((yv - bmu) * bis);
-        } else if (e.stats) {
-          s1[j] += v;
-          s2[j] += v * v;
-        } else if (second && e.colsum1) {
-          t1[j] += v;
-        }
-        d.ptr[idx] = v;
-      }
-    }
-  }
-  const bool want_stats = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
-  if (!want_stats) return;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    s1[j] += __shfl_xor(s1[j], 32);
-    s2[j] += __shfl_xor(s2[j], 32);
-    t1[j] += __shfl_xor(t1[j], 32);
-  }
-  if (h == 0) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int lc = wn * TN * 32 + j * 32 + li;
-      red[(wm * 3 + 0) * BN + lc] = s1[j];
-      red[(wm * 3 + 1) * BN + lc] = s2[j];
-      red[(wm * 3 + 2) * BN + lc] = t1[j];
-    }
-  }
-  __syncthreads();
-  const int grp = blockIdx.x % kStatGroups;
-  const int nsplit = min(e.n_split, N);
-  for (int lc = tid; lc < BN; lc += NT) {
-    float a = 0.f, b = 0.f, c = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) { a += red[(w * 3 + 0) * BN + lc]; b += red[(w * 3 + 1) * BN + lc]; c += red[(w * 3 + 2) * BN + lc]; }
-    const int col = n0 + lc;
-    if (col < nsplit) {
-      double* st = e.yref ? e.bstats : e.stats;
-      if (st) {
-        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
-        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b);
-      }
-    } else if (e.colsum1) {
-      const int n2 = N - nsplit;
-      atomicAdd(e.colsum1 + (size_t)grp * n2 + (col - nsplit), (double)c);
-    }
-  }
 }
 
 // ABL: ablation switches for tools/igemm_bench.cpp only (0 in the library):
@@ -694,23 +550,6 @@ __global__ __launch_bounds__(256) void k_splitk_epi(const IgemmArgs args) {
 // Each thread owns fixed columns (channel slice of A; (tap, channel) of B) and
 // walks its staged pixel rows incrementally (no divisions in the loop).
 // ---------------------------------------------------------------------------
-struct PixIt {
-  int n, y, x;
-  __device__ __forceinline__ void init(int p, int Hg, int Wg) {
-    const int hw = Hg * Wg;
-    n = p / hw;
-    const int r = p - n * hw;
-    y = r / Wg;
-    x = r - y * Wg;
-  }
-  __device__ __forceinline__ void advance(int d, int Hg, int Wg) {
-    x += d;
-    while (x >= Wg) {
-      x -= Wg;
-      if (++y == Hg) { y = 0; ++n; }
-    }
-  }
-};
 
 template <int BM, int BN, int WM, int WN>
 __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
@@ -886,13 +725,26 @@ static TileInfo tile_info(int id) {
     case 12: return {128, 128, 16, 3};
     case 13: return {64, 128, 16, 4};
     case 14: return {128, 64, 16, 4};
+    // bf16 operands, register staged (k_igemm_bf, igemm_bf16.hip)
+    case 21: return {256, 128, 32, 2};
+    case 22: return {128, 128, 32, 3};
+    case 23: return {128, 64, 32, 4};
+    case 24: return {64, 128, 32, 4};
+    case 25: return {256, 64, 32, 2};
+    case 26: return {128, 256, 32, 2};
     default: return {0, 0, 0, 0};
   }
 }
 
+static bool is_bf16_tile(int tile) { return tile >= 21 && tile <= 26; }
+
+// A tile applies when the shape divides and the packed B operand is in the
+// tile's precision (fp32 `b` for tiles 1-14, bf16 `bh` for 21-26).
 bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   const TileInfo t = tile_info(tile);
-  return t.bm > 0 && a.N % t.bn == 0 && a.K % t.bk == 0 && a.a.Cg % t.bk == 0 && a.a.c_split % t.bk == 0;
+  const bool prec_ok = is_bf16_tile(tile) ? a.bh != nullptr : a.b != nullptr;
+  return t.bm > 0 && prec_ok && a.N % t.bn == 0 && a.K % t.bk == 0 && a.a.Cg % t.bk == 0 &&
+         a.a.c_split % t.bk == 0;
 }
 long long igemm_tile_count(const IgemmArgs& a, int tile) {
   const TileInfo t = tile_info(tile);
@@ -945,6 +797,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 12: return go_igemm_g<128, 128, 2, 2>(a, s);
     case 13: return go_igemm_g<64, 128, 2, 2>(a, s);
     case 14: return go_igemm_g<128, 64, 2, 2>(a, s);
+    case 21: case 22: case 23: case 24: case 25: case 26: return go_igemm_bf16(a, s, tile);
     default: return hipErrorInvalidValue;
   }
 }
@@ -962,6 +815,17 @@ static bool igemm_args_ok(const IgemmArgs& a) {
 static int heuristic_tile(const IgemmArgs& a) {
   if (g_tune_igemm > 0 && igemm_tile_fits(a, g_tune_igemm)) return g_tune_igemm;
   const long long cus = num_cus();
+  if (a.bh != nullptr) {  // bf16 operands: same shape rules over the bf16 tiles
+    if (a.K % 32 || a.a.Cg % 32 || a.a.c_split % 32) return -1;
+    if (a.N % 128 == 0) {
+      const long long t256 = ((a.M + 255) / 256) * (long long)(a.N / 128);
+      const long long t128 = ((a.M + 127) / 128) * (long long)(a.N / 128);
+      if (a.N >= 256 && t256 >= 3 * cus / 2) return 21;
+      if (t128 >= 2 * cus) return 22;
+      return 24;
+    }
+    return a.N % 64 == 0 ? 23 : -1;
+  }
   if (a.N % 128 == 0) {
     const long long t256 = ((a.M + 255) / 256) * (long long)(a.N / 128);
     const long long t128 = ((a.M + 127) / 128) * (long long)(a.N / 128);
@@ -999,16 +863,18 @@ hipError_t launch_igemm_v(const IgemmArgs& a0, hipStream_t s, GemmChoice c) {
   return hipGetLastError();
 }
 
-// wgrad tile table: id -> (BM, BN)
+// wgrad tile table: id -> (BM, BN); 0-4 fp32 (k_wgrad), 10-14 bf16 (k_wgrad_bf)
 static void wgrad_tile(int id, int& bm, int& bn) {
   static const int t[5][2] = {{128, 128}, {128, 192}, {64, 192}, {64, 128}, {64, 64}};
-  bm = (id >= 0 && id < 5) ? t[id][0] : 0;
-  bn = (id >= 0 && id < 5) ? t[id][1] : 0;
+  static const int tb[5][2] = {{128, 128}, {128, 192}, {64, 128}, {64, 64}, {256, 128}};
+  bm = bn = 0;
+  if (id >= 0 && id < 5) { bm = t[id][0]; bn = t[id][1]; }
+  if (id >= 10 && id < 15) { bm = tb[id - 10][0]; bn = tb[id - 10][1]; }
 }
 bool wgrad_tile_fits(const WgradArgs& a, int tile) {
   int bm, bn;
   wgrad_tile(tile, bm, bn);
-  return bm > 0 && a.Mo % bm == 0 && a.No % bn == 0;
+  return bm > 0 && (tile >= 10) == (a.bf16 != 0) && a.Mo % bm == 0 && a.No % bn == 0;
 }
 
 hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
@@ -1016,7 +882,11 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   if (a.Mo % 64 != 0 || a.P <= 0 || a.gb.Cg % 4 != 0 || a.gb.c_split % 4 != 0 || a.ga.Cg % 4 != 0)
     return hipErrorInvalidValue;
   int tile = c.tile;
-  if (tile < 0) {
+  if (tile < 0 && a.bf16) {
+    if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 10;
+    else if (a.No % 128 == 0) tile = 12;
+    else tile = 13;
+  } else if (tile < 0) {
     if (g_tune_wgrad == 1) tile = 4;  // force the small tile (A/B tests)
     else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 0;
     else if (a.Mo % 128 == 0 && a.No % 192 == 0) tile = 1;
@@ -1036,10 +906,12 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   if (splits > max_splits) splits = max_splits;
   if (splits < 1) splits = 1;
   int pps = (a.P + splits - 1) / splits;
-  pps = (pps + 15) / 16 * 16;
+  const int kq = tile >= 10 ? 32 : 16;  // pixels per K-step
+  pps = (pps + kq - 1) / kq * kq;
   splits = (a.P + pps - 1) / pps;
   a.pix_per_split = pps;
   dim3 grid(a.Mo / bm, a.No / bn, splits);
+  if (tile >= 10) return go_wgrad_bf16(a, s, tile, grid);
   switch (tile) {
     case 0: hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
     case 1: hipLaunchKernelGGL((k_wgrad<128, 192, 2, 2>), grid, dim3(256), 0, s, a); break;

@@ -19,6 +19,20 @@ hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream
 namespace {
 thread_local std::string g_op_err;
 inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
+// unet_set_tuning("op_precision", UNET_PREC_*): GEMM arithmetic of the per-op
+// entry points (the plan has its own, unet_plan_create_ex)
+int g_op_prec = UNET_PREC_FP32;
+
+// bf16 per-op GEMMs: round the packed fp32 B (n elements) into `scratch` and
+// point the GEMM at it
+hipError_t op_b_to_bf16(IgemmArgs& a, size_t n, void* scratch, hipStream_t s) {
+  if (g_op_prec != UNET_PREC_BF16) return hipSuccess;
+  uint16_t* bh = reinterpret_cast<uint16_t*>(scratch);
+  hipError_t e = launch_f2bf(a.b, bh, n, s);
+  a.bh = bh;
+  a.b = nullptr;
+  return e;
+}
 }  // namespace
 
 #define OPCK(x)                                                           \
@@ -62,6 +76,8 @@ int unet_conv3x3_fwd(const float* x, int n, int h, int w, int ci, const float* w
   a.K = 9 * ci;
   a.e.bias = bias;
   a.e.d[0] = Dst{y, h - 2, w - 2, co, 0, 0};
+  OPCK(op_b_to_bf16(a, 9 * (size_t)ci * co, reinterpret_cast<char*>(ws) + al256(sizeof(float) * 9 * (size_t)ci * co),
+                    s));
   OPCK(launch_igemm(a, s));
   return 0;
 }
@@ -98,6 +114,7 @@ int unet_conv3x3_dgrad(const float* dy, int n, int h, int w, int ci, const float
   a.N = ci;
   a.K = 9 * co;
   a.e.d[0] = Dst{dx, h, w, ci, 0, 0};
+  OPCK(op_b_to_bf16(a, 9 * (size_t)ci * co, wf, s));
   OPCK(launch_igemm(a, s));
   return 0;
 }
@@ -138,6 +155,7 @@ int unet_conv3x3_wgrad(const float* x, const float* dy, int n, int h, int w, int
   a.No = 9 * ci;
   a.P = n * (h - 2) * (w - 2);
   a.out = dwp;
+  a.bf16 = g_op_prec == UNET_PREC_BF16;
   OPCK(launch_wgrad(a, s));
   OPCK(launch_permute_last2(dwp, co, 9, ci, dw, s));
   if (db) {
@@ -174,6 +192,7 @@ int unet_convT2_fwd(const float* x, int n, int h, int w, int ci, const float* wt
   a.e.bias = bias;
   a.e.shuffle_co = co;
   a.e.d[0] = Dst{y, 2 * h, 2 * w, co, 0, 0};
+  OPCK(op_b_to_bf16(a, 4 * (size_t)ci * co, p + 2 * al256(sizeof(float) * 4 * (size_t)ci * co), s));
   OPCK(launch_igemm(a, s));
   return 0;
 }
@@ -207,6 +226,7 @@ int unet_convT2_bwd(const float* x, const float* dy, int n, int h, int w, int ci
   a.N = ci;
   a.K = 4 * co;
   a.e.d[0] = Dst{dx, h, w, ci, 0, 0};
+  OPCK(op_b_to_bf16(a, 4 * (size_t)ci * co, p + 3 * wb + al256(sizeof(double) * kStatGroups * 2 * co), s));
   OPCK(launch_igemm(a, s));
   OPCK(hipMemsetAsync(dwp, 0, sizeof(float) * 4 * (size_t)ci * co, s));
   WgradArgs g;
@@ -231,6 +251,7 @@ int unet_convT2_bwd(const float* x, const float* dy, int n, int h, int w, int ci
   g.No = 4 * co;
   g.P = n * h * w;
   g.out = dwp;
+  g.bf16 = g_op_prec == UNET_PREC_BF16;
   OPCK(launch_wgrad(g, s));
   OPCK(launch_permute_last2(dwp, ci, 4, co, dw, s));
   OPCK(hipMemsetAsync(st2, 0, sizeof(double) * kStatGroups * 2 * co, s));
@@ -322,7 +343,10 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "force_split") g_force_split = value;
   else if (k == "force_tile") g_force_tile = value;
   else if (k == "concurrent") g_concurrent = value;
-  else return -EINVAL;
+  else if (k == "op_precision") {
+    if (value != UNET_PREC_FP32 && value != UNET_PREC_BF16) return -EINVAL;
+    g_op_prec = value;
+  } else return -EINVAL;
   return 0;
 }
 

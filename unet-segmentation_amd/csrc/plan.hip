@@ -84,6 +84,11 @@ double conv_flops(const Conv& c, int n) { return 2.0 * n * c.ho * c.wo * (double
 
 struct unet_plan {
   int n = 0, cin = 0, h = 0, w = 0, ncls = 0, ho = 0, wo = 0;
+  int prec = UNET_PREC_FP32;  // GEMM operand precision (include/unet_hip.h)
+  // every packed GEMM weight matrix (conv wf/wd, convT wf/wd) lies in one
+  // contiguous fp32 region; with bf16 GEMMs its RNE copy is `pack16` (same
+  // element offsets), refreshed by one conversion launch per forward
+  Buf pack_region, pack16;
   Conv L[18];
   ConvT T[4];
   Pool P[4];
@@ -175,26 +180,26 @@ int env_autotune() { return unet::g_autotune; }
 constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 
 std::string igemm_key(const IgemmArgs& a) {
-  char b[192];
+  char b[200];
   const Epilogue& e = a.e;
   const int epi = (e.shuffle_co ? 1 : 0) | (e.stats ? 2 : 0) | (e.yref ? 4 : 0) | (e.colsum1 ? 8 : 0) |
                   (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0);
-  snprintf(b, sizeof b, "igemm M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d", a.M, a.N, a.K, a.a.Cg,
-           a.a.taps_h, a.a.taps_w, a.a.stride, a.a.Hg, a.a.Wg, epi);
+  snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d", a.bh ? "_bf16" : "", a.M,
+           a.N, a.K, a.a.Cg, a.a.taps_h, a.a.taps_w, a.a.stride, a.a.Hg, a.a.Wg, epi);
   return b;
 }
 
 std::string wgrad_key(const WgradArgs& a) {
   char b[192];
-  snprintf(b, sizeof b, "wgrad Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d", a.Mo, a.No, a.P, a.gb.Cg,
-           a.gb.taps_h, a.gb.taps_w, a.gb.stride, a.gb.Hg, a.gb.Wg);
+  snprintf(b, sizeof b, "wgrad%s Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d", a.bf16 ? "_bf16" : "", a.Mo,
+           a.No, a.P, a.gb.Cg, a.gb.taps_h, a.gb.taps_w, a.gb.stride, a.gb.Hg, a.gb.Wg);
   return b;
 }
 
 std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) {
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
-  for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14}) {
+  for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 21, 22, 23, 24, 25, 26}) {  // fits() filters by precision
     if (!igemm_tile_fits(a, t)) continue;
     v.push_back({t, 1});
     const long long cnt = igemm_tile_count(a, t);
@@ -210,7 +215,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
 
 std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   std::vector<GemmChoice> v;
-  for (int t = 0; t < 5; ++t) {
+  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14}) {  // fits() filters by precision
     if (!wgrad_tile_fits(a, t)) continue;
     for (int per_cu : {4, 8, 16}) v.push_back({t, per_cu});
   }
@@ -260,7 +265,7 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
     if (unet::g_force_tile > 0) {
       if (igemm_tile_fits(a, unet::g_force_tile)) return GemmChoice{unet::g_force_tile, ks};
     }
-    for (int t : {4, 1, 2, 8})
+    for (int t : {4, 1, 2, 8, 21, 22, 24, 23})
       if (igemm_tile_fits(a, t)) return GemmChoice{t, ks};
     return GemmChoice{};
   }
@@ -320,10 +325,20 @@ GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
 
 hipError_t run_igemm(const Ctx& c, IgemmArgs a) {
   a.slab = c.f(c.p->slab);
+  if (c.p->prec == UNET_PREC_BF16) {  // B -> its bf16 copy at the same element offset
+    const char* b = reinterpret_cast<const char*>(a.b);
+    const char* base = c.ws + c.p->pack_region.off;
+    if (b < base || b >= base + c.p->pack_region.bytes) return hipErrorInvalidValue;
+    a.bh = reinterpret_cast<const uint16_t*>(c.ws + c.p->pack16.off) + (b - base) / sizeof(float);
+    a.b = nullptr;
+  }
   return launch_igemm_v(a, c.s, choose_igemm(c, a));
 }
 
-hipError_t run_wgrad(const Ctx& c, const WgradArgs& a) { return launch_wgrad_v(a, c.s, choose_wgrad(c, a)); }
+hipError_t run_wgrad(const Ctx& c, WgradArgs a) {
+  a.bf16 = c.p->prec == UNET_PREC_BF16;
+  return launch_wgrad_v(a, c.s, choose_wgrad(c, a));
+}
 
 Src src_of(const Ctx& c, const Conv& L, bool transform) {
   Src s;
@@ -400,6 +415,8 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       ConvT& T = p->T[k];
       CK(launch_pack_convT(P<float>(prm, T.pw), T.ci, T.co, c.f(T.wf), c.f(T.wd), s));
     }
+    if (p->prec == UNET_PREC_BF16)
+      CK(launch_f2bf(c.f(p->pack_region), reinterpret_cast<uint16_t*>(c.u8(p->pack16)), p->pack_region.bytes / 4, s));
   }
   if (!train) {
     for (int l = 0; l < 18; ++l) {
@@ -693,15 +710,26 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
 // =========================== C-ABI =======================================
 extern "C" {
 
-const char* unet_version(void) { return "unet_hip 0.1 gfx950 fp32-mfma"; }
+const char* unet_version(void) { return "unet_hip 0.2 gfx950 fp32/bf16-mfma"; }
 const char* unet_last_error(void) { return g_err.c_str(); }
 
 unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
+  return unet_plan_create_ex(n, c_in, h, w, n_classes, UNET_PREC_FP32);
+}
+
+int unet_plan_precision(const unet_plan* p) { return p ? p->prec : -EINVAL; }
+
+unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int prec) {
   if (n < 1 || c_in < 1 || c_in > 4 || n_classes < 1 || n_classes > 4) {
     set_err("unet_plan_create: need n>=1, 1<=c_in<=4, 1<=n_classes<=4");
     return nullptr;
   }
+  if (prec != UNET_PREC_FP32 && prec != UNET_PREC_BF16) {
+    set_err("unet_plan_create_ex: precision must be UNET_PREC_FP32 or UNET_PREC_BF16");
+    return nullptr;
+  }
   auto* p = new unet_plan();
+  p->prec = prec;
   p->n = n;
   p->cin = c_in;
   p->h = h;
@@ -822,6 +850,22 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
     p->slab = al.take(std::min(mx, kSlabBudget));
     p->tune_scratch = al.take(wmax);
   }
+  {
+    const size_t pack_start = al.top;
+    for (int l = 1; l < 18; ++l) {
+      Conv& L = p->L[l];
+      L.wf = al.take(fsz(9LL * L.co * L.ci));
+      L.wd = al.take(fsz(9LL * L.co * L.ci));
+    }
+    for (int k = 0; k < 4; ++k) {
+      ConvT& T = p->T[k];
+      T.wf = al.take(fsz(4LL * T.co * T.ci));
+      T.wd = al.take(fsz(4LL * T.co * T.ci));
+    }
+    p->pack_region.off = pack_start;
+    p->pack_region.bytes = al.top - pack_start;
+    if (prec == UNET_PREC_BF16) p->pack16 = al.take(p->pack_region.bytes / 2);
+  }
   for (int l = 0; l < 18; ++l) {
     Conv& L = p->L[l];
     const long long pix = (long long)n * L.ho * L.wo;
@@ -831,10 +875,6 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
     L.scale = al.take(fsz(L.co));
     L.shift = al.take(fsz(L.co));
     L.coef = al.take(fsz(4LL * L.co));
-    if (l > 0) {
-      L.wf = al.take(fsz(9LL * L.co * L.ci));
-      L.wd = al.take(fsz(9LL * L.co * L.ci));
-    }
     L.dz = al.take(fsz(pix * L.co));
     L.dyp = al.take(fsz((long long)n * (L.ho + 4) * (L.wo + 4) * L.co));
   }
@@ -843,8 +883,6 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
     const long long opix = (long long)n * 4 * T.h * T.w;
     T.u = al.take(fsz(opix * T.co));
     T.du = al.take(fsz(opix * T.co));
-    T.wf = al.take(fsz(4LL * T.co * T.ci));
-    T.wd = al.take(fsz(4LL * T.co * T.ci));
     Skip& sk = p->S[k];
     sk.d = al.take(fsz((long long)n * sk.th * sk.tw * sk.c));
   }

@@ -65,7 +65,9 @@ constexpr int kStatGroups = 64;  // fp64 atomic accumulators are spread over gro
 
 struct IgemmArgs {
   Gather a;          // A rows (M = nimg*Hg*Wg pixels), K = taps*Cg
-  const float* b;    // packed B[N][K] (k contiguous)
+  const float* b = nullptr;      // packed B[N][K] (k contiguous), fp32 tiles
+  const uint16_t* bh = nullptr;  // the same packed B in bf16, bf16 tiles (A is
+                                 // rounded to bf16 when staged)
   int M, N, K;
   Epilogue e;
   // split-K: > 1 slices the K chunks over blockIdx.z; raw partial tiles go to
@@ -82,12 +84,14 @@ struct WgradArgs {
   int P;             // pixels
   int pix_per_split;
   float* out;        // [Mo][No] fp32, accumulated with atomics (zeroed by caller)
+  int bf16 = 0;      // 1: operands rounded to bf16 when staged (bf16 tiles 10-14)
 };
 
 // ---------------- launchers (kernels.hip) ----------------
 // Variant of a GEMM launch.  igemm: tile id (1-4, 6-9 register-staged,
-// 11-14 LDS-DMA staged; see igemm.hip) and K
-// split; wgrad: tile id (0-4) and target workgroups per CU of the pixel split.
+// 11-14 LDS-DMA staged, 21-26 bf16 operands; see igemm.hip) and K
+// split; wgrad: tile id (0-4 fp32, 10-14 bf16) and target workgroups per CU of
+// the pixel split.
 // tile < 0 = built-in heuristic.  Chosen per launch site by the plan's autotuner.
 struct GemmChoice {
   int tile = -1;
@@ -104,6 +108,11 @@ size_t igemm_slab_bytes(const IgemmArgs& a, int ksplit);
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s);  // heuristic
 hipError_t launch_wgrad_v(const WgradArgs& a, hipStream_t s, GemmChoice c);
 bool wgrad_tile_fits(const WgradArgs& a, int tile);
+// bf16-operand kernels (igemm_bf16.hip), dispatched by the launchers above
+hipError_t go_igemm_bf16(const IgemmArgs& a, hipStream_t s, int tile);
+hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid);
+// out[i] = bf16(in[i]) (RNE), n a multiple of 4, both 16-B aligned
+hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s);
 
 // inc.c0: Ci in {1,2,3,4} direct conv from an NCHW input; y NHWC (Co = 64 multiple).
 hipError_t launch_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w,

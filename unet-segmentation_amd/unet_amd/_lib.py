@@ -22,6 +22,8 @@ SIGNATURES = {
     "unet_version": (ctypes.c_char_p, []),
     "unet_last_error": (ctypes.c_char_p, []),
     "unet_plan_create": (_vp, [_i, _i, _i, _i, _i]),
+    "unet_plan_create_ex": (_vp, [_i, _i, _i, _i, _i, _i]),
+    "unet_plan_precision": (_i, [_vp]),
     "unet_plan_destroy": (None, [_vp]),
     "unet_plan_out_hw": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "unet_plan_workspace_bytes": (_sz, [_vp]),

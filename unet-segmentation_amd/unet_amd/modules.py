@@ -7,7 +7,11 @@ Mirrors the reference interface:
   from scripts/train.py:54-61, ``.parameters()`` for optim.SGD and
   ``.train()/.eval()`` behave as in the reference).  The submodules are
   parameter holders; ``UNet.forward`` runs the whole network as one HIP plan
-  (NHWC activations, fp32 MFMA implicit GEMM) inside one autograd node.
+  (NHWC activations, MFMA implicit GEMM) inside one autograd node.
+  GEMM precision: fp32 by default; bf16 operands with fp32 accumulation inside
+  ``torch.autocast("cuda", dtype=torch.bfloat16)`` (the reference's convs under
+  autocast) or when ``model.precision = "bf16"``.  Activations, BatchNorm,
+  logits and gradients stay fp32 either way.
 * ``WeightedCrossEntropyLoss()(inputs, targets, weight_maps)`` --
   utils/losses.py:29-57, fused forward+backward kernel.
 
@@ -102,12 +106,12 @@ class _Runner:
     def __setstate__(self, state):
         self.__init__()
 
-    def plan(self, n, c, h, w, k):
-        key = (n, c, h, w, k)
+    def plan(self, n, c, h, w, k, precision="fp32"):
+        key = (n, c, h, w, k, precision)
         with self.lock:
             p = self.plans.get(key)
             if p is None:
-                p = Plan(n, c, h, w, k)
+                p = Plan(n, c, h, w, k, precision)
                 self.plans[key] = p
             return p
 
@@ -123,8 +127,8 @@ def _check_tensor(t, name):
 
 class _UNetFunction(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, module, train, *params):
-        plan = module._runner.plan(x.shape[0], x.shape[1], x.shape[2], x.shape[3], module.n_classes)
+    def forward(ctx, x, module, train, precision, *params):
+        plan = module._runner.plan(x.shape[0], x.shape[1], x.shape[2], x.shape[3], module.n_classes, precision)
         state = module._state_tensors()
         for name, t in state:
             if t.is_floating_point():
@@ -151,7 +155,7 @@ class _UNetFunction(torch.autograd.Function):
         grads = [torch.empty_like(p) for p in ctx.params]
         ctx.plan.backward(ctx.tab, _lib.ptr_array(grads), x, dlogits, ctx.ws)
         ctx.ws = None
-        return (None, None, None, *grads)
+        return (None, None, None, None, *grads)
 
 
 class UNet(nn.Module):
@@ -179,6 +183,9 @@ class UNet(nn.Module):
         self.up4 = Up(128, 64, 64, bilinear)
         self.outc = OutConv(64, n_classes)
         self._runner = _Runner()
+        # GEMM precision: None = follow torch.autocast (bf16 inside a cuda
+        # bfloat16 autocast region, else fp32); "fp32" / "bf16" force it
+        self.precision = None
 
     # reference helper (models/unet_model.py:88-102), kept for API parity
     @staticmethod
@@ -197,7 +204,17 @@ class UNet(nn.Module):
         if x.dim() != 4 or x.shape[1] != self.n_channels:
             raise ValueError(f"expected input (N, {self.n_channels}, H, W), got {tuple(x.shape)}")
         params = tuple(self.parameters())
-        return _UNetFunction.apply(x, self, bool(self.training), *params)
+        return _UNetFunction.apply(x, self, bool(self.training), self.gemm_precision(), *params)
+
+    def gemm_precision(self):
+        """GEMM precision the next forward uses ("fp32" or "bf16")."""
+        if self.precision is not None:
+            if self.precision not in ("fp32", "bf16"):
+                raise ValueError(f"precision must be None, 'fp32' or 'bf16', got {self.precision!r}")
+            return self.precision
+        if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
+            return "bf16"
+        return "fp32"
 
 
 class _WCEFunction(torch.autograd.Function):

@@ -8,16 +8,23 @@ from . import _lib
 N_PARAMS = 136   # state_dict entries (parameters + BN buffers)
 N_GRADS = 82     # named_parameters
 N_SEGMENTS = 9   # backward segments: head+up4, up3, up2, up1, down4, down3, down2, down1, inc
+# GEMM arithmetic (include/unet_hip.h UNET_PREC_*): fp32 operands, or bf16
+# operands with fp32 accumulation (configs C3/C5, torch.autocast(bfloat16))
+PRECISIONS = {"fp32": 0, "bf16": 1}
 
 
 class Plan:
-    """One compiled schedule for input shape (n, c, h, w) and n_classes."""
+    """One compiled schedule for input shape (n, c, h, w), n_classes and GEMM
+    precision ("fp32" or "bf16")."""
 
-    def __init__(self, n, c, h, w, n_classes):
+    def __init__(self, n, c, h, w, n_classes, precision="fp32"):
+        if precision not in PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(PRECISIONS)}, got {precision!r}")
         self.lib = _lib.load()
-        self.handle = self.lib.unet_plan_create(n, c, h, w, n_classes)
+        self.handle = self.lib.unet_plan_create_ex(n, c, h, w, n_classes, PRECISIONS[precision])
         if not self.handle:
-            raise ValueError(f"unet_plan_create({n},{c},{h},{w},{n_classes}): {_lib.last_error()}")
+            raise ValueError(f"unet_plan_create_ex({n},{c},{h},{w},{n_classes},{precision}): {_lib.last_error()}")
+        self.precision = precision
         oh, ow = ctypes.c_int(), ctypes.c_int()
         _lib.check(self.lib.unet_plan_out_hw(self.handle, ctypes.byref(oh), ctypes.byref(ow)), "unet_plan_out_hw")
         self.shape = (n, c, h, w)

@@ -9,6 +9,8 @@ SGD(lr, momentum=0.99).step() -- with the same arithmetic as the drop-in
   module's parameters are re-homed as views, so ``state_dict`` is unchanged);
 * one persistent plan workspace (no per-step allocation);
 * the optimizer is one fused kernel over the flat buffer;
+* ``precision="bf16"`` runs the convolution GEMMs on bf16 operands with fp32
+  accumulation (configs C3/C5); weights, gradients and the optimizer stay fp32;
 * with a process group, the backward runs in 9 segments and each segment's
   gradient bucket is all-reduced (RCCL over xGMI) while later segments compute.
 """
@@ -59,7 +61,7 @@ class FlatParams:
 
 class Trainer:
     def __init__(self, model, batch, height, width, lr=1e-4, momentum=0.99, process_group=None,
-                 overlap=True):
+                 overlap=True, precision="fp32"):
         from .modules import UNet
         if not isinstance(model, UNet):
             raise TypeError("Trainer drives the MI355X UNet")
@@ -70,7 +72,7 @@ class Trainer:
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         self.flat = FlatParams(model)
         dev = self.flat.flat.device
-        self.plan = Plan(batch, model.n_channels, height, width, model.n_classes)
+        self.plan = Plan(batch, model.n_channels, height, width, model.n_classes, precision)
         self.ws = torch.empty(self.plan.workspace_bytes, dtype=torch.uint8, device=dev)
         self.state = [t for _, t in model.state_dict(keep_vars=True).items()]
         self.param_tab = _lib.ptr_array(self.state)
