@@ -144,8 +144,9 @@ int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int 
  *                  split) the first time it meets a GEMM shape and caches the
  *                  fastest per shape; 0 = built-in heuristic only.
  *  "igemm_variant" heuristic override for A/B measurements (-1 = off, 1..9 =
- *                  forced tile shape); "wgrad_variant" (-1 = off, 1 = 64x64
- *                  tile, >=2 = workgroups per CU for the pixel split);
+ *                  forced tile shape; 21-26, 31-36 bf16 tiles); "wgrad_variant"
+ *                  (-1 = off, 1 = 64x64 tile, 2..9 = workgroups per CU for the
+ *                  pixel split; bf16 GEMMs: 10-14, 20-21 = forced bf16 tile);
  *  "concurrent"    1 (default, or env UNET_CONCURRENT) = a plan's backward
  *                  runs the weight-gradient GEMMs on a side stream beside the
  *                  dX chain (joined before the call returns); 0 = one stream.

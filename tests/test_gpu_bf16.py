@@ -84,13 +84,23 @@ def op_bf16(lib):
     lib.unet_set_tuning(b"op_precision", PREC_BF16)
     yield lib
     lib.unet_set_tuning(b"op_precision", 0)
+    lib.unet_set_tuning(b"igemm_variant", -1)
+    lib.unet_set_tuning(b"wgrad_variant", -1)
+
+
+# per-op GEMM tile: -1 = built-in choice (row-gather k_igemm_bf), 31-36 = the
+# halo-tiled k_conv3_bf shapes (8x32, 16x16, 4x32/128, 8x16, 8x32/128)
+HALO = [-1, 31, 32, 33, 34, 35, 36]
 
 
 # ------------------------------- per-op -------------------------------------
+@pytest.mark.parametrize("variant", HALO)
 @pytest.mark.parametrize("n,h,w,ci,co,tf", [(2, 14, 13, 64, 128, False), (2, 11, 17, 64, 64, True),
-                                              (1, 30, 29, 128, 256, True), (3, 9, 9, 256, 64, False)])
-def test_bf16_conv3x3_fwd(op_bf16, n, h, w, ci, co, tf):
+                                              (1, 30, 41, 128, 256, True), (3, 9, 9, 256, 64, False)])
+def test_bf16_conv3x3_fwd(op_bf16, n, h, w, ci, co, tf, variant):
+    """Grids smaller and larger than the halo tiles (overhanging tiles masked)."""
     lib = op_bf16
+    lib.unet_set_tuning(b"igemm_variant", variant)
     rng = np.random.default_rng(10)
     x = f32(rng.standard_normal((n, h, w, ci)))
     wt = f32(rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci))
@@ -111,9 +121,11 @@ def test_bf16_conv3x3_fwd(op_bf16, n, h, w, ci, co, tf):
     assert rel_err(O.conv_valid_fwd(xin, wt, b), ref) > 1e-4
 
 
-@pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 9, 14, 128, 64), (2, 8, 8, 64, 256)])
-def test_bf16_conv3x3_dgrad(op_bf16, n, h, w, ci, co):
+@pytest.mark.parametrize("variant", HALO)
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 19, 40, 128, 64), (2, 8, 8, 64, 256)])
+def test_bf16_conv3x3_dgrad(op_bf16, n, h, w, ci, co, variant):
     lib = op_bf16
+    lib.unet_set_tuning(b"igemm_variant", variant)
     rng = np.random.default_rng(11)
     x = f32(rng.standard_normal((n, h, w, ci)))
     wt = f32(rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci))
@@ -127,11 +139,15 @@ def test_bf16_conv3x3_dgrad(op_bf16, n, h, w, ci, co):
     assert rel_err(host(dx), ref) < 5e-5
 
 
+@pytest.mark.parametrize("variant", [-1, 10, 12, 20, 21])
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 40, 37, 128, 128), (2, 10, 9, 64, 128),
-                                         (1, 7, 5, 64, 64)])
-def test_bf16_conv3x3_wgrad(op_bf16, n, h, w, ci, co):
-    """Pixel counts that are not multiples of the 32-pixel K step (ragged tails)."""
+                                         (1, 7, 5, 64, 64), (2, 21, 44, 192, 128)])
+def test_bf16_conv3x3_wgrad(op_bf16, n, h, w, ci, co, variant):
+    """Pixel counts that are not multiples of the K step and grids that are not
+    multiples of the halo tiles (ragged tails); 10/12 = pixel-column tiles
+    (k_wgrad_bf), 20/21 = halo-tiled all-taps kernel (k_wgrad3_bf, 8x16 / 4x32)."""
     lib = op_bf16
+    lib.unet_set_tuning(b"wgrad_variant", variant)
     rng = np.random.default_rng(12)
     x = f32(rng.standard_normal((n, h, w, ci)))
     wt = f32(rng.standard_normal((co, ci, 3, 3)))
@@ -209,7 +225,8 @@ def check_vs_bf16_oracle(m, params, x, tgt, wmap, tag=""):
     # 3e-3 of the logit scale: under one bf16 ulp (2^-8) of the largest logit
     assert lerr <= max(3e-3, 4 * lfloor), (tag, lerr, lfloor)
     lo_err, lo_floor = abs(loss.item() - rloss) / abs(rloss), abs(loss32 - rloss) / abs(rloss)
-    assert lo_err <= max(1e-4, 4 * lo_floor), (tag, lo_err, lo_floor)
+    # the loss averages the logits: its noise is bounded by theirs
+    assert lo_err <= max(1e-4, 4 * lo_floor, 0.5 * lfloor), (tag, lo_err, lo_floor)
     worst = 0.0
     for name, p in m.named_parameters():
         g = host(p.grad)
@@ -257,10 +274,12 @@ def gemm_mode(request, lib):
 
 
 @pytest.mark.parametrize("gemm_mode", ["heuristic", "tile21", "tile22", "tile23", "tile24", "tile25", "tile26",
-                                       "tile22+split3", "tile24+split8"], indirect=True)
+                                       "tile22+split3", "tile24+split8", "tile31", "tile32", "tile33", "tile34",
+                                       "tile35", "tile36", "tile31+split2", "tile34+split3"], indirect=True)
 def test_bf16_gemm_variants_vs_bf16_oracle(gemm_mode):
-    """Every bf16 tile (21-26) and split-K on every conv / convT / dgrad GEMM of a
-    train step; the weight gradients run the bf16 wgrad tiles."""
+    """Every bf16 tile (21-26 row gather, 31-36 halo-tiled 3x3 -- the convT GEMMs
+    fall back to the built-in tile there) and split-K on every conv / convT /
+    dgrad GEMM of a train step; the weight gradients run the bf16 wgrad tiles."""
     params = O.hash_init(1, 2, seed=21, bn_random=True)
     x, tgt, wmap = F.make_inputs(21, 2, 1, 188)
     check_vs_bf16_oracle(make_model(params), params, x, tgt, wmap, gemm_mode)

@@ -35,7 +35,7 @@ def last_step(d):
 def family(name):
     if "conv_first" in name:
         return "stage1"
-    if "igemm" in name or "wgrad<" in name:
+    if "igemm" in name or "conv3_bf" in name or ("wgrad" in name and "first" not in name):
         return "conv"
     return "other"
 

@@ -3,12 +3,9 @@
 // 1x1 head, the fused weighted cross-entropy, SGD-momentum and weight repacks.
 // All NHWC activations are touched as float4 (16 B per lane) so every wave
 // instruction moves 1 KiB of contiguous bytes where the layout allows it.
-#include "unet_internal.h"
+#include "gemm_common.h"
 
 namespace unet {
-
-__device__ __forceinline__ float4 ld4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-__device__ __forceinline__ void st4(float* p, float4 v) { *reinterpret_cast<float4*>(p) = v; }
 
 static inline int cdiv(long long a, long long b) { return (int)((a + b - 1) / b); }
 static inline int grid_cap(long long work, int per_block, int cap = 4096) {
@@ -321,6 +318,8 @@ __global__ __launch_bounds__(256) void k_bnb_finalize(const double* __restrict__
 }
 
 // dYpad[n][y+pad][x+pad][c] = k0*dz + k1*(y - mean) + k2 ; border written as 0.
+// H16: dYpad stored bf16 (it is only ever a bf16 GEMM operand then).
+template <int H16>
 __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restrict__ yr,
                             const float* __restrict__ coef, int n, int h, int w, int C,
                             float* __restrict__ dyp, int pad) {
@@ -347,7 +346,10 @@ __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restric
       out.z = fmaf(k0.z, d.z, fmaf(k1.z, yv.z - mu.z, k2.z));
       out.w = fmaf(k0.w, d.w, fmaf(k1.w, yv.w - mu.w, k2.w));
     }
-    st4(dyp + i * 4, out);
+    if (H16)
+      reinterpret_cast<uint2*>(dyp)[i] = make_uint2(bf16pack(out.x, out.y), bf16pack(out.z, out.w));
+    else
+      st4(dyp + i * 4, out);
   }
 }
 
@@ -372,11 +374,15 @@ hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const 
   return hipGetLastError();
 }
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h, int w, int c,
-                            float* dypad, int pad, hipStream_t s) {
+                            float* dypad, int pad, hipStream_t s, int out_h16) {
   if (c % 4) return hipErrorInvalidValue;
   const long long work = (long long)n * (h + 2 * pad) * (w + 2 * pad) * (c / 4);
-  hipLaunchKernelGGL(k_bnb_apply, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad,
-                     pad);
+  if (out_h16)
+    hipLaunchKernelGGL(k_bnb_apply<1>, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, s, dz, y, coef, n, h, w, c,
+                       dypad, pad);
+  else
+    hipLaunchKernelGGL(k_bnb_apply<0>, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, s, dz, y, coef, n, h, w, c,
+                       dypad, pad);
   return hipGetLastError();
 }
 
@@ -384,6 +390,7 @@ hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, 
 // MaxPool2d(2) forward (models/unet_model.py:28) of relu(bn(y)): floor mode,
 // scan order (0,0),(0,1),(1,0),(1,1) with strict '>' so the FIRST max wins.
 // ---------------------------------------------------------------------------
+template <int H16>  // pooled map stored bf16 (a bf16 GEMM operand only)
 __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y, uint8_t* __restrict__ arg) {
   const int C = s.C, C4 = C / 4, ho = h / 2, wo = w / 2;
   const long long total = (long long)n * ho * wo * C4;
@@ -418,15 +425,22 @@ __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y,
       if (v[k].z > best.z) { best.z = v[k].z; a.z = k; }
       if (v[k].w > best.w) { best.w = v[k].w; a.w = k; }
     }
-    st4(y + i * 4, best);
+    if (H16)
+      reinterpret_cast<uint2*>(y)[i] = make_uint2(bf16pack(best.x, best.y), bf16pack(best.z, best.w));
+    else
+      st4(y + i * 4, best);
     *reinterpret_cast<uchar4*>(arg + i * 4) = a;
   }
 }
 
-hipError_t launch_maxpool_fwd(const Src& s, int n, int h, int w, float* y, uint8_t* arg, hipStream_t st) {
-  if (s.C % 4) return hipErrorInvalidValue;
+hipError_t launch_maxpool_fwd(const Src& s, int n, int h, int w, float* y, uint8_t* arg, hipStream_t st,
+                              int out_h16) {
+  if (s.C % 4 || s.h16) return hipErrorInvalidValue;
   const long long work = (long long)n * (h / 2) * (w / 2) * (s.C / 4);
-  hipLaunchKernelGGL(k_maxpool_fwd, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, st, s, n, h, w, y, arg);
+  if (out_h16)
+    hipLaunchKernelGGL(k_maxpool_fwd<1>, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, st, s, n, h, w, y, arg);
+  else
+    hipLaunchKernelGGL(k_maxpool_fwd<0>, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, st, s, n, h, w, y, arg);
   return hipGetLastError();
 }
 

@@ -8,6 +8,8 @@
 // v_mfma_f32_32x32x16_bf16 on gfx950): lane l holds column l&31 of a 32x32 tile,
 // register r holds row (r&3) + 8*(r>>2) + 4*(l>>5).
 #pragma once
+#include <type_traits>
+
 #include "unet_internal.h"
 
 namespace unet {
@@ -39,6 +41,19 @@ __device__ __forceinline__ unsigned bf16pack(float a, float b) {
 __device__ __forceinline__ uint4 bf16pack8(float4 a, float4 b) {
   return make_uint4(bf16pack(a.x, a.y), bf16pack(a.z, a.w), bf16pack(b.x, b.y), bf16pack(b.z, b.w));
 }
+__device__ __forceinline__ uint16_t bf16_of(float v) { return (uint16_t)(bf16pack(v, 0.f) & 0xffffu); }
+// 4 bf16 (uint2) -> 4 fp32 (exact)
+__device__ __forceinline__ float4 bf16x4_to_f4(uint2 u) {
+  return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+                     __uint_as_float(u.y & 0xffff0000u));
+}
+// store one element of a Dst (fp32 or bf16 storage)
+__device__ __forceinline__ void dst_store(const Dst& d, size_t idx, float v) {
+  if (d.h16)
+    reinterpret_cast<uint16_t*>(d.ptr)[idx] = bf16_of(v);
+  else
+    d.ptr[idx] = v;
+}
 
 // Pixel iterator over an (nimg, Hg, Wg) grid (weight-gradient GEMMs walk their
 // staged pixel rows incrementally, no divisions in the loop).
@@ -66,13 +81,36 @@ struct PixIt {
   }
 };
 
+// Tile row -> output row m of the GEMM.  LinearRows: rows m0.. of a
+// pixel-linear tile.  HaloRows: a TH x TW spatial tile of image n at (y0, x0)
+// in row-major order (the halo-tiled 3x3 kernels); rows outside the grid are
+// not stored.
+struct LinearRows {
+  int m0, M;
+  __device__ __forceinline__ bool map(int row, int& m) const {
+    m = m0 + row;
+    return m < M;
+  }
+};
+template <int TW>
+struct HaloRows {
+  int n, y0, x0, Hg, Wg;
+  __device__ __forceinline__ bool map(int row, int& m) const {
+    const int y = y0 + row / TW, x = x0 + row % TW;
+    m = (n * Hg + y) * Wg + x;
+    return y < Hg && x < Wg;
+  }
+};
+
 // Split-K partial store or the full epilogue of an implicit-GEMM tile: bias,
 // destination mapping (linear / pixel shuffle / cropped), ReLU mask + BN-bwd
 // statistics, BN statistics, concat column sums.  `red` is WM*3*BN floats of
 // LDS that no wave reads or writes any more (a barrier precedes its use).
-template <int BM, int BN, int WM, int WN, int NT>
+template <int BM, int BN, int WM, int WN, int NT, class RowMap = LinearRows>
 __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&acc)[BM / (WM * 32)][BN / (WN * 32)],
-                                             int m0, int n0, int wm, int wn, int tid, float* red) {
+                                             int m0, int n0, int wm, int wn, int tid, float* red,
+                                             RowMap rows = RowMap{0, 0}) {
+  if constexpr (std::is_same<RowMap, LinearRows>::value) rows = LinearRows{m0, args.M};
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   const Gather& g = args.a;
   const int M = args.M;
@@ -88,8 +126,8 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
       for (int i = 0; i < TM; ++i)
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          const int m = m0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-          if (m < M) sl[(size_t)m * N + col] = acc[i][j][r];
+          int m;
+          if (rows.map(wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h, m)) sl[(size_t)m * N + col] = acc[i][j][r];
         }
     }
     return;
@@ -117,8 +155,8 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
         const int row = wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-        const int m = m0 + row;
-        if (m >= M) continue;
+        int m;
+        if (!rows.map(row, m)) continue;
         float v = acc[i][j][r] + bias;
         size_t idx;
         if (linear) {
@@ -144,7 +182,7 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
         } else if (second && e.colsum1) {
           t1[j] += v;
         }
-        d.ptr[idx] = v;
+        dst_store(d, idx, v);
       }
     }
   }

@@ -511,7 +511,11 @@ __global__ __launch_bounds__(256) void k_splitk_epi(const IgemmArgs args) {
         s2[q] += vv[q] * vv[q];
       }
     }
-    st4(d.ptr + idx, make_float4(vv[0], vv[1], vv[2], vv[3]));
+    if (d.h16)
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(d.ptr) + idx) =
+          make_uint2(bf16pack(vv[0], vv[1]), bf16pack(vv[2], vv[3]));
+    else
+      st4(d.ptr + idx, make_float4(vv[0], vv[1], vv[2], vv[3]));
   }
   const bool want = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
   if (!want) return;
@@ -732,23 +736,38 @@ static TileInfo tile_info(int id) {
     case 24: return {64, 128, 32, 4};
     case 25: return {256, 64, 32, 2};
     case 26: return {128, 256, 32, 2};
+    // bf16 halo-tiled 3x3 (k_conv3_bf): bm = pixels per tile, bk = one
+    // 32-channel chunk x 9 taps (the split-K unit)
+    case 31: return {256, 64, 288, 2};
+    case 32: return {256, 64, 288, 2};
+    case 33: return {256, 64, 288, 2};
+    case 34: return {128, 128, 288, 1};
+    case 35: return {128, 64, 288, 2};
+    case 36: return {256, 128, 288, 1};
     default: return {0, 0, 0, 0};
   }
 }
 
-static bool is_bf16_tile(int tile) { return tile >= 21 && tile <= 26; }
+static bool is_halo_tile(int tile) { return tile >= 31 && tile <= 36; }
+static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_halo_tile(tile); }
 
 // A tile applies when the shape divides and the packed B operand is in the
 // tile's precision (fp32 `b` for tiles 1-14, bf16 `bh` for 21-26).
 bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   const TileInfo t = tile_info(tile);
   const bool prec_ok = is_bf16_tile(tile) ? a.bh != nullptr : a.b != nullptr;
+  if (is_halo_tile(tile))  // 3x3 stride-1 gathers only (conv fwd / dgrad), K = 9 x Cg
+    return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
+           a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
   return t.bm > 0 && prec_ok && a.N % t.bn == 0 && a.K % t.bk == 0 && a.a.Cg % t.bk == 0 &&
          a.a.c_split % t.bk == 0;
 }
 long long igemm_tile_count(const IgemmArgs& a, int tile) {
   const TileInfo t = tile_info(tile);
   if (t.bm == 0) return 0;
+  int th, tw, bn;
+  if (halo_tile_shape(tile, th, tw, bn))
+    return (long long)a.a.nimg * ((a.a.Hg + th - 1) / th) * ((a.a.Wg + tw - 1) / tw) * (a.N / bn);
   return (long long)((a.M + t.bm - 1) / t.bm) * (a.N / t.bn);
 }
 int igemm_tile_slots(int tile) { return tile_info(tile).slots; }
@@ -797,7 +816,8 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 12: return go_igemm_g<128, 128, 2, 2>(a, s);
     case 13: return go_igemm_g<64, 128, 2, 2>(a, s);
     case 14: return go_igemm_g<128, 64, 2, 2>(a, s);
-    case 21: case 22: case 23: case 24: case 25: case 26: return go_igemm_bf16(a, s, tile);
+    case 21: case 22: case 23: case 24: case 25: case 26:
+    case 31: case 32: case 33: case 34: case 35: case 36: return go_igemm_bf16(a, s, tile);
     default: return hipErrorInvalidValue;
   }
 }
@@ -872,6 +892,7 @@ static void wgrad_tile(int id, int& bm, int& bn) {
   if (id >= 10 && id < 15) { bm = tb[id - 10][0]; bn = tb[id - 10][1]; }
 }
 bool wgrad_tile_fits(const WgradArgs& a, int tile) {
+  if (tile == 20 || tile == 21) return wgrad3_fits(a);  // halo-tiled 3x3, all taps
   int bm, bn;
   wgrad_tile(tile, bm, bn);
   return bm > 0 && (tile >= 10) == (a.bf16 != 0) && a.Mo % bm == 0 && a.No % bn == 0;
@@ -883,7 +904,9 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     return hipErrorInvalidValue;
   int tile = c.tile;
   if (tile < 0 && a.bf16) {
-    if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 10;
+    if (g_tune_wgrad >= 10 && wgrad_tile_fits(a, g_tune_wgrad)) tile = g_tune_wgrad;  // forced (tests)
+    else if (wgrad3_fits(a)) tile = 20;
+    else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 10;
     else if (a.No % 128 == 0) tile = 12;
     else tile = 13;
   } else if (tile < 0) {
@@ -895,6 +918,7 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     else tile = 4;
   }
   if (!wgrad_tile_fits(a, tile)) return hipErrorInvalidValue;
+  if (tile == 20 || tile == 21) return go_wgrad3_bf16(a, s, tile, c.split > 0 ? c.split : 4);
   int bm, bn;
   wgrad_tile(tile, bm, bn);
   const int tiles = (a.Mo / bm) * (a.No / bn);

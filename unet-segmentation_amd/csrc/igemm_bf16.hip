@@ -111,17 +111,22 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
   float4 ra[AV][2];
   uint4 rb[BV];
   float4 sc0, sc1, sh0, sh1;
-  bool tf = false;
+  bool tf = false, h16 = false;
   auto issue = [&](int k0) {
     const bool second = it_c >= g.c_split;
     const Src& s = second ? g.s[1] : g.s[0];
     const int c = (second ? it_c - g.c_split : it_c) + chunk * 8;
     const int toff = it_ty * s.W + it_tx;
+    h16 = s.h16 != 0;
 #pragma unroll
     for (int q = 0; q < AV; ++q) {
-      const float* p = s.ptr + (size_t)((second ? rb1[q] : rb0[q]) + toff) * s.C + c;
-      ra[q][0] = ld4(p);
-      ra[q][1] = ld4(p + 4);
+      const size_t e = (size_t)((second ? rb1[q] : rb0[q]) + toff) * s.C + c;
+      if (h16) {  // stored bf16: 8 channels = 16 B, staged as is
+        ra[q][0] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(s.ptr) + e));
+      } else {
+        ra[q][0] = ld4(s.ptr + e);
+        ra[q][1] = ld4(s.ptr + e + 4);
+      }
     }
 #pragma unroll
     for (int q = 0; q < BV; ++q) rb[q] = *reinterpret_cast<const uint4*>(bptr[q] + k0);
@@ -143,12 +148,18 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
     unsigned short* Bs = As + BM * LDR;
 #pragma unroll
     for (int q = 0; q < AV; ++q) {
-      float4 v0 = ra[q][0], v1 = ra[q][1];
-      if (tf) {
-        v0 = affine_relu4(v0, sc0, sh0);
-        v1 = affine_relu4(v1, sc1, sh1);
+      uint4 o;
+      if (h16) {
+        o = __builtin_bit_cast(uint4, ra[q][0]);
+      } else {
+        float4 v0 = ra[q][0], v1 = ra[q][1];
+        if (tf) {
+          v0 = affine_relu4(v0, sc0, sh0);
+          v1 = affine_relu4(v1, sc1, sh1);
+        }
+        o = bf16pack8(v0, v1);
       }
-      *reinterpret_cast<uint4*>(As + (row0 + RPP * q) * LDR + chunk * 8) = bf16pack8(v0, v1);
+      *reinterpret_cast<uint4*>(As + (row0 + RPP * q) * LDR + chunk * 8) = o;
     }
 #pragma unroll
     for (int q = 0; q < BV; ++q) *reinterpret_cast<uint4*>(Bs + (row0 + RPP * q) * LDR + chunk * 8) = rb[q];
@@ -188,6 +199,209 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
 }
 
 // ---------------------------------------------------------------------------
+// k_conv3_bf: halo-tiled 3x3 stride-1 implicit GEMM (conv forward and conv
+// input gradient), bf16 operands.  A workgroup owns a TH x TW spatial tile of
+// one image's output grid and BN output columns.  Per 32-channel chunk it
+// stages the (TH+2) x (TW+2) input halo ONCE (BN+ReLU applied, rounded to bf16)
+// and the chunk's weights for all 9 taps; the 9 taps then read shifted pixel
+// windows of the same LDS halo.  Against the pixel-row gather of k_igemm_bf
+// (every A element fetched 9 times from L2) the A traffic drops to the halo
+// overhead ((TH+2)(TW+2)/(TH TW), 1.33 at 8x32): the row-gather kernels are
+// bound by that L2 traffic on the wide layers ("LDS-stage input
+// tiles with a 2-px halo").
+// LDS: halo [(TH+2)(TW+2)][40] bf16, weights [9][BN][40] bf16, BN scale/shift
+// [2][Cg] fp32; one buffer, the next chunk in registers while this one computes.
+// MFMA rows = output pixels in row-major tile order (32 per fragment), so a
+// fragment lane reads LDS pixel (ry + ty)(TW+2) + rx + tx: one ds_read_b128.
+// ---------------------------------------------------------------------------
+template <int TH, int TW, int BN>
+constexpr size_t conv3_bf_smem(int cg) {
+  return (size_t)((TH + 2) * (TW + 2) + 9 * BN) * kBfLdr * 2 + (size_t)2 * cg * 4;
+}
+
+template <int TH, int TW, int BN, int WM, int WN, int MINW>
+__global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs args) {
+  constexpr int NT = WM * WN * 64, BM = TH * TW, LDR = kBfLdr;
+  constexpr int HW2 = TW + 2, PH = (TH + 2) * HW2;  // halo pixels
+  constexpr int FM = BM / 32, TM = FM / WM, TN = BN / (WN * 32);
+  constexpr int UA = PH * 4, UB = 9 * BN * 4;  // 16-B staging units (8 channels / 8 k each)
+  constexpr int NA = (UA + NT - 1) / NT, NB = (UB + NT - 1) / NT;
+  constexpr int A_ELEMS = PH * LDR, B_ELEMS = 9 * BN * LDR;
+  static_assert(BM % 32 == 0 && FM % WM == 0 && TM >= 1 && TN >= 1, "tile");
+  static_assert(WM * 3 * BN * 4 <= A_ELEMS * 2, "epilogue reduction must fit the halo buffer");
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
+  unsigned short* As = smem;
+  unsigned short* Bs = smem + A_ELEMS;
+  float* ssc = reinterpret_cast<float*>(smem + A_ELEMS + B_ELEMS);  // [2][Cg]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const Gather& g = args.a;
+  const int Cg = g.Cg, K = args.K, Hg = g.Hg, Wg = g.Wg;
+  const int tiles_x = (Wg + TW - 1) / TW, tiles_y = (Hg + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int x0 = (t % tiles_x) * TW;
+  t /= tiles_x;
+  const int y0 = (t % tiles_y) * TH;
+  const int n = t / tiles_y;
+  const int n0 = blockIdx.y * BN;
+
+  // consumer BN+ReLU parameters of the concatenated channel range
+  const bool any_tf = g.s[0].scale != nullptr || (g.c_split < Cg && g.s[1].scale != nullptr);
+  if (any_tf) {
+    for (int c = tid; c < Cg; c += NT) {
+      const bool sec = c >= g.c_split;
+      const Src& sr = sec ? g.s[1] : g.s[0];
+      const int cl = sec ? c - g.c_split : c;
+      ssc[c] = sr.scale ? sr.scale[cl] : 1.f;
+      ssc[Cg + c] = sr.scale ? sr.shift[cl] : 0.f;
+    }
+  }
+
+  // staging units: A = (halo pixel, 8-channel piece), B = (tap, row, 8-k piece)
+  int pi0[NA], pi1[NA];
+  const uint16_t* bsrc[NB];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    const int u = min(tid + k * NT, UA - 1);
+    const int ph = u >> 2;
+    const int hy = ph / HW2, hx = ph - (ph / HW2) * HW2;
+    const int yy = min(y0 + hy, Hg + 1), xx = min(x0 + hx, Wg + 1);  // overhang: any in-range pixel
+    pi0[k] = (n * g.s[0].H + yy + g.s[0].oy) * g.s[0].W + xx + g.s[0].ox;
+    pi1[k] = (n * g.s[1].H + yy + g.s[1].oy) * g.s[1].W + xx + g.s[1].ox;
+  }
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int u = min(tid + k * NT, UB - 1);
+    const int r = (u >> 2) % BN, tap = (u >> 2) / BN;
+    bsrc[k] = args.bh + (size_t)(n0 + r) * K + tap * Cg + (u & 3) * 8;
+  }
+
+  const int nk_all = Cg / 32;
+  int kc0 = 0, kc1 = nk_all;
+  if (args.ksplit > 1) {
+    const int per = (nk_all + args.ksplit - 1) / args.ksplit;
+    kc0 = blockIdx.z * per;
+    kc1 = min(nk_all, kc0 + per);
+  }
+
+  float4 ra[NA][2];
+  uint4 rb[NB];
+  auto issue = [&](int kc) {
+    const int c0 = kc * 32;
+    const bool second = c0 >= g.c_split;
+    const Src& s = second ? g.s[1] : g.s[0];
+    const int cl = (second ? c0 - g.c_split : c0) + (tid & 3) * 8;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      if (tid + k * NT < UA) {
+        const size_t e = (size_t)(second ? pi1[k] : pi0[k]) * s.C + cl;
+        if (s.h16) {  // stored bf16: staged as is
+          ra[k][0] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(s.ptr) + e));
+        } else {
+          ra[k][0] = ld4(s.ptr + e);
+          ra[k][1] = ld4(s.ptr + e + 4);
+        }
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (tid + k * NT < UB) rb[k] = *reinterpret_cast<const uint4*>(bsrc[k] + c0);
+  };
+  auto commit = [&](int kc) {
+    const int c = kc * 32 + (tid & 3) * 8;
+    const Src& sc_src = c >= g.c_split ? g.s[1] : g.s[0];
+    const bool tf = sc_src.scale != nullptr, h16 = sc_src.h16 != 0;
+    float4 sc0, sc1, sh0, sh1;
+    if (tf) {
+      sc0 = ld4(ssc + c);
+      sc1 = ld4(ssc + c + 4);
+      sh0 = ld4(ssc + Cg + c);
+      sh1 = ld4(ssc + Cg + c + 4);
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      if (u < UA) {
+        uint4 o;
+        if (h16) {
+          o = __builtin_bit_cast(uint4, ra[k][0]);
+        } else {
+          float4 v0 = ra[k][0], v1 = ra[k][1];
+          if (tf) {
+            v0 = affine_relu4(v0, sc0, sh0);
+            v1 = affine_relu4(v1, sc1, sh1);
+          }
+          o = bf16pack8(v0, v1);
+        }
+        *reinterpret_cast<uint4*>(As + (u >> 2) * LDR + (u & 3) * 8) = o;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int u = tid + k * NT;
+      if (u < UB) *reinterpret_cast<uint4*>(Bs + (u >> 2) * LDR + (u & 3) * 8) = rb[k];
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int h = lane >> 5, li = lane & 31;
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = (wm * TM + i) * 32 + li;
+    abase[i] = (p / TW) * HW2 + p % TW;
+  }
+  auto compute = [&] {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int off = (tap / 3) * HW2 + tap % 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8_t*>(As + (abase[i] + off) * LDR + 16 * s + 8 * h);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (tap * BN + wn * TN * 32 + j * 32 + li) * LDR + 16 * s + 8 * h);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  if (any_tf) __syncthreads();  // scale/shift table before the first commit
+  if (kc0 < kc1) {
+    issue(kc0);
+    commit(kc0);
+  }
+  __syncthreads();
+  for (int kc = kc0; kc < kc1; ++kc) {
+    const bool more = kc + 1 < kc1;
+    if (more) issue(kc + 1);
+    compute();
+    __syncthreads();
+    if (more) {
+      commit(kc + 1);
+      __syncthreads();
+    }
+  }
+  igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, reinterpret_cast<float*>(smem),
+                                   HaloRows<TW>{n, y0, x0, Hg, Wg});
+}
+
+// ---------------------------------------------------------------------------
 // k_wgrad_bf: C[i][j] = sum_p bf16(A_p[i]) * bf16(B_p[j]) over the pixels p of
 // this workgroup's slice (blockIdx.z), fp32 atomics into out[Mo][No].
 // A_p = channels of ga.s[0] (dY, or the BN+ReLU'd convT input), B_p = the
@@ -199,7 +413,10 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
 // Units: (channel quad, 8-pixel group) with the group fastest across lanes
 // (keeps the four 16-B stores of 8 consecutive lanes on distinct bank quads).
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN>
+// AH / BH: storage of the A / B sources (0 fp32, 1 bf16, 2 per unit -- the
+// concat gather of an up block's first conv mixes an fp32 skip and a bf16
+// upsampled map); compile-time so that the staging loads carry no branches.
+template <int BM, int BN, int WM, int WN, int AH, int BH>
 __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs args) {
   constexpr int NT = WM * WN * 64, BK = kBfBK, LDR = kBfLdr;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
@@ -218,9 +435,10 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
   if (nk <= 0) return;
 
   // per-unit constants (unit u: A if u < UA, else B; wave-uniform split since UA % 64 == 0)
-  bool act[UPT], isb[UPT], tf[UPT];
-  int grp[UPT], lrow[UPT], C[UPT], H[UPT], W[UPT], oy[UPT], ox[UPT], stride[UPT], Hg[UPT], Wg[UPT];
-  const float* base[UPT];
+  bool act[UPT], isb[UPT], tf[UPT], h16[UPT];
+  int grp[UPT], lrow[UPT], C[UPT], H_[UPT], W[UPT], oy[UPT], ox[UPT], stride[UPT], Hg[UPT], Wg[UPT];
+  const float* base[UPT];      // fp32 storage
+  const uint16_t* baseh[UPT];  // bf16 storage
   float4 sc[UPT], sh[UPT];
   PixIt it[UPT];
 #pragma unroll
@@ -251,8 +469,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
     }
     if (!act[k]) { s = &args.ga.s[0]; c = 0; }
     base[k] = s->ptr + c;
+    baseh[k] = reinterpret_cast<const uint16_t*>(s->ptr) + c;
     C[k] = s->C;
-    H[k] = s->H;
+    H_[k] = s->H;
     W[k] = s->W;
     oy[k] = s->oy + ty;
     ox[k] = s->ox + tx;
@@ -260,6 +479,7 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
     Hg[k] = gg.Hg;
     Wg[k] = gg.Wg;
     tf[k] = s->scale != nullptr && act[k];
+    h16[k] = isb[k] ? (BH == 2 ? s->h16 != 0 : BH == 1) : AH == 1;
     sc[k] = make_float4(1.f, 1.f, 1.f, 1.f);
     sh[k] = make_float4(0.f, 0.f, 0.f, 0.f);
     if (tf[k]) {
@@ -271,21 +491,39 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
 
   float4 v[UPT][8];
   unsigned valid[UPT];
+  // one unit's 8 pixel loads; H = storage of its source (0 fp32, 1 bf16, 2 per
+  // unit).  Unconditional: the iterator never leaves the grid, so the address
+  // is valid past `pend` too; invalid pixels are zeroed in commit.  bf16 data
+  // stays raw (bits in .x/.y) until commit, so no load is waited for here.
+  auto load_unit = [&](auto hc, int k, int pb) {
+    constexpr int H = decltype(hc)::value;
+    valid[k] = 0;
+    PixIt q = it[k];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const bool ok = act[k] && pb + j < pend;
+      const int pix = (q.n * H_[k] + q.y * stride[k] + oy[k]) * W[k] + q.x * stride[k] + ox[k];
+      const size_t e = (size_t)pix * C[k];
+      const bool half = H == 1 || (H == 2 && h16[k]);
+      if (half) {
+        const uint2 r = *reinterpret_cast<const uint2*>(baseh[k] + e);
+        v[k][j] = make_float4(__uint_as_float(r.x), __uint_as_float(r.y), 0.f, 0.f);
+      } else {
+        v[k][j] = ld4(base[k] + e);
+      }
+      valid[k] |= ok ? (1u << j) : 0u;
+      if (pb + j + 1 < pend) q.next(Hg[k], Wg[k]);
+    }
+    if (pb + BK < pend) it[k].advance(BK, Hg[k], Wg[k]);
+  };
   auto issue = [&](int p0) {  // p0 = first pixel of the stage
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
-      valid[k] = 0;
-      PixIt q = it[k];
       const int pb = p0 + grp[k] * 8;
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const bool ok = act[k] && pb + j < pend;
-        const int pix = (q.n * H[k] + q.y * stride[k] + oy[k]) * W[k] + q.x * stride[k] + ox[k];
-        v[k][j] = ok ? ld4(base[k] + (size_t)pix * C[k]) : make_float4(0.f, 0.f, 0.f, 0.f);
-        valid[k] |= ok ? (1u << j) : 0u;
-        if (pb + j + 1 < pend) q.next(Hg[k], Wg[k]);
-      }
-      if (pb + BK < pend) it[k].advance(BK, Hg[k], Wg[k]);
+      if (isb[k])  // wave-uniform: a wave stages A units or B units
+        load_unit(std::integral_constant<int, BH>{}, k, pb);
+      else
+        load_unit(std::integral_constant<int, AH>{}, k, pb);
     }
   };
   auto commit = [&](int buf) {
@@ -293,12 +531,15 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
 #pragma unroll
     for (int k = 0; k < UPT; ++k) {
       if (!act[k]) continue;
-      if (tf[k]) {
+      const bool wide = isb[k] ? (BH == 2 ? h16[k] : BH == 1) : AH == 1;
+      if (wide) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float4 t = affine_relu4(v[k][j], sc[k], sh[k]);
-          v[k][j] = (valid[k] >> j) & 1 ? t : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int j = 0; j < 8; ++j) v[k][j] = bf16x4_to_f4(make_uint2(__float_as_uint(v[k][j].x), __float_as_uint(v[k][j].y)));
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float4 t = tf[k] ? affine_relu4(v[k][j], sc[k], sh[k]) : v[k][j];
+        v[k][j] = (valid[k] >> j) & 1 ? t : make_float4(0.f, 0.f, 0.f, 0.f);
       }
       unsigned short* dst = S + lrow[k] * LDR + grp[k] * 8;
       *reinterpret_cast<uint4*>(dst + 0 * LDR) =
@@ -353,6 +594,251 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
 }
 
 // ---------------------------------------------------------------------------
+// k_wgrad3_bf: halo-tiled weight gradient of a 3x3 stride-1 conv, all 9 taps in
+// one workgroup.  dW[co][tap][ci] = sum_p dY[p][co] * X[p + tap][ci].  A
+// workgroup owns 64 output channels (co) x 64 input channels (ci) x 9 taps and
+// walks TH x TW output-pixel tiles (strided over blockIdx.z): per tile it stages
+// the dY tile once and the (TH+2) x (TW+2) X halo once (consumer BN+ReLU,
+// bf16), and every tap reads a shifted pixel window of that halo.  Against the
+// (tap, channel)-column gather of k_wgrad_bf (X fetched once per tap, dY once
+// per 64/128-column block) the operand traffic drops to ~1.4x the tensors.
+// The MFMA k is the pixel; both LDS images are [pixel][64 channels] bf16
+// (128-B rows, 16-B chunks swizzled by c ^ (((row >> 1) & 1) << 2)) and the
+// operands come out transposed with ds_read_b64_tr_b16 (T10): a 16-lane group
+// reads 4 pixels x 16 channels and lane i receives channel i of the 4 pixels,
+// which is the 32x32x16 operand layout (row = channel, k = pixel).  Any 4
+// consecutive rows are conflict-free under that swizzle, so the shifted tap
+// windows need no realignment.
+// Waves (8): co tile w & 1, ci tile (w >> 1) & 1, tap group w >> 2 (taps 0-4 or
+// 5-8): one accumulator per tap of the group.
+// ---------------------------------------------------------------------------
+typedef __bf16 bf16x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((__vector_size__(4 * sizeof(__bf16)))) __bf16 lds_bf16x4_t;
+
+__device__ __forceinline__ bf16x4_t tr_read(const unsigned char* p) {
+  auto q = (__attribute__((address_space(3))) lds_bf16x4_t*)(const_cast<unsigned char*>(p));
+  return __builtin_bit_cast(bf16x4_t, __builtin_amdgcn_ds_read_tr16_b64_v4bf16(q));
+}
+__device__ __forceinline__ int wg3_swz(int row, int chunk) { return chunk ^ (((row >> 1) & 1) << 2); }
+
+template <int TH, int TW>
+constexpr size_t wgrad3_smem() {
+  return (size_t)(TH * TW + (TH + 2) * (TW + 2)) * 128 + 2 * 64 * 4;
+}
+
+template <int TH, int TW, int D16>
+__global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
+  constexpr int NT = 512, BC = 64, ROWB = 128, NTAP = 5;
+  constexpr int PT = TH * TW, HW2 = TW + 2, PH = (TH + 2) * HW2;
+  constexpr int UA = PT * 8, UB = PH * 8;  // 16-B units: (pixel, 8-channel chunk)
+  constexpr int NA = (UA + NT - 1) / NT, NB = (UB + NT - 1) / NT;
+  static_assert(TW % 16 == 0 && UA % NT == 0, "a 16-pixel k-step stays inside one tile row");
+  extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
+  unsigned char* Ad = wsm;                                       // dY tile [PT][64]
+  unsigned char* Bx = wsm + PT * ROWB;                           // X halo [PH][64]
+  float* ssc = reinterpret_cast<float*>(wsm + (PT + PH) * ROWB);  // [2][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Gather& gb = args.gb;
+  const Src& ds = args.ga.s[0];
+  const int i0 = blockIdx.x * 64;  // co block
+  const int cb = blockIdx.y * BC;  // ci block (gather channel index)
+  const int Hg = gb.Hg, Wg = gb.Wg, Ci = gb.Cg;
+  const bool second = cb >= gb.c_split;  // a 64-channel block never straddles the concat split
+  const Src& xs = second ? gb.s[1] : gb.s[0];
+  const int xc = second ? cb - gb.c_split : cb;
+  const bool xtf = xs.scale != nullptr, x16 = xs.h16 != 0;
+  if (xtf) {
+    for (int c = tid; c < BC; c += NT) {
+      ssc[c] = xs.scale[xc + c];
+      ssc[BC + c] = xs.shift[xc + c];
+    }
+  }
+  const int tiles_x = (Wg + TW - 1) / TW, tiles_y = (Hg + TH - 1) / TH;
+  const int tiles = gb.nimg * tiles_x * tiles_y;
+
+  // staging registers: dY (bf16 raw, or fp32 pairs), X (bf16 raw bits in [0], or an fp32 pair)
+  uint4 rdh[NA];
+  float4 rdf[D16 ? 1 : NA][2];
+  float4 rx[NB][2];
+  unsigned dvalid = 0;
+  auto issue = [&](int t) {
+    const int x0 = (t % tiles_x) * TW;
+    const int r = t / tiles_x;
+    const int y0 = (r % tiles_y) * TH, n = r / tiles_y;
+    dvalid = 0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      const int p = u >> 3, ch = u & 7;
+      const int y = y0 + p / TW, x = x0 + p % TW;
+      dvalid |= (y < Hg && x < Wg) ? (1u << k) : 0u;
+      const int yy = min(y, Hg - 1), xx = min(x, Wg - 1);
+      const size_t e = (size_t)((n * ds.H + yy + ds.oy) * ds.W + xx + ds.ox) * ds.C + i0 + ch * 8;
+      if constexpr (D16) {
+        rdh[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(ds.ptr) + e);
+      } else {
+        rdf[k][0] = ld4(ds.ptr + e);
+        rdf[k][1] = ld4(ds.ptr + e + 4);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int u = min(tid + k * NT, UB - 1);
+      const int hp = u >> 3, ch = u & 7;
+      const int yy = min(y0 + hp / HW2, Hg + 1), xx = min(x0 + hp % HW2, Wg + 1);
+      const size_t e = (size_t)((n * xs.H + yy + xs.oy) * xs.W + xx + xs.ox) * xs.C + xc + ch * 8;
+      if (x16) {
+        rx[k][0] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(xs.ptr) + e));
+      } else {
+        rx[k][0] = ld4(xs.ptr + e);
+        rx[k][1] = ld4(xs.ptr + e + 4);
+      }
+    }
+  };
+  auto commit = [&] {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      const int p = u >> 3, ch = u & 7;
+      uint4 o;
+      if constexpr (D16) o = rdh[k];
+      else o = bf16pack8(rdf[k][0], rdf[k][1]);
+      if (!((dvalid >> k) & 1)) o = make_uint4(0u, 0u, 0u, 0u);  // pixels past the grid add nothing
+      *reinterpret_cast<uint4*>(Ad + p * ROWB + wg3_swz(p, ch) * 16) = o;
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int u = tid + k * NT;
+      if (u < UB) {
+        const int hp = u >> 3, ch = u & 7;
+        uint4 o;
+        if (x16) {
+          o = __builtin_bit_cast(uint4, rx[k][0]);
+        } else {
+          float4 v0 = rx[k][0], v1 = rx[k][1];
+          if (xtf) {
+            v0 = affine_relu4(v0, ld4(ssc + ch * 8), ld4(ssc + BC + ch * 8));
+            v1 = affine_relu4(v1, ld4(ssc + ch * 8 + 4), ld4(ssc + BC + ch * 8 + 4));
+          }
+          o = bf16pack8(v0, v1);
+        }
+        *reinterpret_cast<uint4*>(Bx + hp * ROWB + wg3_swz(hp, ch) * 16) = o;
+      }
+    }
+  };
+
+  floatx16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  // transposed-read lane roles: group g16 = lane >> 4 reads channel half (g16 & 1)
+  // of k half (g16 >> 1); lane 4q + p of the group addresses pixel row q, channels 4p..4p+3
+  const int g16 = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int hk = g16 >> 1;
+  const int ct = wave & 1, it_ = (wave >> 1) & 1, tap0 = (wave >> 2) * NTAP;
+  const int ntap = wave >> 2 ? 9 - NTAP : NTAP;  // wave-uniform
+  const int colA = ct * 32 + (g16 & 1) * 16 + pp * 4, colB = it_ * 32 + (g16 & 1) * 16 + pp * 4;
+  const int cA = colA >> 3, bA = (colA & 7) * 2, cB = colB >> 3, bB = (colB & 7) * 2;
+  auto compute = [&] {
+#pragma unroll 2
+    for (int ks = 0; ks < PT / 16; ++ks) {
+      const int prow = (ks * 16) / TW, px0 = (ks * 16) % TW;
+      bf16x8_t fa;
+      {
+        const int pa = ks * 16 + 8 * hk + q;
+        const bf16x4_t lo = tr_read(Ad + pa * ROWB + wg3_swz(pa, cA) * 16 + bA);
+        const bf16x4_t hi = tr_read(Ad + (pa + 4) * ROWB + wg3_swz(pa + 4, cA) * 16 + bA);
+        fa = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      }
+#pragma unroll
+      for (int j = 0; j < NTAP; ++j) {
+        if (j < ntap) {
+          const int tap = tap0 + j;
+          const int hb = (prow + tap / 3) * HW2 + px0 + tap % 3 + 8 * hk + q;
+          const bf16x4_t lo = tr_read(Bx + hb * ROWB + wg3_swz(hb, cB) * 16 + bB);
+          const bf16x4_t hi = tr_read(Bx + (hb + 4) * ROWB + wg3_swz(hb + 4, cB) * 16 + bB);
+          const bf16x8_t fb = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  if (xtf) __syncthreads();  // scale/shift table before the first commit
+  int t = blockIdx.z;
+  if (t < tiles) {
+    issue(t);
+    commit();
+  }
+  __syncthreads();
+  for (; t < tiles; t += gridDim.z) {
+    const bool more = t + (int)gridDim.z < tiles;
+    if (more) issue(t + gridDim.z);
+    compute();
+    __syncthreads();
+    if (more) {
+      commit();
+      __syncthreads();
+    }
+  }
+  // accumulate into out[co][tap * Ci + ci] (fp32 atomics, one per element per workgroup)
+  const int h = lane >> 5, li = lane & 31;
+#pragma unroll
+  for (int j = 0; j < NTAP; ++j) {
+    if (j < ntap) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = i0 + ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = (tap0 + j) * Ci + cb + it_ * 32 + li;
+        atomicAdd(args.out + (size_t)row * args.No + col, acc[j][r]);
+      }
+    }
+  }
+}
+
+template <int TH, int TW, int D16>
+static hipError_t go_wgrad3(const WgradArgs& a, hipStream_t s, int per_cu) {
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad3_bf<TH, TW, D16>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)wgrad3_smem<TH, TW>());
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int tiles = a.gb.nimg * ((a.gb.Hg + TH - 1) / TH) * ((a.gb.Wg + TW - 1) / TW);
+  const int blocks = (a.Mo / 64) * (a.gb.Cg / 64);
+  int splits = (per_cu * num_cus() + blocks - 1) / blocks;
+  splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
+  dim3 grid(a.Mo / 64, a.gb.Cg / 64, splits);
+  const size_t smem = wgrad3_smem<TH, TW>();
+  hipLaunchKernelGGL((k_wgrad3_bf<TH, TW, D16>), grid, dim3(512), smem, s, a);
+  return hipGetLastError();
+}
+
+// halo-tiled 3x3 weight gradient (tiles 20: 8x16, 21: 4x32 output pixels per step)
+bool wgrad3_fits(const WgradArgs& a) {
+  const Gather& g = a.gb;
+  return a.bf16 && g.taps_h == 3 && g.taps_w == 3 && g.stride == 1 && a.No == 9 * g.Cg && a.Mo % 64 == 0 &&
+         g.Cg % 64 == 0 && (g.c_split % 64 == 0 || g.c_split >= g.Cg) && a.ga.Cg == a.Mo && a.ga.taps_h == 1 &&
+         a.ga.taps_w == 1 && g.Hg == a.ga.Hg && g.Wg == a.ga.Wg && g.nimg == a.ga.nimg;
+}
+
+hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu) {
+  if (!wgrad3_fits(a)) return hipErrorInvalidValue;
+  const bool d16 = a.ga.s[0].h16 != 0;
+  switch (tile * 2 + (d16 ? 1 : 0)) {
+    case 40: return go_wgrad3<8, 16, 0>(a, s, per_cu);
+    case 41: return go_wgrad3<8, 16, 1>(a, s, per_cu);
+    case 42: return go_wgrad3<4, 32, 0>(a, s, per_cu);
+    case 43: return go_wgrad3<4, 32, 1>(a, s, per_cu);
+    default: return hipErrorInvalidValue;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // fp32 -> bf16 (RNE) of the packed weight region, 4 elements per lane-step
 // ---------------------------------------------------------------------------
 __global__ void k_f2bf(const float* __restrict__ in, uint16_t* __restrict__ out, size_t n4) {
@@ -385,8 +871,47 @@ static hipError_t go_bf(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int TH, int TW, int BN, int WM, int WN, int MINW>
+static hipError_t go_halo(const IgemmArgs& a, hipStream_t s) {
+  if (a.bh == nullptr || a.N % BN != 0 || a.a.Cg % 32 != 0 || a.a.c_split % 32 != 0 || a.a.taps_h != 3 ||
+      a.a.taps_w != 3 || a.a.stride != 1 || a.K != 9 * a.a.Cg || a.a.Cg > 1024)
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3_bf<TH, TW, BN, WM, WN, MINW>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize,
+                                       (int)conv3_bf_smem<TH, TW, BN>(1024));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const long long tiles = (long long)a.a.nimg * ((a.a.Hg + TH - 1) / TH) * ((a.a.Wg + TW - 1) / TW);
+  dim3 grid((unsigned)tiles, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
+  const size_t smem = conv3_bf_smem<TH, TW, BN>(a.a.Cg);
+  hipLaunchKernelGGL((k_conv3_bf<TH, TW, BN, WM, WN, MINW>), grid, dim3(WM * WN * 64), smem, s, a);
+  return hipGetLastError();
+}
+
+// halo tile shapes: id -> (TH, TW, BN); see go_igemm_bf16
+bool halo_tile_shape(int tile, int& th, int& tw, int& bn) {
+  switch (tile) {
+    case 31: th = 8; tw = 32; bn = 64; return true;
+    case 32: th = 8; tw = 32; bn = 64; return true;
+    case 33: th = 16; tw = 16; bn = 64; return true;
+    case 34: th = 4; tw = 32; bn = 128; return true;
+    case 35: th = 8; tw = 16; bn = 64; return true;
+    case 36: th = 8; tw = 32; bn = 128; return true;
+    default: return false;
+  }
+}
+
 hipError_t go_igemm_bf16(const IgemmArgs& a, hipStream_t s, int tile) {
   switch (tile) {
+    case 31: return go_halo<8, 32, 64, 8, 1, 4>(a, s);
+    case 32: return go_halo<8, 32, 64, 4, 1, 2>(a, s);
+    case 33: return go_halo<16, 16, 64, 8, 1, 4>(a, s);
+    case 34: return go_halo<4, 32, 128, 4, 2, 2>(a, s);
+    case 35: return go_halo<8, 16, 64, 4, 1, 2>(a, s);
+    case 36: return go_halo<8, 32, 128, 4, 2, 2>(a, s);
     case 21: return go_bf<256, 128, 4, 2>(a, s);
     case 22: return go_bf<128, 128, 2, 2>(a, s);
     case 23: return go_bf<128, 64, 2, 2>(a, s);
@@ -397,17 +922,32 @@ hipError_t go_igemm_bf16(const IgemmArgs& a, hipStream_t s, int tile) {
   }
 }
 
-hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid) {
-  if (!a.bf16 || a.pix_per_split % kBfBK != 0) return hipErrorInvalidValue;
+template <int AH, int BH>
+static hipError_t wgrad_bf_tile(const WgradArgs& a, hipStream_t s, int tile, dim3 grid) {
   switch (tile) {
-    case 10: hipLaunchKernelGGL((k_wgrad_bf<128, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
-    case 11: hipLaunchKernelGGL((k_wgrad_bf<128, 192, 2, 2>), grid, dim3(256), 0, s, a); break;
-    case 12: hipLaunchKernelGGL((k_wgrad_bf<64, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
-    case 13: hipLaunchKernelGGL((k_wgrad_bf<64, 64, 2, 2>), grid, dim3(256), 0, s, a); break;
-    case 14: hipLaunchKernelGGL((k_wgrad_bf<256, 128, 4, 2>), grid, dim3(512), 0, s, a); break;
+    case 10: hipLaunchKernelGGL((k_wgrad_bf<128, 128, 2, 2, AH, BH>), grid, dim3(256), 0, s, a); break;
+    case 11: hipLaunchKernelGGL((k_wgrad_bf<128, 192, 2, 2, AH, BH>), grid, dim3(256), 0, s, a); break;
+    case 12: hipLaunchKernelGGL((k_wgrad_bf<64, 128, 2, 2, AH, BH>), grid, dim3(256), 0, s, a); break;
+    case 13: hipLaunchKernelGGL((k_wgrad_bf<64, 64, 2, 2, AH, BH>), grid, dim3(256), 0, s, a); break;
+    case 14: hipLaunchKernelGGL((k_wgrad_bf<256, 128, 4, 2, AH, BH>), grid, dim3(512), 0, s, a); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
+}
+
+hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid) {
+  if (!a.bf16 || a.pix_per_split % kBfBK != 0) return hipErrorInvalidValue;
+  const int ah = a.ga.s[0].h16;
+  const bool two = a.gb.c_split < a.gb.Cg;
+  const int bh = two && a.gb.s[0].h16 != a.gb.s[1].h16 ? 2 : a.gb.s[0].h16;
+  switch (ah * 3 + bh) {
+    case 0: return wgrad_bf_tile<0, 0>(a, s, tile, grid);
+    case 1: return wgrad_bf_tile<0, 1>(a, s, tile, grid);
+    case 2: return wgrad_bf_tile<0, 2>(a, s, tile, grid);
+    case 3: return wgrad_bf_tile<1, 0>(a, s, tile, grid);
+    case 4: return wgrad_bf_tile<1, 1>(a, s, tile, grid);
+    default: return wgrad_bf_tile<1, 2>(a, s, tile, grid);
+  }
 }
 
 }  // namespace unet

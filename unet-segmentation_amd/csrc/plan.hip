@@ -199,7 +199,7 @@ std::string wgrad_key(const WgradArgs& a) {
 std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) {
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
-  for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 21, 22, 23, 24, 25, 26}) {  // fits() filters by precision
+  for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35, 36}) {  // fits() filters
     if (!igemm_tile_fits(a, t)) continue;
     v.push_back({t, 1});
     const long long cnt = igemm_tile_count(a, t);
@@ -215,8 +215,12 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
 
 std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   std::vector<GemmChoice> v;
-  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14}) {  // fits() filters by precision
+  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21}) {  // fits() filters by precision
     if (!wgrad_tile_fits(a, t)) continue;
+    if (t >= 20) {  // halo-tiled: workgroups per CU (2 resident)
+      for (int per_cu : {2, 4, 8}) v.push_back({t, per_cu});
+      continue;
+    }
     for (int per_cu : {4, 8, 16}) v.push_back({t, per_cu});
   }
   return v;
@@ -374,6 +378,7 @@ Gather input_gather(const Ctx& c, int l) {
     s.H = pl.h / 2;
     s.W = pl.w / 2;
     s.C = pl.c;
+    s.h16 = p->prec == UNET_PREC_BF16;
     g.s[0] = s;
     g.Cg = g.c_split = L.ci;
   } else {  // first conv of up block: cat([crop(skip), up], 1)
@@ -388,6 +393,7 @@ Gather input_gather(const Ctx& c, int l) {
     b.H = 2 * p->T[k].h;
     b.W = 2 * p->T[k].w;
     b.C = p->T[k].co;
+    b.h16 = p->prec == UNET_PREC_BF16;
     g.s[0] = a;
     g.s[1] = b;
     g.c_split = sk.c;
@@ -461,7 +467,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       a.K = T.ci;
       a.e.bias = P<float>(prm, T.pw + 1);  // bias[co], col = ab*Co + co
       a.e.shuffle_co = T.co;
-      a.e.d[0] = Dst{c.f(T.u), 2 * T.h, 2 * T.w, T.co, 0, 0};
+      a.e.d[0] = Dst{c.f(T.u), 2 * T.h, 2 * T.w, T.co, 0, 0, p->prec == UNET_PREC_BF16};
       Timer t(p, s, UNET_KC_CONV_FWD, 2.0 * a.M * a.N * a.K, 0);
       CK(run_igemm(c, a));
     }
@@ -482,7 +488,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
     if (l <= 7 && l % 2 == 1) {  // encoder output -> MaxPool2d(2)
       Pool& pl = p->P[l / 2];
       Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * pl.h * pl.w * pl.c * 1.25);
-      CK(launch_maxpool_fwd(src_of(c, L, true), n, pl.h, pl.w, c.f(pl.p), c.u8(pl.arg), s));
+      CK(launch_maxpool_fwd(src_of(c, L, true), n, pl.h, pl.w, c.f(pl.p), c.u8(pl.arg), s, p->prec == UNET_PREC_BF16));
     }
   }
   {
@@ -540,11 +546,14 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     if (!in_seg(seg_of_layer(l))) continue;
     Conv& L = p->L[l];
     const double M = (double)n * L.ho * L.wo;
+    const int dy16 = p->prec == UNET_PREC_BF16 && l > 0;
     CK(launch_bnb_finalize(c.d(L.bstats), L.co, M, P<float>(prm, L.pw + 2), c.f(L.mean), c.f(L.invstd),
                            P<float>(grd, L.gw + 2), P<float>(grd, L.gw + 3), P<float>(grd, L.gw + 1), c.f(L.coef), s));
     {
       Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * ((double)(L.ho + 4) * (L.wo + 4) + 2.0 * L.ho * L.wo) * L.co);
-      CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), n, L.ho, L.wo, L.co, c.f(L.dyp), 2, s));
+      // bf16 plans store dY(l > 0) in bf16: it only feeds bf16 GEMMs (inc.c0's
+      // fp32 direct weight-gradient kernel reads dY(0))
+      CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), n, L.ho, L.wo, L.co, c.f(L.dyp), 2, s, dy16));
     }
     if (conc) {
       CK(hipEventRecord(p->ev_dy[l], s));
@@ -556,6 +565,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     dy.W = L.wo + 4;
     dy.C = L.co;
     dy.oy = dy.ox = 2;
+    dy.h16 = dy16;
     if (l == 0) {
       Timer t(p, sw, UNET_KC_STAGE1, 2.0 * M * L.co * L.ci * 9,
               4.0 * n * ((double)p->cin * p->h * p->w + (double)L.ho * L.wo * L.co));
@@ -624,7 +634,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       ConvT& T = p->T[k];
       Skip& sk = p->S[k];
       a.e.d[0] = Dst{c.f(sk.d), sk.th, sk.tw, sk.c, 0, 0};
-      a.e.d[1] = Dst{c.f(T.du), 2 * T.h, 2 * T.w, T.co, 0, 0};
+      a.e.d[1] = Dst{c.f(T.du), 2 * T.h, 2 * T.w, T.co, 0, 0, p->prec == UNET_PREC_BF16};
       a.e.n_split = sk.c;
       a.e.colsum1 = c.d(T.colsum);
       {
@@ -651,6 +661,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
         du.H = 2 * T.h;
         du.W = 2 * T.w;
         du.C = T.co;
+        du.h16 = p->prec == UNET_PREC_BF16;
         w.gb.s[0] = du;
         w.gb.s[1] = du;
         w.gb.Cg = w.gb.c_split = T.co;
@@ -674,6 +685,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       du.H = 2 * T.h;
       du.W = 2 * T.w;
       du.C = T.co;
+      du.h16 = p->prec == UNET_PREC_BF16;
       b.a.s[0] = du;
       b.a.s[1] = du;
       b.a.Cg = b.a.c_split = T.co;

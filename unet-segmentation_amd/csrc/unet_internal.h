@@ -18,6 +18,11 @@ struct Src {
   int oy = 0, ox = 0;        // origin added to the pixel position (crop / pad)
   const float* scale = nullptr;  // nullptr: identity
   const float* shift = nullptr;
+  // 1: the elements are bf16 (ptr reinterpreted as uint16_t*).  Only tensors
+  // that are GEMM operands and nothing else (pooled maps, padded dY, convT
+  // output and its gradient) are stored this way, in UNET_PREC_BF16 plans --
+  // the GEMMs round them to bf16 anyway -- and never with a transform.
+  int h16 = 0;
 };
 
 // Implicit-GEMM gather of operand rows: row m enumerates pixels of an
@@ -41,6 +46,7 @@ struct Dst {
   float* ptr = nullptr;
   int H = 0, W = 0, C = 0;
   int oy = 0, ox = 0;
+  int h16 = 0;  // 1: store bf16 (RNE; ptr reinterpreted as uint16_t*)
 };
 
 struct Epilogue {
@@ -110,7 +116,12 @@ hipError_t launch_wgrad_v(const WgradArgs& a, hipStream_t s, GemmChoice c);
 bool wgrad_tile_fits(const WgradArgs& a, int tile);
 // bf16-operand kernels (igemm_bf16.hip), dispatched by the launchers above
 hipError_t go_igemm_bf16(const IgemmArgs& a, hipStream_t s, int tile);
+// halo-tiled 3x3 tiles 31-36: output tile TH x TW pixels x BN columns
+bool halo_tile_shape(int tile, int& th, int& tw, int& bn);
 hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid);
+// halo-tiled 3x3 weight gradient (wgrad tiles 20, 21): all 9 taps per workgroup
+bool wgrad3_fits(const WgradArgs& a);
+hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
 // out[i] = bf16(in[i]) (RNE), n a multiple of 4, both 16-B aligned
 hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s);
 
@@ -141,10 +152,10 @@ hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const 
                                float* dbeta, float* dbias_conv, float* coef, hipStream_t s);
 // dYpad interior = coef0*dz + coef1*y + coef2; border (pad each side) = 0.
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h,
-                            int w, int c, float* dypad, int pad, hipStream_t s);
+                            int w, int c, float* dypad, int pad, hipStream_t s, int out_h16 = 0);
 // MaxPool2d(2) fwd with BN+ReLU transform on load (src grid H x W, pooled H/2 x W/2).
 hipError_t launch_maxpool_fwd(const Src& src, int n, int h, int w, float* y, uint8_t* arg,
-                              hipStream_t s);
+                              hipStream_t s, int out_h16 = 0);
 // Maxpool bwd fused: dz = route(dpool) + crop-embedded dskip (may be null), then
 // ReLU mask + BN-bwd stats (if scale != null).  Writes dz' (n,h,w,c).
 hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, const float* dskip,
