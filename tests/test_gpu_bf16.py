@@ -89,8 +89,9 @@ def op_bf16(lib):
 
 
 # per-op GEMM tile: -1 = built-in choice (row-gather k_igemm_bf), 31-36 = the
-# halo-tiled k_conv3_bf shapes (8x32, 16x16, 4x32/128, 8x16, 8x32/128)
-HALO = [-1, 31, 32, 33, 34, 35, 36]
+# halo-tiled k_conv3_bf shapes (8x32, 16x16, 4x32/128, 8x16, 8x32/128), 41-44 =
+# the persistent pipelined k_conv3p_bf (8x32 / 16x16, one or two rounds per CU)
+HALO = [-1, 31, 32, 33, 34, 35, 36, 41, 42, 44]
 
 
 # ------------------------------- per-op -------------------------------------
@@ -275,7 +276,8 @@ def gemm_mode(request, lib):
 
 @pytest.mark.parametrize("gemm_mode", ["heuristic", "tile21", "tile22", "tile23", "tile24", "tile25", "tile26",
                                        "tile22+split3", "tile24+split8", "tile31", "tile32", "tile33", "tile34",
-                                       "tile35", "tile36", "tile31+split2", "tile34+split3"], indirect=True)
+                                       "tile35", "tile36", "tile31+split2", "tile34+split3", "tile41", "tile42",
+                                       "tile43", "tile44", "tile41+split3"], indirect=True)
 def test_bf16_gemm_variants_vs_bf16_oracle(gemm_mode):
     """Every bf16 tile (21-26 row gather, 31-36 halo-tiled 3x3 -- the convT GEMMs
     fall back to the built-in tile there) and split-K on every conv / convT /

@@ -744,11 +744,12 @@ static TileInfo tile_info(int id) {
     case 34: return {128, 128, 288, 1};
     case 35: return {128, 64, 288, 2};
     case 36: return {256, 128, 288, 1};
+    case 41: case 42: case 43: case 44: return {256, 64, 288, 1};  // persistent k_conv3p_bf
     default: return {0, 0, 0, 0};
   }
 }
 
-static bool is_halo_tile(int tile) { return tile >= 31 && tile <= 36; }
+static bool is_halo_tile(int tile) { return (tile >= 31 && tile <= 36) || (tile >= 41 && tile <= 44); }
 static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_halo_tile(tile); }
 
 // A tile applies when the shape divides and the packed B operand is in the
@@ -817,7 +818,8 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 13: return go_igemm_g<64, 128, 2, 2>(a, s);
     case 14: return go_igemm_g<128, 64, 2, 2>(a, s);
     case 21: case 22: case 23: case 24: case 25: case 26:
-    case 31: case 32: case 33: case 34: case 35: case 36: return go_igemm_bf16(a, s, tile);
+    case 31: case 32: case 33: case 34: case 35: case 36:
+    case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
     default: return hipErrorInvalidValue;
   }
 }

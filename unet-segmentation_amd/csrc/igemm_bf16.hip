@@ -594,6 +594,214 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
 }
 
 // ---------------------------------------------------------------------------
+// k_conv3p_bf: the halo-tiled 3x3 GEMM of k_conv3_bf as a persistent, software-
+// pipelined loop.  A workgroup owns one 64-column block (blockIdx.y) and walks
+// (tile, 32-channel chunk) stages of its tiles (tile = blockIdx.x + i*gridDim.x,
+// chunks of its split-K slice blockIdx.z).  Two LDS stage buffers: while stage
+// s computes from one, stage s+1 (loaded into registers during stage s-1) is
+// committed into the other and stage s+2's loads are issued -- one barrier per
+// stage, load latency hidden behind a whole stage of MFMAs, no pipeline drain
+// at tile boundaries (the epilogue of a finished tile runs between stages).
+// LDS rows are 64 B (32 bf16) without padding; the 16-B chunk c of row r sits
+// at slot c ^ ((r >> 2) & 3), which keeps every ds_read_b128 group of 16 lanes
+// (16 consecutive rows from any start) on distinct bank quads.
+// 8 waves (WM = 8 along the tile's 32-pixel fragments, TN = 2), BN = 64.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int c3p_off(int row, int chunk) { return row * 32 + ((chunk ^ ((row >> 2) & 3)) << 3); }
+
+template <int TH, int TW>
+constexpr size_t conv3p_smem(int cg) {
+  return (size_t)2 * ((TH + 2) * (TW + 2) + 9 * 64) * 64 + (size_t)2 * cg * 4 + (size_t)8 * 3 * 64 * 4;
+}
+
+template <int TH, int TW>
+__global__ __launch_bounds__(512, 2) void k_conv3p_bf(const IgemmArgs args) {
+  constexpr int NT = 512, BN = 64, WM = 8, WN = 1, BM = TH * TW;
+  constexpr int HW2 = TW + 2, PH = (TH + 2) * HW2;
+  constexpr int FM = BM / 32, TM = FM / WM, TN = BN / 32;
+  constexpr int UA = PH * 4, UB = 9 * BN * 4;  // 16-B staging units
+  constexpr int NA = (UA + NT - 1) / NT, NB = (UB + NT - 1) / NT;
+  constexpr int A_EL = PH * 32, B_EL = 9 * BN * 32, ST_EL = A_EL + B_EL;  // bf16 elements
+  static_assert(BM % 32 == 0 && FM % WM == 0 && TM >= 1, "tile");
+  extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
+  float* ssc = reinterpret_cast<float*>(smem + 2 * ST_EL);  // [2][Cg]
+  const Gather& g = args.a;
+  const int Cg = g.Cg, K = args.K, Hg = g.Hg, Wg = g.Wg;
+  float* red = ssc + 2 * Cg;  // epilogue reduction [WM*3][BN]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int n0 = blockIdx.y * BN;
+  const int tiles_x = (Wg + TW - 1) / TW, tiles_y = (Hg + TH - 1) / TH;
+  const int tiles = g.nimg * tiles_x * tiles_y;
+
+  const bool any_tf = g.s[0].scale != nullptr || (g.c_split < Cg && g.s[1].scale != nullptr);
+  if (any_tf) {
+    for (int c = tid; c < Cg; c += NT) {
+      const bool sec = c >= g.c_split;
+      const Src& sr = sec ? g.s[1] : g.s[0];
+      const int cl = sec ? c - g.c_split : c;
+      ssc[c] = sr.scale ? sr.scale[cl] : 1.f;
+      ssc[Cg + c] = sr.scale ? sr.shift[cl] : 0.f;
+    }
+  }
+
+  // K slice of this workgroup (split-K over blockIdx.z) and its stage list
+  const int nk_all = Cg / 32;
+  int kc0 = 0, kc1 = nk_all;
+  if (args.ksplit > 1) {
+    const int per = (nk_all + args.ksplit - 1) / args.ksplit;
+    kc0 = blockIdx.z * per;
+    kc1 = min(nk_all, kc0 + per);
+  }
+  const int nk = kc1 - kc0;
+  const int my_tiles = (tiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
+  const int S = nk > 0 ? my_tiles * nk : 0;
+
+  // B staging units (tap, row, piece) are the same for every stage but the chunk
+  const uint16_t* bsrc[NB];
+  int boff[NB];
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int u = min(tid + k * NT, UB - 1);
+    const int r = (u >> 2) % BN, tap = (u >> 2) / BN;
+    bsrc[k] = args.bh + (size_t)(n0 + r) * K + tap * Cg + (u & 3) * 8;
+    boff[k] = A_EL + c3p_off(u >> 2, u & 3);
+  }
+
+  float4 ra[NA][2];
+  uint4 rb[NB];
+  auto tile_of = [&](int s, int& n, int& y0, int& x0) {
+    int t = (int)blockIdx.x + (s / nk) * (int)gridDim.x;
+    x0 = (t % tiles_x) * TW;
+    t /= tiles_x;
+    y0 = (t % tiles_y) * TH;
+    n = t / tiles_y;
+  };
+  auto issue = [&](int s) {
+    int n, y0, x0;
+    tile_of(s, n, y0, x0);
+    const int c0 = (kc0 + s % nk) * 32;
+    const bool second = c0 >= g.c_split;
+    const Src& src = second ? g.s[1] : g.s[0];
+    const int cl = (second ? c0 - g.c_split : c0) + (tid & 3) * 8;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = min(tid + k * NT, UA - 1);
+      const int ph = u >> 2;
+      const int yy = min(y0 + ph / HW2, Hg + 1), xx = min(x0 + ph % HW2, Wg + 1);  // overhang: any in-range pixel
+      const size_t e = (size_t)((n * src.H + yy + src.oy) * src.W + xx + src.ox) * src.C + cl;
+      if (src.h16) {
+        ra[k][0] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(src.ptr) + e));
+      } else {
+        ra[k][0] = ld4(src.ptr + e);
+        ra[k][1] = ld4(src.ptr + e + 4);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) rb[k] = *reinterpret_cast<const uint4*>(bsrc[k] + c0);
+  };
+  auto commit = [&](int s, int buf) {
+    unsigned short* st = smem + buf * ST_EL;
+    const int c = (kc0 + s % nk) * 32 + (tid & 3) * 8;
+    const Src& src = c >= g.c_split ? g.s[1] : g.s[0];
+    const bool tf = src.scale != nullptr, h16 = src.h16 != 0;
+    float4 sc0, sc1, sh0, sh1;
+    if (tf) {
+      sc0 = ld4(ssc + c);
+      sc1 = ld4(ssc + c + 4);
+      sh0 = ld4(ssc + Cg + c);
+      sh1 = ld4(ssc + Cg + c + 4);
+    }
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      if (u < UA) {
+        uint4 o;
+        if (h16) {
+          o = __builtin_bit_cast(uint4, ra[k][0]);
+        } else {
+          float4 v0 = ra[k][0], v1 = ra[k][1];
+          if (tf) {
+            v0 = affine_relu4(v0, sc0, sh0);
+            v1 = affine_relu4(v1, sc1, sh1);
+          }
+          o = bf16pack8(v0, v1);
+        }
+        *reinterpret_cast<uint4*>(st + c3p_off(u >> 2, u & 3)) = o;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (tid + k * NT < UB) *reinterpret_cast<uint4*>(st + boff[k]) = rb[k];
+  };
+
+  floatx16 acc[TM][TN];
+  auto zero_acc = [&] {
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  };
+  zero_acc();
+
+  const int h = lane >> 5, li = lane & 31;
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = (wm * TM + i) * 32 + li;
+    abase[i] = (p / TW) * HW2 + p % TW;
+  }
+  auto compute = [&](int buf) {
+    const unsigned short* st = smem + buf * ST_EL;
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int off = (tap / 3) * HW2 + tap % 3;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int ch = 2 * s + h;
+        bf16x8_t fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          fa[i] = *reinterpret_cast<const bf16x8_t*>(st + c3p_off(abase[i] + off, ch));
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const bf16x8_t*>(st + A_EL + c3p_off(tap * BN + wn * TN * 32 + j * 32 + li, ch));
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      }
+    }
+  };
+
+  if (any_tf) __syncthreads();  // scale/shift table before the first commit
+  if (S > 0) {
+    issue(0);
+    commit(0, 0);
+    if (S > 1) issue(1);
+  }
+  __syncthreads();
+  for (int s = 0; s < S; ++s) {
+    if (s + 1 < S) {
+      commit(s + 1, (s + 1) & 1);  // buffer of stage s-1: free since the last barrier
+      if (s + 2 < S) issue(s + 2);
+    }
+    compute(s & 1);
+    if (s % nk == nk - 1) {  // tile finished: epilogue (its own LDS reduction buffer)
+      int n, y0, x0;
+      tile_of(s, n, y0, x0);
+      igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, red, HaloRows<TW>{n, y0, x0, Hg, Wg});
+      zero_acc();
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------
 // k_wgrad3_bf: halo-tiled weight gradient of a 3x3 stride-1 conv, all 9 taps in
 // one workgroup.  dW[co][tap][ci] = sum_p dY[p][co] * X[p + tap][ci].  A
 // workgroup owns 64 output channels (co) x 64 input channels (ci) x 9 taps and
@@ -891,6 +1099,29 @@ static hipError_t go_halo(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int TH, int TW>
+static hipError_t go_halo_p(const IgemmArgs& a, hipStream_t s, int waves_of_cus) {
+  if (a.bh == nullptr || a.N % 64 != 0 || a.a.Cg % 32 != 0 || a.a.c_split % 32 != 0 || a.a.taps_h != 3 ||
+      a.a.taps_w != 3 || a.a.stride != 1 || a.K != 9 * a.a.Cg || a.a.Cg > 1024)
+    return hipErrorInvalidValue;
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3p_bf<TH, TW>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)conv3p_smem<TH, TW>(1024));
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const long long tiles = (long long)a.a.nimg * ((a.a.Hg + TH - 1) / TH) * ((a.a.Wg + TW - 1) / TW);
+  const int ks = a.ksplit > 1 ? a.ksplit : 1;
+  const long long cols = (long long)(a.N / 64) * ks;
+  long long gx = ((long long)waves_of_cus * num_cus() + cols - 1) / cols;  // one resident workgroup per CU
+  gx = gx < 1 ? 1 : (gx > tiles ? tiles : gx);
+  dim3 grid((unsigned)gx, a.N / 64, ks);
+  const size_t smem = conv3p_smem<TH, TW>(a.a.Cg);
+  hipLaunchKernelGGL((k_conv3p_bf<TH, TW>), grid, dim3(512), smem, s, a);
+  return hipGetLastError();
+}
+
 // halo tile shapes: id -> (TH, TW, BN); see go_igemm_bf16
 bool halo_tile_shape(int tile, int& th, int& tw, int& bn) {
   switch (tile) {
@@ -900,6 +1131,8 @@ bool halo_tile_shape(int tile, int& th, int& tw, int& bn) {
     case 34: th = 4; tw = 32; bn = 128; return true;
     case 35: th = 8; tw = 16; bn = 64; return true;
     case 36: th = 8; tw = 32; bn = 128; return true;
+    case 41: case 43: th = 8; tw = 32; bn = 64; return true;
+    case 42: case 44: th = 16; tw = 16; bn = 64; return true;
     default: return false;
   }
 }
@@ -912,6 +1145,11 @@ hipError_t go_igemm_bf16(const IgemmArgs& a, hipStream_t s, int tile) {
     case 34: return go_halo<4, 32, 128, 4, 2, 2>(a, s);
     case 35: return go_halo<8, 16, 64, 4, 1, 2>(a, s);
     case 36: return go_halo<8, 32, 128, 4, 2, 2>(a, s);
+    // persistent pipelined (k_conv3p_bf): 1 or 2 rounds of workgroups per CU
+    case 41: return go_halo_p<8, 32>(a, s, 1);
+    case 42: return go_halo_p<16, 16>(a, s, 1);
+    case 43: return go_halo_p<8, 32>(a, s, 2);
+    case 44: return go_halo_p<16, 16>(a, s, 2);
     case 21: return go_bf<256, 128, 4, 2>(a, s);
     case 22: return go_bf<128, 128, 2, 2>(a, s);
     case 23: return go_bf<128, 64, 2, 2>(a, s);
