@@ -431,12 +431,14 @@ class UNetOracle:
     backward.  ``params`` maps reference state_dict names -> arrays (PyTorch
     shapes); activations are NHWC in ``dtype``.
 
-    ``gemm="bf16"`` restates the HIP path's bf16-operand GEMMs (UNET_PREC_BF16,
-    the reference's convs under torch.autocast(bfloat16)): every 3x3 conv after
-    the first, every ConvTranspose2d and their input / weight gradients see both
-    operands rounded to bf16 (after the producer's BatchNorm+ReLU); products
-    are accumulated exactly.  The first conv (Ci <= 4), the 1x1 head, BatchNorm,
-    pooling, biases, the loss and every stored activation stay unrounded."""
+    ``gemm="bf16"`` restates the HIP path's bf16 arithmetic (UNET_PREC_BF16, the
+    reference's convs under torch.autocast(bfloat16)): every 3x3 conv after the
+    first, every ConvTranspose2d and their input / weight gradients see both
+    operands rounded to bf16 (after the producer's BatchNorm+ReLU), products
+    accumulated exactly; every raw conv output (the first conv's too) is
+    rounded to bf16 before BatchNorm, as the bf16 plan stores it.  The first
+    conv's arithmetic (Ci <= 4), the 1x1 head, BatchNorm statistics, pooling,
+    biases, gradients and the loss stay unrounded."""
 
     def __init__(self, params, dtype=np.float64, bn_momentum=BN_MOMENTUM, gemm="fp32"):
         if gemm not in ("fp32", "bf16"):
@@ -468,6 +470,7 @@ class UNetOracle:
             q = not (pre == _dc_prefix("inc") and conv_i == "0")  # first conv: direct fp32 kernel
             y = conv_valid_fwd(self._q(a, q), self._q(self._w(pre + conv_i + ".weight"), q),
                                self._w(pre + conv_i + ".bias"))
+            y = self._q(y)  # bf16 plans store every raw conv output in bf16 (BatchNorm sees the rounded values)
             g, b = self._w(pre + bn_i + ".weight"), self._w(pre + bn_i + ".bias")
             if train:
                 z, bn_cache, mean, var_unb = bn_train_fwd(y, g, b)

@@ -43,7 +43,7 @@ __device__ void reduce_pairs_to_global(const float (&a)[4], const float (&b)[4],
 // + conv bias, + BatchNorm batch statistics (sum, sumsq) of the output.
 // Block = one output row segment of 64 pixels; thread = (channel, pixel phase).
 // ---------------------------------------------------------------------------
-template <int CI>
+template <int CI, int H16>  // H16: y stored bf16 (statistics of the rounded values)
 __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict__ x, int h, int w,
                                                         const float* __restrict__ wt,
                                                         const float* __restrict__ bias, float* __restrict__ y,
@@ -76,7 +76,13 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict_
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) acc = fmaf(tile[ci][ky][px + kx], wr[(ci * 3 + ky) * 3 + kx], acc);
     if (gx < wo) {
-      y[((size_t)(n * ho + row) * wo + gx) * 64 + c] = acc;
+      const size_t yi = ((size_t)(n * ho + row) * wo + gx) * 64 + c;
+      if (H16) {
+        acc = round_bf(acc);
+        reinterpret_cast<uint16_t*>(y)[yi] = bf16_of(acc);
+      } else {
+        y[yi] = acc;
+      }
       s1 += acc;
       s2 += acc * acc;
     }
@@ -201,16 +207,23 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ 
                                                         red[3][threadIdx.x]);
 }
 
+template <int H16>
+static void conv_first_go(dim3 grid, int ci, const float* x, int h, int w, const float* wt, const float* bias, float* y,
+                          double* stats, hipStream_t s) {
+  switch (ci) {
+    case 1: hipLaunchKernelGGL((k_conv_first_fwd<1, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+    case 2: hipLaunchKernelGGL((k_conv_first_fwd<2, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+    case 3: hipLaunchKernelGGL((k_conv_first_fwd<3, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+    default: hipLaunchKernelGGL((k_conv_first_fwd<4, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+  }
+}
+
 hipError_t launch_conv_first_fwd(const float* x, int n, int ci, int h, int w, const float* wt,
-                                 const float* bias, int co, float* y, double* stats, hipStream_t s) {
+                                 const float* bias, int co, float* y, double* stats, hipStream_t s, int out_h16) {
   if (co != 64 || ci < 1 || ci > 4 || h < 3 || w < 3) return hipErrorInvalidValue;
   dim3 grid(cdiv(w - 2, 64), h - 2, n);
-  switch (ci) {
-    case 1: hipLaunchKernelGGL(k_conv_first_fwd<1>, grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
-    case 2: hipLaunchKernelGGL(k_conv_first_fwd<2>, grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
-    case 3: hipLaunchKernelGGL(k_conv_first_fwd<3>, grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
-    default: hipLaunchKernelGGL(k_conv_first_fwd<4>, grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
-  }
+  if (out_h16) conv_first_go<1>(grid, ci, x, h, w, wt, bias, y, stats, s);
+  else conv_first_go<0>(grid, ci, x, h, w, wt, bias, y, stats, s);
   return hipGetLastError();
 }
 
@@ -319,7 +332,7 @@ __global__ __launch_bounds__(256) void k_bnb_finalize(const double* __restrict__
 
 // dYpad[n][y+pad][x+pad][c] = k0*dz + k1*(y - mean) + k2 ; border written as 0.
 // H16: dYpad stored bf16 (it is only ever a bf16 GEMM operand then).
-template <int H16>
+template <int H16, int Y16>  // H16: dYpad stored bf16; Y16: y stored bf16
 __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restrict__ yr,
                             const float* __restrict__ coef, int n, int h, int w, int C,
                             float* __restrict__ dyp, int pad) {
@@ -338,7 +351,9 @@ __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restric
     float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
     if (yy >= 0 && yy < h && xx >= 0 && xx < w) {
       const size_t src = (((size_t)nn * h + yy) * w + xx) * C + c4 * 4;
-      const float4 d = ld4(dz + src), yv = ld4(yr + src);
+      const float4 d = ld4(dz + src);
+      const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + src))
+                            : ld4(yr + src);
       const float4 k0 = ld4(coef + c4 * 4), k1 = ld4(coef + C + c4 * 4), k2 = ld4(coef + 2 * C + c4 * 4),
                    mu = ld4(coef + 3 * C + c4 * 4);
       out.x = fmaf(k0.x, d.x, fmaf(k1.x, yv.x - mu.x, k2.x));
@@ -374,15 +389,16 @@ hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const 
   return hipGetLastError();
 }
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h, int w, int c,
-                            float* dypad, int pad, hipStream_t s, int out_h16) {
+                            float* dypad, int pad, hipStream_t s, int out_h16, int y_h16) {
   if (c % 4) return hipErrorInvalidValue;
   const long long work = (long long)n * (h + 2 * pad) * (w + 2 * pad) * (c / 4);
-  if (out_h16)
-    hipLaunchKernelGGL(k_bnb_apply<1>, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, s, dz, y, coef, n, h, w, c,
-                       dypad, pad);
-  else
-    hipLaunchKernelGGL(k_bnb_apply<0>, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, s, dz, y, coef, n, h, w, c,
-                       dypad, pad);
+  const dim3 grid(grid_cap(work, 256, 8192));
+  switch (out_h16 * 2 + y_h16) {
+    case 0: hipLaunchKernelGGL((k_bnb_apply<0, 0>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad); break;
+    case 1: hipLaunchKernelGGL((k_bnb_apply<0, 1>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad); break;
+    case 2: hipLaunchKernelGGL((k_bnb_apply<1, 0>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad); break;
+    default: hipLaunchKernelGGL((k_bnb_apply<1, 1>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad); break;
+  }
   return hipGetLastError();
 }
 
@@ -390,7 +406,7 @@ hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, 
 // MaxPool2d(2) forward (models/unet_model.py:28) of relu(bn(y)): floor mode,
 // scan order (0,0),(0,1),(1,0),(1,1) with strict '>' so the FIRST max wins.
 // ---------------------------------------------------------------------------
-template <int H16>  // pooled map stored bf16 (a bf16 GEMM operand only)
+template <int H16, int Y16>  // H16: pooled map stored bf16 (a GEMM operand only); Y16: input y stored bf16
 __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y, uint8_t* __restrict__ arg) {
   const int C = s.C, C4 = C / 4, ho = h / 2, wo = w / 2;
   const long long total = (long long)n * ho * wo * C4;
@@ -406,7 +422,9 @@ __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y,
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       const int yy = 2 * yo + (k >> 1), xx = 2 * xo + (k & 1);
-      float4 t = ld4(s.ptr + ((size_t)(nn * s.H + yy + s.oy) * s.W + xx + s.ox) * C + c4 * 4);
+      const size_t si = ((size_t)(nn * s.H + yy + s.oy) * s.W + xx + s.ox) * C + c4 * 4;
+      float4 t = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + si))
+                     : ld4(s.ptr + si);
       if (s.scale) {
         const float4 a = ld4(s.scale + c4 * 4), b = ld4(s.shift + c4 * 4);
         t.x = fmaxf(fmaf(t.x, a.x, b.x), 0.f);
@@ -435,18 +453,22 @@ __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y,
 
 hipError_t launch_maxpool_fwd(const Src& s, int n, int h, int w, float* y, uint8_t* arg, hipStream_t st,
                               int out_h16) {
-  if (s.C % 4 || s.h16) return hipErrorInvalidValue;
+  if (s.C % 4) return hipErrorInvalidValue;
   const long long work = (long long)n * (h / 2) * (w / 2) * (s.C / 4);
-  if (out_h16)
-    hipLaunchKernelGGL(k_maxpool_fwd<1>, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, st, s, n, h, w, y, arg);
-  else
-    hipLaunchKernelGGL(k_maxpool_fwd<0>, dim3(grid_cap(work, 256, 8192)), dim3(256), 0, st, s, n, h, w, y, arg);
+  const dim3 grid(grid_cap(work, 256, 8192));
+  switch (out_h16 * 2 + (s.h16 ? 1 : 0)) {
+    case 0: hipLaunchKernelGGL((k_maxpool_fwd<0, 0>), grid, dim3(256), 0, st, s, n, h, w, y, arg); break;
+    case 1: hipLaunchKernelGGL((k_maxpool_fwd<0, 1>), grid, dim3(256), 0, st, s, n, h, w, y, arg); break;
+    case 2: hipLaunchKernelGGL((k_maxpool_fwd<1, 0>), grid, dim3(256), 0, st, s, n, h, w, y, arg); break;
+    default: hipLaunchKernelGGL((k_maxpool_fwd<1, 1>), grid, dim3(256), 0, st, s, n, h, w, y, arg); break;
+  }
   return hipGetLastError();
 }
 
 // Maxpool backward fused with the skip-gradient add (the encoder output feeds
 // both the pool and the center-cropped concat, models/unet_model.py:107,130-142),
 // the ReLU mask and the BN-backward statistics of that layer.
+template <int Y16>  // y stored bf16
 __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restrict__ dpool,
                                                            const uint8_t* __restrict__ arg,
                                                            const float* __restrict__ dskip, int soy, int sox,
@@ -488,7 +510,8 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
     }
     const size_t oi = (size_t)p * C + c;
     if (scale) {
-      const float4 yv = ld4(yr + oi);
+      const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
+                            : ld4(yr + oi);
       d.x = (fmaf(yv.x, sc.x, sf.x) > 0.f) ? d.x : 0.f;
       d.y = (fmaf(yv.y, sc.y, sf.y) > 0.f) ? d.y : 0.f;
       d.z = (fmaf(yv.z, sc.z, sf.z) > 0.f) ? d.z : 0.f;
@@ -507,12 +530,17 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
 hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, const float* dskip, int soy, int sox,
                                     int sh, int sw, const float* y, const float* scale, const float* shift,
                                     const float* mean, const float* invstd, int n, int h, int w, int c, float* dz,
-                                    double* bstats, hipStream_t s) {
+                                    double* bstats, hipStream_t s, int y_h16) {
   if (c % 4 || (256 % (c / 4)) != 0) return hipErrorInvalidValue;
   const long long pixels = (long long)n * h * w;
   const int ppb = 256 / (c / 4);
-  hipLaunchKernelGGL(k_maxpool_bwd_fused, dim3(grid_cap(pixels, ppb * 4, 4096)), dim3(256), 0, s, dpool, arg, dskip,
-                     soy, sox, sh, sw, y, scale, shift, mean, invstd, n, h, w, c, dz, bstats);
+  const dim3 grid(grid_cap(pixels, ppb * 4, 4096));
+  if (y_h16)
+    hipLaunchKernelGGL(k_maxpool_bwd_fused<1>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
+                       shift, mean, invstd, n, h, w, c, dz, bstats);
+  else
+    hipLaunchKernelGGL(k_maxpool_bwd_fused<0>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
+                       shift, mean, invstd, n, h, w, c, dz, bstats);
   return hipGetLastError();
 }
 
@@ -536,7 +564,9 @@ __global__ __launch_bounds__(256) void k_head_fwd(Src s, int n, int h, int w, co
     const long long t = p / w;
     const int yy = (int)(t % h);
     const int nn = (int)(t / h);
-    float4 v = ld4(s.ptr + ((size_t)(nn * s.H + yy + s.oy) * s.W + xx + s.ox) * 64 + c);
+    const size_t si = ((size_t)(nn * s.H + yy + s.oy) * s.W + xx + s.ox) * 64 + c;
+    float4 v = s.h16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + si))
+                     : ld4(s.ptr + si);
     if (s.scale) {
       v.x = fmaxf(fmaf(v.x, sc.x, sf.x), 0.f);
       v.y = fmaxf(fmaf(v.y, sc.y, sf.y), 0.f);
@@ -586,7 +616,8 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
     const int nn = (int)(p / hw);
     const long long r = p - nn * hw;
     const size_t ii = ((size_t)(nn * s.H + (int)(r / w) + s.oy) * s.W + (int)(r % w) + s.ox) * 64 + c;
-    const float4 yv = ld4(s.ptr + ii);
+    const float4 yv = s.h16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + ii))
+                            : ld4(s.ptr + ii);
     float g[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) g[k] = dl[((size_t)nn * K + k) * hw + r];

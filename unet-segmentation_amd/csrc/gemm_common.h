@@ -42,6 +42,12 @@ __device__ __forceinline__ uint4 bf16pack8(float4 a, float4 b) {
   return make_uint4(bf16pack(a.x, a.y), bf16pack(a.z, a.w), bf16pack(b.x, b.y), bf16pack(b.z, b.w));
 }
 __device__ __forceinline__ uint16_t bf16_of(float v) { return (uint16_t)(bf16pack(v, 0.f) & 0xffffu); }
+// v rounded to the nearest bf16, as fp32
+__device__ __forceinline__ float round_bf(float v) { return __uint_as_float((unsigned)bf16_of(v) << 16); }
+// element idx of an fp32 or bf16 tensor
+__device__ __forceinline__ float ld_elem(const float* p, size_t idx, int h16) {
+  return h16 ? __uint_as_float((unsigned)reinterpret_cast<const uint16_t*>(p)[idx] << 16) : p[idx];
+}
 // 4 bf16 (uint2) -> 4 fp32 (exact)
 __device__ __forceinline__ float4 bf16x4_to_f4(uint2 u) {
   return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
@@ -158,6 +164,9 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
         int m;
         if (!rows.map(row, m)) continue;
         float v = acc[i][j][r] + bias;
+        // a bf16-stored conv output: its BatchNorm statistics are those of the
+        // rounded values the consumers will normalise
+        if (e.stats && d.h16) v = round_bf(v);
         size_t idx;
         if (linear) {
           idx = (size_t)m * d.C + dcol;
@@ -172,7 +181,7 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
           idx = ((size_t)(n * d.H + y + d.oy) * d.W + x + d.ox) * d.C + dcol;
         }
         if (bwd_mask) {
-          const float yv = e.yref[idx];
+          const float yv = ld_elem(e.yref, idx, e.yref_h16);
           v = (fmaf(yv, bsc, bsh) > 0.f) ? v : 0.f;
           s1[j] += v;
           s2[j] += v * ((yv - bmu) * bis);

@@ -494,8 +494,14 @@ __global__ __launch_bounds__(256) void k_splitk_epi(const IgemmArgs args) {
       }
     }
     float vv[4] = {v.x, v.y, v.z, v.w};
+    if (e.stats && d.h16) {  // bf16-stored conv output: statistics of the rounded values
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vv[q] = round_bf(vv[q]);
+    }
     if (bwd_mask) {
-      const float4 y4 = ld4(e.yref + idx);
+      const float4 y4 = e.yref_h16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(
+                                         reinterpret_cast<const uint16_t*>(e.yref) + idx))
+                                   : ld4(e.yref + idx);
       const float yv[4] = {y4.x, y4.y, y4.z, y4.w};
 #pragma unroll
       for (int q = 0; q < 4; ++q) {

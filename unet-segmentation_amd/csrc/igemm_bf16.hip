@@ -40,6 +40,24 @@ __device__ __forceinline__ void bf_mfma_step(floatx16 (&acc)[TM][TN], const unsi
     for (int j = 0; j < TN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
 }
 
+// 8 staged channels of an A operand -> 8 bf16 for LDS.  fp32 storage: r0, r1
+// hold the values; bf16 storage: r0 holds the raw 16 bytes (copied as is, or
+// widened, BN+ReLU-transformed and re-rounded when the source has a transform).
+__device__ __forceinline__ uint4 stage8(float4 r0, float4 r1, bool h16, bool tf, float4 sc0, float4 sc1, float4 sh0,
+                                       float4 sh1) {
+  if (h16) {
+    const uint4 u = __builtin_bit_cast(uint4, r0);
+    if (!tf) return u;
+    r0 = bf16x4_to_f4(make_uint2(u.x, u.y));
+    r1 = bf16x4_to_f4(make_uint2(u.z, u.w));
+  }
+  if (tf) {
+    r0 = affine_relu4(r0, sc0, sh0);
+    r1 = affine_relu4(r1, sc1, sh1);
+  }
+  return bf16pack8(r0, r1);
+}
+
 constexpr int igemm_bf_minw(int BM, int BN, int WM, int WN) {
   int blocks = 163840 / (2 * (BM + BN) * kBfLdr * 2);
   if (blocks > 8) blocks = 8;
@@ -147,20 +165,9 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
     unsigned short* As = lds + buf * STAGE;
     unsigned short* Bs = As + BM * LDR;
 #pragma unroll
-    for (int q = 0; q < AV; ++q) {
-      uint4 o;
-      if (h16) {
-        o = __builtin_bit_cast(uint4, ra[q][0]);
-      } else {
-        float4 v0 = ra[q][0], v1 = ra[q][1];
-        if (tf) {
-          v0 = affine_relu4(v0, sc0, sh0);
-          v1 = affine_relu4(v1, sc1, sh1);
-        }
-        o = bf16pack8(v0, v1);
-      }
-      *reinterpret_cast<uint4*>(As + (row0 + RPP * q) * LDR + chunk * 8) = o;
-    }
+    for (int q = 0; q < AV; ++q)
+      *reinterpret_cast<uint4*>(As + (row0 + RPP * q) * LDR + chunk * 8) =
+          stage8(ra[q][0], ra[q][1], h16, tf, sc0, sc1, sh0, sh1);
 #pragma unroll
     for (int q = 0; q < BV; ++q) *reinterpret_cast<uint4*>(Bs + (row0 + RPP * q) * LDR + chunk * 8) = rb[q];
   };
@@ -322,20 +329,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
       const int u = tid + k * NT;
-      if (u < UA) {
-        uint4 o;
-        if (h16) {
-          o = __builtin_bit_cast(uint4, ra[k][0]);
-        } else {
-          float4 v0 = ra[k][0], v1 = ra[k][1];
-          if (tf) {
-            v0 = affine_relu4(v0, sc0, sh0);
-            v1 = affine_relu4(v1, sc1, sh1);
-          }
-          o = bf16pack8(v0, v1);
-        }
-        *reinterpret_cast<uint4*>(As + (u >> 2) * LDR + (u & 3) * 8) = o;
-      }
+      if (u < UA)
+        *reinterpret_cast<uint4*>(As + (u >> 2) * LDR + (u & 3) * 8) =
+            stage8(ra[k][0], ra[k][1], h16, tf, sc0, sc1, sh0, sh1);
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
@@ -716,20 +712,8 @@ __global__ __launch_bounds__(512, 2) void k_conv3p_bf(const IgemmArgs args) {
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
       const int u = tid + k * NT;
-      if (u < UA) {
-        uint4 o;
-        if (h16) {
-          o = __builtin_bit_cast(uint4, ra[k][0]);
-        } else {
-          float4 v0 = ra[k][0], v1 = ra[k][1];
-          if (tf) {
-            v0 = affine_relu4(v0, sc0, sh0);
-            v1 = affine_relu4(v1, sc1, sh1);
-          }
-          o = bf16pack8(v0, v1);
-        }
-        *reinterpret_cast<uint4*>(st + c3p_off(u >> 2, u & 3)) = o;
-      }
+      if (u < UA)
+        *reinterpret_cast<uint4*>(st + c3p_off(u >> 2, u & 3)) = stage8(ra[k][0], ra[k][1], h16, tf, sc0, sc1, sh0, sh1);
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k)
@@ -920,18 +904,15 @@ __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
       const int u = tid + k * NT;
       if (u < UB) {
         const int hp = u >> 3, ch = u & 7;
-        uint4 o;
-        if (x16) {
-          o = __builtin_bit_cast(uint4, rx[k][0]);
-        } else {
-          float4 v0 = rx[k][0], v1 = rx[k][1];
-          if (xtf) {
-            v0 = affine_relu4(v0, ld4(ssc + ch * 8), ld4(ssc + BC + ch * 8));
-            v1 = affine_relu4(v1, ld4(ssc + ch * 8 + 4), ld4(ssc + BC + ch * 8 + 4));
-          }
-          o = bf16pack8(v0, v1);
+        float4 sc0 = make_float4(1.f, 1.f, 1.f, 1.f), sc1 = sc0, sh0 = make_float4(0.f, 0.f, 0.f, 0.f), sh1 = sh0;
+        if (xtf) {
+          sc0 = ld4(ssc + ch * 8);
+          sc1 = ld4(ssc + ch * 8 + 4);
+          sh0 = ld4(ssc + BC + ch * 8);
+          sh1 = ld4(ssc + BC + ch * 8 + 4);
         }
-        *reinterpret_cast<uint4*>(Bx + hp * ROWB + wg3_swz(hp, ch) * 16) = o;
+        *reinterpret_cast<uint4*>(Bx + hp * ROWB + wg3_swz(hp, ch) * 16) =
+            stage8(rx[k][0], rx[k][1], x16, xtf, sc0, sc1, sh0, sh1);
       }
     }
   };

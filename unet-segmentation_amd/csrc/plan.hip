@@ -351,6 +351,7 @@ Src src_of(const Ctx& c, const Conv& L, bool transform) {
   s.H = L.ho;
   s.W = L.wo;
   s.C = L.co;
+  s.h16 = c.p->prec == UNET_PREC_BF16;  // raw conv outputs of a bf16 plan are stored bf16
   if (transform) {
     s.scale = c.f(L.scale);
     s.shift = c.f(L.shift);
@@ -447,7 +448,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
     Timer t(p, s, UNET_KC_STAGE1, conv_flops(L, n),
             4.0 * n * ((double)p->cin * p->h * p->w + (double)L.ho * L.wo * L.co));
     CK(launch_conv_first_fwd(x, n, p->cin, p->h, p->w, P<float>(prm, L.pw), P<float>(prm, L.pw + 1), L.co,
-                             c.f(L.y), train ? c.d(L.stats) : nullptr, s));
+                             c.f(L.y), train ? c.d(L.stats) : nullptr, s, p->prec == UNET_PREC_BF16));
   }
   if (int r = finalize(0)) return r;
   for (int l = 1; l < 18; ++l) {
@@ -479,7 +480,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
     a.N = L.co;
     a.K = 9 * L.ci;
     a.e.bias = P<float>(prm, L.pw + 1);
-    a.e.d[0] = Dst{c.f(L.y), L.ho, L.wo, L.co, 0, 0};
+    a.e.d[0] = Dst{c.f(L.y), L.ho, L.wo, L.co, 0, 0, p->prec == UNET_PREC_BF16};
     a.e.stats = train ? c.d(L.stats) : nullptr;
     {
       Timer t(p, s, UNET_KC_CONV_FWD, conv_flops(L, n), 0);
@@ -554,7 +555,8 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * ((double)(L.ho + 4) * (L.wo + 4) + 2.0 * L.ho * L.wo) * L.co);
       // bf16 plans store dY(l > 0) in bf16: it only feeds bf16 GEMMs (inc.c0's
       // fp32 direct weight-gradient kernel reads dY(0))
-      CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), n, L.ho, L.wo, L.co, c.f(L.dyp), 2, s, dy16));
+      CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), n, L.ho, L.wo, L.co, c.f(L.dyp), 2, s, dy16,
+                          p->prec == UNET_PREC_BF16));
     }
     if (conc) {
       CK(hipEventRecord(p->ev_dy[l], s));
@@ -609,6 +611,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       Conv& Q = p->L[l - 1];
       a.e.d[0] = Dst{c.f(Q.dz), Q.ho, Q.wo, Q.co, 0, 0};
       a.e.yref = c.f(Q.y);
+      a.e.yref_h16 = p->prec == UNET_PREC_BF16;
       a.e.bn_scale = c.f(Q.scale);
       a.e.bn_shift = c.f(Q.shift);
       a.e.bn_mean = c.f(Q.mean);
@@ -629,7 +632,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * (double)Q.ho * Q.wo * Q.co * 2.6);
       CK(launch_maxpool_bwd_fused(c.f(pl.dp), c.u8(pl.arg), c.f(sk.d), sk.oy, sk.ox, sk.th, sk.tw, c.f(Q.y),
                                   c.f(Q.scale), c.f(Q.shift), c.f(Q.mean), c.f(Q.invstd), n, Q.ho, Q.wo, Q.co,
-                                  c.f(Q.dz), c.d(Q.bstats), s));
+                                  c.f(Q.dz), c.d(Q.bstats), s, p->prec == UNET_PREC_BF16));
     } else {  // first conv of up block: split into skip grad and upsampled grad
       const int k = (l - 10) / 2;
       ConvT& T = p->T[k];
@@ -701,6 +704,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       b.K = 4 * T.co;
       b.e.d[0] = Dst{c.f(Q.dz), Q.ho, Q.wo, Q.co, 0, 0};
       b.e.yref = c.f(Q.y);
+      b.e.yref_h16 = p->prec == UNET_PREC_BF16;
       b.e.bn_scale = c.f(Q.scale);
       b.e.bn_shift = c.f(Q.shift);
       b.e.bn_mean = c.f(Q.mean);

@@ -59,6 +59,7 @@ struct Epilogue {
   // backward: mask the d[0] values with ReLU'(yref*scale+shift) and collect
   // bstats[g][col][2] = (sum dz', sum dz' * xhat), xhat = (yref-mean)*invstd
   const float* yref = nullptr;
+  int yref_h16 = 0;  // yref stored bf16 (raw conv outputs of a bf16 plan)
   const float* bn_scale = nullptr;
   const float* bn_shift = nullptr;
   const float* bn_mean = nullptr;
@@ -128,7 +129,7 @@ hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s);
 // inc.c0: Ci in {1,2,3,4} direct conv from an NCHW input; y NHWC (Co = 64 multiple).
 hipError_t launch_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w,
                                  const float* wt_oihw, const float* bias, int co, float* y,
-                                 double* stats, hipStream_t s);
+                                 double* stats, hipStream_t s, int out_h16 = 0);
 // Written per workgroup into `slabs` (conv_first_wgrad_ws_bytes) then reduced
 // into dw_oihw (overwritten, not accumulated).
 constexpr int kFirstWgradSlabs = 2048;
@@ -152,7 +153,8 @@ hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const 
                                float* dbeta, float* dbias_conv, float* coef, hipStream_t s);
 // dYpad interior = coef0*dz + coef1*y + coef2; border (pad each side) = 0.
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h,
-                            int w, int c, float* dypad, int pad, hipStream_t s, int out_h16 = 0);
+                            int w, int c, float* dypad, int pad, hipStream_t s, int out_h16 = 0,
+                            int y_h16 = 0);
 // MaxPool2d(2) fwd with BN+ReLU transform on load (src grid H x W, pooled H/2 x W/2).
 hipError_t launch_maxpool_fwd(const Src& src, int n, int h, int w, float* y, uint8_t* arg,
                               hipStream_t s, int out_h16 = 0);
@@ -162,7 +164,7 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
                                     int skip_oy, int skip_ox, int skip_h, int skip_w,
                                     const float* y, const float* scale, const float* shift,
                                     const float* mean, const float* invstd, int n, int h, int w,
-                                    int c, float* dz, double* bstats, hipStream_t s);
+                                    int c, float* dz, double* bstats, hipStream_t s, int y_h16 = 0);
 // 1x1 head (OutConv, models/unet_model.py:56-63) forward: logits NCHW.
 hipError_t launch_head_fwd(const Src& src, int n, int h, int w, int c, const float* wt,
                            const float* bias, int k, float* logits, hipStream_t s);
