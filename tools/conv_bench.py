@@ -1,0 +1,93 @@
+"""A/B timing of the bf16 3x3-conv GEMM variants through the per-op C-ABI.
+
+    python tools/conv_bench.py [--reps 20]
+
+For U-Net layer shapes (batch 8, 512x512 input) it times unet_conv3x3_fwd /
+unet_conv3x3_dgrad with op_precision=bf16 and each forced igemm variant
+(-1 = built-in choice, 21-26 row gather, 31-36 halo, 41-44 persistent halo),
+interleaved in one process (rule: perf deltas from interleaved rounds), and
+prints the median microseconds and TFLOP/s per variant.
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "unet-segmentation_amd"))
+from unet_amd import _lib  # noqa: E402
+
+# (name, n, h, w, ci, co): conv input grid h x w (output h-2 x w-2)
+SHAPES = [
+    ("inc.c1", 8, 510, 510, 64, 64),
+    ("down1.c1", 8, 252, 252, 128, 128),
+    ("down2.c1", 8, 123, 123, 256, 256),
+    ("down3.c1", 8, 58, 58, 512, 512),
+    ("down4.c1", 8, 26, 26, 1024, 1024),
+    ("up1.c0", 8, 48, 48, 1024, 512),
+    ("up4.c1", 8, 326, 326, 64, 64),
+]
+VARIANTS = [-1, 21, 22, 23, 24, 31, 32, 33, 34, 35, 36, 41, 42, 43, 44]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--dgrad", action="store_true")
+    args = ap.parse_args()
+    lib = _lib.load()
+    lib.unet_set_tuning(b"op_precision", 1)
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    for name, n, h, w, ci, co in SHAPES:
+        g = torch.Generator(device="cuda").manual_seed(0)
+        x = torch.randn((n, h, w, ci), device="cuda", generator=g)
+        wt = torch.randn((co, ci, 3, 3), device="cuda", generator=g) / (3 * ci ** 0.5)
+        b = torch.randn(co, device="cuda", generator=g)
+        sc = torch.rand(ci, device="cuda", generator=g) + 0.5
+        sh = torch.randn(ci, device="cuda", generator=g) * 0.1
+        y = torch.empty((n, h - 2, w - 2, co), device="cuda")
+        dy = torch.randn((n, h - 2, w - 2, co), device="cuda", generator=g)
+        dx = torch.empty((n, h, w, ci), device="cuda")
+        ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
+        flops = 2.0 * n * (h - 2) * (w - 2) * ci * co * 9
+
+        def run():
+            if args.dgrad:
+                rc = lib.unet_conv3x3_dgrad(dy.data_ptr(), n, h, w, ci, wt.data_ptr(), co, dx.data_ptr(),
+                                            ws.data_ptr(), st)
+            else:
+                rc = lib.unet_conv3x3_fwd(x.data_ptr(), n, h, w, ci, wt.data_ptr(), b.data_ptr(), co, sc.data_ptr(),
+                                          sh.data_ptr(), y.data_ptr(), ws.data_ptr(), st)
+            return rc
+
+        times = {v: [] for v in VARIANTS}
+        ok = {}
+        for v in VARIANTS:
+            lib.unet_set_tuning(b"igemm_variant", v)
+            ok[v] = run() == 0
+        torch.cuda.synchronize()
+        for _ in range(args.reps):
+            for v in VARIANTS:
+                if not ok[v]:
+                    continue
+                lib.unet_set_tuning(b"igemm_variant", v)
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                run()
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) * 1e3)
+        line = f"{name:9s} {'dgrad' if args.dgrad else 'fwd':5s}"
+        for v in VARIANTS:
+            if ok[v]:
+                t = sorted(times[v])[len(times[v]) // 2]
+                line += f" | {v}:{t:7.1f}us {flops / t / 1e6:6.1f}TF"
+        print(line, flush=True)
+    lib.unet_set_tuning(b"igemm_variant", -1)
+    lib.unet_set_tuning(b"op_precision", 0)
+
+
+if __name__ == "__main__":
+    main()

@@ -55,16 +55,16 @@ def main():
     h = int(sys.argv[3]) if len(sys.argv) > 3 else 512
     rows = sorted(csv.DictReader(open(path)), key=lambda r: int(r["Start_Timestamp"]))
     starts = [i for i, r in enumerate(rows) if "conv_first_fwd" in r["Kernel_Name"]]
-    s, e = starts[-2], starts[-1]
-    step = rows[s:e]
-    conv = [r for r in step if "k_igemm" in r["Kernel_Name"] or "k_wgrad" in r["Kernel_Name"]]
+    # the last step of bench.py is its serial timing step (no side stream)
+    step = rows[starts[-1]:]
+    conv = [r for r in step if any(k in r["Kernel_Name"] for k in ("k_igemm", "k_wgrad", "k_conv3"))]
     seq = geometry(n, h)
     assert len(conv) == len(seq), (len(conv), len(seq))
     tot_t = tot_f = 0.0
     print(f"{'layer':24s} {'kernel':26s} {'blocks':>7s} {'us':>8s} {'TF/s':>7s}")
     for (name, fl), r in zip(seq, conv):
         us = (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-        gx = int(r["Grid_Size_X"]) // 256 * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
+        gx = int(r["Grid_Size_X"]) // int(r.get("Workgroup_Size_X", 256)) * int(r["Grid_Size_Y"]) * int(r["Grid_Size_Z"])
         kn = r["Kernel_Name"].split("(")[0].replace("void unet::", "")
         tot_t += us
         tot_f += fl

@@ -53,6 +53,21 @@ __device__ __forceinline__ float4 bf16x4_to_f4(uint2 u) {
   return make_float4(__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
                      __uint_as_float(u.y & 0xffff0000u));
 }
+// g.s[second], picked field by field: a reference into the kernel-argument
+// array selected at run time makes the compiler copy the array to scratch
+__device__ __forceinline__ Src pick_src(const Gather& g, bool second) {
+  Src r;
+  r.ptr = second ? g.s[1].ptr : g.s[0].ptr;
+  r.H = second ? g.s[1].H : g.s[0].H;
+  r.W = second ? g.s[1].W : g.s[0].W;
+  r.C = second ? g.s[1].C : g.s[0].C;
+  r.oy = second ? g.s[1].oy : g.s[0].oy;
+  r.ox = second ? g.s[1].ox : g.s[0].ox;
+  r.scale = second ? g.s[1].scale : g.s[0].scale;
+  r.shift = second ? g.s[1].shift : g.s[0].shift;
+  r.h16 = second ? g.s[1].h16 : g.s[0].h16;
+  return r;
+}
 // store one element of a Dst (fp32 or bf16 storage)
 __device__ __forceinline__ void dst_store(const Dst& d, size_t idx, float v) {
   if (d.h16)

@@ -111,7 +111,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   int nissued = 0;
   auto issue = [&](Stage& st, int k0) {
     const bool second = it_c >= g.c_split;
-    const Src& s = second ? g.s[1] : g.s[0];
+    const Src s = pick_src(g, second);
     const int c = (second ? it_c - g.c_split : it_c) + col4 * 4;
     const int toff = it_ty * s.W + it_tx;
     if (!(ABL & 1) && (!(ABL & 512) || nissued++ < 2)) {
@@ -328,7 +328,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_g_minw(BM, BN, WM, WN)) void k_
   if (any_tf) {
     for (int c = tid; c < Cg; c += NT) {
       const bool sec = c >= g.c_split;
-      const Src& sr = sec ? g.s[1] : g.s[0];
+      const Src sr = pick_src(g, sec);
       const int cl = sec ? c - g.c_split : c;
       ssc[c] = sr.scale ? sr.scale[cl] : 1.f;
       ssc[Cg + c] = sr.scale ? sr.shift[cl] : 0.f;
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_g_minw(BM, BN, WM, WN)) void k_
 
   auto issue = [&](int slot, int k0) {
     const bool second = it_c >= g.c_split;
-    const Src& s = second ? g.s[1] : g.s[0];
+    const Src s = pick_src(g, second);
     const int c = second ? it_c - g.c_split : it_c;
     const int toff = it_ty * s.W + it_tx;
     float* As = dl + slot * STAGE;

@@ -20,6 +20,9 @@
 namespace unet {
 
 typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
+// 16-B staging register (an array of the HIP uint4 struct is not promoted to
+// registers; one of ext_vector_type is)
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBfBK = 32;   // k per LDS stage (two 16-k MFMA steps)
 constexpr int kBfLdr = 40;  // bf16 elements per LDS row (32 + 8 pad)
@@ -126,13 +129,13 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
     it_tx = tap - it_ty * g.taps_w;
   }
 
-  float4 ra[AV][2];
-  uint4 rb[BV];
+  float4 ra0[AV], ra1[AV];  // two 1-D arrays: a [N][2] array of vectors is not promoted to registers
+  u32x4 rb[BV];
   float4 sc0, sc1, sh0, sh1;
   bool tf = false, h16 = false;
   auto issue = [&](int k0) {
     const bool second = it_c >= g.c_split;
-    const Src& s = second ? g.s[1] : g.s[0];
+    const Src s = pick_src(g, second);
     const int c = (second ? it_c - g.c_split : it_c) + chunk * 8;
     const int toff = it_ty * s.W + it_tx;
     h16 = s.h16 != 0;
@@ -140,14 +143,14 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
     for (int q = 0; q < AV; ++q) {
       const size_t e = (size_t)((second ? rb1[q] : rb0[q]) + toff) * s.C + c;
       if (h16) {  // stored bf16: 8 channels = 16 B, staged as is
-        ra[q][0] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(s.ptr) + e));
+        ra0[q] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(s.ptr) + e));
       } else {
-        ra[q][0] = ld4(s.ptr + e);
-        ra[q][1] = ld4(s.ptr + e + 4);
+        ra0[q] = ld4(s.ptr + e);
+        ra1[q] = ld4(s.ptr + e + 4);
       }
     }
 #pragma unroll
-    for (int q = 0; q < BV; ++q) rb[q] = *reinterpret_cast<const uint4*>(bptr[q] + k0);
+    for (int q = 0; q < BV; ++q) rb[q] = *reinterpret_cast<const u32x4*>(bptr[q] + k0);
     tf = s.scale != nullptr;
     if (tf) {
       sc0 = ld4(s.scale + c);
@@ -167,9 +170,9 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
 #pragma unroll
     for (int q = 0; q < AV; ++q)
       *reinterpret_cast<uint4*>(As + (row0 + RPP * q) * LDR + chunk * 8) =
-          stage8(ra[q][0], ra[q][1], h16, tf, sc0, sc1, sh0, sh1);
+          stage8(ra0[q], ra1[q], h16, tf, sc0, sc1, sh0, sh1);
 #pragma unroll
-    for (int q = 0; q < BV; ++q) *reinterpret_cast<uint4*>(Bs + (row0 + RPP * q) * LDR + chunk * 8) = rb[q];
+    for (int q = 0; q < BV; ++q) *reinterpret_cast<u32x4*>(Bs + (row0 + RPP * q) * LDR + chunk * 8) = rb[q];
   };
 
   floatx16 acc[TM][TN];
@@ -258,7 +261,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
   if (any_tf) {
     for (int c = tid; c < Cg; c += NT) {
       const bool sec = c >= g.c_split;
-      const Src& sr = sec ? g.s[1] : g.s[0];
+      const Src sr = pick_src(g, sec);
       const int cl = sec ? c - g.c_split : c;
       ssc[c] = sr.scale ? sr.scale[cl] : 1.f;
       ssc[Cg + c] = sr.scale ? sr.shift[cl] : 0.f;
@@ -267,7 +270,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
 
   // staging units: A = (halo pixel, 8-channel piece), B = (tap, row, 8-k piece)
   int pi0[NA], pi1[NA];
-  const uint16_t* bsrc[NB];
+  int bsrc[NB];  // element offsets into args.bh (32-bit: one VGPR, scalar base)
 #pragma unroll
   for (int k = 0; k < NA; ++k) {
     const int u = min(tid + k * NT, UA - 1);
@@ -281,7 +284,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
   for (int k = 0; k < NB; ++k) {
     const int u = min(tid + k * NT, UB - 1);
     const int r = (u >> 2) % BN, tap = (u >> 2) / BN;
-    bsrc[k] = args.bh + (size_t)(n0 + r) * K + tap * Cg + (u & 3) * 8;
+    bsrc[k] = (n0 + r) * K + tap * Cg + (u & 3) * 8;
   }
 
   const int nk_all = Cg / 32;
@@ -292,32 +295,32 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     kc1 = min(nk_all, kc0 + per);
   }
 
-  float4 ra[NA][2];
-  uint4 rb[NB];
+  float4 ra0[NA], ra1[NA];  // two 1-D arrays: a [N][2] array of vectors is not promoted to registers
+  u32x4 rb[NB];
   auto issue = [&](int kc) {
     const int c0 = kc * 32;
     const bool second = c0 >= g.c_split;
-    const Src& s = second ? g.s[1] : g.s[0];
+    const Src s = pick_src(g, second);
     const int cl = (second ? c0 - g.c_split : c0) + (tid & 3) * 8;
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
       if (tid + k * NT < UA) {
         const size_t e = (size_t)(second ? pi1[k] : pi0[k]) * s.C + cl;
         if (s.h16) {  // stored bf16: staged as is
-          ra[k][0] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(s.ptr) + e));
+          ra0[k] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(s.ptr) + e));
         } else {
-          ra[k][0] = ld4(s.ptr + e);
-          ra[k][1] = ld4(s.ptr + e + 4);
+          ra0[k] = ld4(s.ptr + e);
+          ra1[k] = ld4(s.ptr + e + 4);
         }
       }
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k)
-      if (tid + k * NT < UB) rb[k] = *reinterpret_cast<const uint4*>(bsrc[k] + c0);
+      if (tid + k * NT < UB) rb[k] = *reinterpret_cast<const u32x4*>(args.bh + bsrc[k] + c0);
   };
   auto commit = [&](int kc) {
     const int c = kc * 32 + (tid & 3) * 8;
-    const Src& sc_src = c >= g.c_split ? g.s[1] : g.s[0];
+    const Src sc_src = pick_src(g, c >= g.c_split);
     const bool tf = sc_src.scale != nullptr, h16 = sc_src.h16 != 0;
     float4 sc0, sc1, sh0, sh1;
     if (tf) {
@@ -331,12 +334,12 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
       const int u = tid + k * NT;
       if (u < UA)
         *reinterpret_cast<uint4*>(As + (u >> 2) * LDR + (u & 3) * 8) =
-            stage8(ra[k][0], ra[k][1], h16, tf, sc0, sc1, sh0, sh1);
+            stage8(ra0[k], ra1[k], h16, tf, sc0, sc1, sh0, sh1);
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       const int u = tid + k * NT;
-      if (u < UB) *reinterpret_cast<uint4*>(Bs + (u >> 2) * LDR + (u & 3) * 8) = rb[k];
+      if (u < UB) *reinterpret_cast<u32x4*>(Bs + (u >> 2) * LDR + (u & 3) * 8) = rb[k];
     }
   };
 
@@ -635,7 +638,7 @@ __global__ __launch_bounds__(512, 2) void k_conv3p_bf(const IgemmArgs args) {
   if (any_tf) {
     for (int c = tid; c < Cg; c += NT) {
       const bool sec = c >= g.c_split;
-      const Src& sr = sec ? g.s[1] : g.s[0];
+      const Src sr = pick_src(g, sec);
       const int cl = sec ? c - g.c_split : c;
       ssc[c] = sr.scale ? sr.scale[cl] : 1.f;
       ssc[Cg + c] = sr.scale ? sr.shift[cl] : 0.f;
@@ -655,18 +658,18 @@ __global__ __launch_bounds__(512, 2) void k_conv3p_bf(const IgemmArgs args) {
   const int S = nk > 0 ? my_tiles * nk : 0;
 
   // B staging units (tap, row, piece) are the same for every stage but the chunk
-  const uint16_t* bsrc[NB];
+  int bsrc[NB];  // element offsets into args.bh (32-bit: one VGPR, scalar base)
   int boff[NB];
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int u = min(tid + k * NT, UB - 1);
     const int r = (u >> 2) % BN, tap = (u >> 2) / BN;
-    bsrc[k] = args.bh + (size_t)(n0 + r) * K + tap * Cg + (u & 3) * 8;
+    bsrc[k] = (n0 + r) * K + tap * Cg + (u & 3) * 8;
     boff[k] = A_EL + c3p_off(u >> 2, u & 3);
   }
 
-  float4 ra[NA][2];
-  uint4 rb[NB];
+  float4 ra0[NA], ra1[NA];  // two 1-D arrays: a [N][2] array of vectors is not promoted to registers
+  u32x4 rb[NB];
   auto tile_of = [&](int s, int& n, int& y0, int& x0) {
     int t = (int)blockIdx.x + (s / nk) * (int)gridDim.x;
     x0 = (t % tiles_x) * TW;
@@ -679,7 +682,7 @@ __global__ __launch_bounds__(512, 2) void k_conv3p_bf(const IgemmArgs args) {
     tile_of(s, n, y0, x0);
     const int c0 = (kc0 + s % nk) * 32;
     const bool second = c0 >= g.c_split;
-    const Src& src = second ? g.s[1] : g.s[0];
+    const Src src = pick_src(g, second);
     const int cl = (second ? c0 - g.c_split : c0) + (tid & 3) * 8;
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
@@ -688,19 +691,19 @@ __global__ __launch_bounds__(512, 2) void k_conv3p_bf(const IgemmArgs args) {
       const int yy = min(y0 + ph / HW2, Hg + 1), xx = min(x0 + ph % HW2, Wg + 1);  // overhang: any in-range pixel
       const size_t e = (size_t)((n * src.H + yy + src.oy) * src.W + xx + src.ox) * src.C + cl;
       if (src.h16) {
-        ra[k][0] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(src.ptr) + e));
+        ra0[k] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(src.ptr) + e));
       } else {
-        ra[k][0] = ld4(src.ptr + e);
-        ra[k][1] = ld4(src.ptr + e + 4);
+        ra0[k] = ld4(src.ptr + e);
+        ra1[k] = ld4(src.ptr + e + 4);
       }
     }
 #pragma unroll
-    for (int k = 0; k < NB; ++k) rb[k] = *reinterpret_cast<const uint4*>(bsrc[k] + c0);
+    for (int k = 0; k < NB; ++k) rb[k] = *reinterpret_cast<const u32x4*>(args.bh + bsrc[k] + c0);
   };
   auto commit = [&](int s, int buf) {
     unsigned short* st = smem + buf * ST_EL;
     const int c = (kc0 + s % nk) * 32 + (tid & 3) * 8;
-    const Src& src = c >= g.c_split ? g.s[1] : g.s[0];
+    const Src src = pick_src(g, c >= g.c_split);
     const bool tf = src.scale != nullptr, h16 = src.h16 != 0;
     float4 sc0, sc1, sh0, sh1;
     if (tf) {
@@ -713,11 +716,11 @@ __global__ __launch_bounds__(512, 2) void k_conv3p_bf(const IgemmArgs args) {
     for (int k = 0; k < NA; ++k) {
       const int u = tid + k * NT;
       if (u < UA)
-        *reinterpret_cast<uint4*>(st + c3p_off(u >> 2, u & 3)) = stage8(ra[k][0], ra[k][1], h16, tf, sc0, sc1, sh0, sh1);
+        *reinterpret_cast<uint4*>(st + c3p_off(u >> 2, u & 3)) = stage8(ra0[k], ra1[k], h16, tf, sc0, sc1, sh0, sh1);
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k)
-      if (tid + k * NT < UB) *reinterpret_cast<uint4*>(st + boff[k]) = rb[k];
+      if (tid + k * NT < UB) *reinterpret_cast<u32x4*>(st + boff[k]) = rb[k];
   };
 
   floatx16 acc[TM][TN];
