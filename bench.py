@@ -32,6 +32,8 @@ METRIC = "training images/sec (512×512×1, batch=8) at 1/2/4/8 MI355X; IoU vs r
 FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md: f32 MFMA = f32 vector peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sparsity)
 HBM_PEAK_GBS = 8000.0
+GEMM_DESC = {"fp32": "fp32", "bf16": "bf16-operand/fp32-acc",
+             "bf16x3": "fp32-accurate bf16x3 split-operand (3 bf16 MFMA products, fp32 acc)"}
 
 
 def init_weights(m):
@@ -106,8 +108,9 @@ def main():
     ap.add_argument("--batch", type=int, default=8, help="images per GPU")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--channels", type=int, default=1, help="input channels (configs[4]: 3)")
-    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16"],
-                    help="GEMM operand precision (bf16 = bf16-in / fp32-acc MFMA)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "bf16x3"],
+                    help="GEMM arithmetic: fp32 MFMA; bf16 = bf16-in / fp32-acc MFMA; bf16x3 = fp32-accurate "
+                         "split operands (hi*hi + hi*lo + lo*hi on the bf16 MFMA)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
     ap.add_argument("--tuning-report", default=None, help="write the GEMM autotuner's choices to this file")
@@ -182,7 +185,9 @@ def main():
         conv_ms = sum(c[0] for c in conv)
         conv_fl = sum(c[1] for c in conv)
         achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-        peak = BF16_MFMA_PEAK_TFLOPS if args.dtype == "bf16" else FP32_MFMA_PEAK_TFLOPS
+        # bf16x3: fp32 GEMM flops at three bf16 MFMA products each
+        peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
+                "bf16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1)}[args.dtype]
         launches = sum(c[3] for c in conv)
         st = tim["stage1"]
         kernels = {k: {"ms": round(v[0], 3), "launches": v[3],
@@ -204,7 +209,7 @@ def main():
             "data": "synthetic: x~U[0,1) (N,1,512,512), Bernoulli(0.4) targets, 10+1/freq(class) weight maps; "
                     "kaiming fan_out init (scripts/train.py:54-61)",
             "config": {"workload": f"U-Net train step {args.size}x{args.size}x{args.channels}, batch {args.batch}/GPU, "
-                                   f"{'fp32' if args.dtype == 'fp32' else 'bf16-operand/fp32-acc'} GEMMs: "
+                                   f"{GEMM_DESC[args.dtype]} GEMMs: "
                                    "fwd + weighted CE + bwd + SGD(0.99)" + ((f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-reduce" if world > 1 else "")),
                        "global_batch": world * args.batch, "image": args.size,
                        "parallelism": f"dp{world}"},

@@ -60,11 +60,18 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes);
  *  UNET_PREC_BF16  both operands rounded to bf16 (RNE) when staged, fp32
  *                  accumulation (v_mfma_f32_32x32x16_bf16): the "bf16-in /
  *                  fp32-acc" of configs C3/C5, what torch.autocast(bfloat16)
- *                  asks of the reference's convolutions.
- * Everything else -- stored activations, BatchNorm statistics, the first conv
- * (Ci <= 4), the 1x1 head, the loss, gradients and the optimizer -- is fp32 in
- * both. */
-enum { UNET_PREC_FP32 = 0, UNET_PREC_BF16 = 1 };
+ *                  asks of the reference's convolutions;
+ *  UNET_PREC_BF16X3 fp32-accurate GEMMs on the bf16 matrix cores: each fp32
+ *                  operand is split v = hi + lo (hi = bf16(v), lo = bf16(v -
+ *                  hi), |v - hi - lo| <= 2^-16 |v|) and a product is taken as
+ *                  hi*hi' + hi*lo' + lo*hi' (three v_mfma_f32_32x32x16_bf16,
+ *                  fp32 accumulation; the dropped lo*lo' is <= 2^-16 of the
+ *                  product).  Storage as in UNET_PREC_FP32; tested against the
+ *                  fp64 oracle at the fp32 tolerances.
+ * Everything else -- the first conv (Ci <= 4), the 1x1 head, BatchNorm, the
+ * loss, gradients and the optimizer -- is fp32 in all three; UNET_PREC_BF16
+ * plans also store the GEMM-only tensors and the raw conv outputs in bf16. */
+enum { UNET_PREC_FP32 = 0, UNET_PREC_BF16 = 1, UNET_PREC_BF16X3 = 2 };
 unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int precision);
 int unet_plan_precision(const unet_plan* p);
 void unet_plan_destroy(unet_plan* p);
@@ -153,7 +160,7 @@ int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int 
  *  "force_split"   k > 1: every plan igemm runs split-K k (tests), 0 = off.
  *  "force_tile"    id > 0: every plan igemm whose shape admits tile id runs
  *                  it (tests; 1-4, 6-9 register-staged, 11-14 LDS-DMA, 21-26
- *                  bf16 operands -- only in a UNET_PREC_BF16 plan).
+ *                  bf16 operands -- only in UNET_PREC_BF16 / _BF16X3 plans).
  *  "op_precision"  UNET_PREC_* of the per-op GEMM entry points below
  *                  (unet_conv3x3_*, unet_convT2_*); default fp32. */
 int unet_set_tuning(const char* key, int value);

@@ -36,9 +36,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--dgrad", action="store_true")
+    ap.add_argument("--prec", type=int, default=1, help="1 = bf16 operands, 2 = bf16x3 split operands")
     args = ap.parse_args()
     lib = _lib.load()
-    lib.unet_set_tuning(b"op_precision", 1)
+    lib.unet_set_tuning(b"op_precision", args.prec)
+    variants = VARIANTS if args.prec == 1 else [-1, 21, 22, 23, 24, 25, 26, 31, 33, 35]
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for name, n, h, w, ci, co in SHAPES:
         g = torch.Generator(device="cuda").manual_seed(0)
@@ -62,14 +64,14 @@ def main():
                                           sh.data_ptr(), y.data_ptr(), ws.data_ptr(), st)
             return rc
 
-        times = {v: [] for v in VARIANTS}
+        times = {v: [] for v in variants}
         ok = {}
-        for v in VARIANTS:
+        for v in variants:
             lib.unet_set_tuning(b"igemm_variant", v)
             ok[v] = run() == 0
         torch.cuda.synchronize()
         for _ in range(args.reps):
-            for v in VARIANTS:
+            for v in variants:
                 if not ok[v]:
                     continue
                 lib.unet_set_tuning(b"igemm_variant", v)
@@ -80,7 +82,7 @@ def main():
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) * 1e3)
         line = f"{name:9s} {'dgrad' if args.dgrad else 'fwd':5s}"
-        for v in VARIANTS:
+        for v in variants:
             if ok[v]:
                 t = sorted(times[v])[len(times[v]) // 2]
                 line += f" | {v}:{t:7.1f}us {flops / t / 1e6:6.1f}TF"

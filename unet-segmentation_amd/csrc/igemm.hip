@@ -29,6 +29,9 @@ constexpr int igemm_minw(int BM, int BN, int WM, int WN, int BK) {
   int blocks = 163840 / lds;
   if (blocks > 8) blocks = 8;
   int w = blocks * WM * WN * 64 / 256;
+  // 8-wave tiles: at most 2 waves/SIMD (256 registers).  At 4 the 256x128 tile
+  // spilled 52 VGPRs to scratch inside the LDS-DMA pipeline and lost parity.
+  if (WM * WN >= 8 && w > 2) w = 2;
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
@@ -111,7 +114,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   int nissued = 0;
   auto issue = [&](Stage& st, int k0) {
     const bool second = it_c >= g.c_split;
-    const Src s = pick_src(g, second);
+    const Src& s = second ? g.s[1] : g.s[0];
     const int c = (second ? it_c - g.c_split : it_c) + col4 * 4;
     const int toff = it_ty * s.W + it_tx;
     if (!(ABL & 1) && (!(ABL & 512) || nissued++ < 2)) {
@@ -278,6 +281,9 @@ constexpr int igemm_g_minw(int BM, int BN, int WM, int WN) {
   int blocks = 163840 / (igemm_g_lds_floats(BM, BN) * 4 + 2048);
   if (blocks > 8) blocks = 8;
   int w = blocks * WM * WN * 64 / 256;
+  // 8-wave tiles: at most 2 waves/SIMD (256 registers).  At 4 the 256x128 tile
+  // spilled 52 VGPRs to scratch inside the LDS-DMA pipeline and lost parity.
+  if (WM * WN >= 8 && w > 2) w = 2;
   return w < 1 ? 1 : (w > 8 ? 8 : w);
 }
 
@@ -328,7 +334,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_g_minw(BM, BN, WM, WN)) void k_
   if (any_tf) {
     for (int c = tid; c < Cg; c += NT) {
       const bool sec = c >= g.c_split;
-      const Src sr = pick_src(g, sec);
+      const Src& sr = sec ? g.s[1] : g.s[0];
       const int cl = sec ? c - g.c_split : c;
       ssc[c] = sr.scale ? sr.scale[cl] : 1.f;
       ssc[Cg + c] = sr.scale ? sr.shift[cl] : 0.f;
@@ -356,7 +362,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_g_minw(BM, BN, WM, WN)) void k_
 
   auto issue = [&](int slot, int k0) {
     const bool second = it_c >= g.c_split;
-    const Src s = pick_src(g, second);
+    const Src& s = second ? g.s[1] : g.s[0];
     const int c = second ? it_c - g.c_split : it_c;
     const int toff = it_ty * s.W + it_tx;
     float* As = dl + slot * STAGE;
@@ -762,7 +768,8 @@ static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_hal
 // tile's precision (fp32 `b` for tiles 1-14, bf16 `bh` for 21-26).
 bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   const TileInfo t = tile_info(tile);
-  const bool prec_ok = is_bf16_tile(tile) ? a.bh != nullptr : a.b != nullptr;
+  const bool prec_ok = is_bf16_tile(tile) ? a.bh != nullptr && (a.bl == nullptr || bf16_tile_splits(tile))
+                                           : a.b != nullptr;
   if (is_halo_tile(tile))  // 3x3 stride-1 gathers only (conv fwd / dgrad), K = 9 x Cg
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;

@@ -61,8 +61,64 @@ __device__ __forceinline__ uint4 stage8(float4 r0, float4 r1, bool h16, bool tf,
   return bf16pack8(r0, r1);
 }
 
-constexpr int igemm_bf_minw(int BM, int BN, int WM, int WN) {
-  int blocks = 163840 / (2 * (BM + BN) * kBfLdr * 2);
+// Split operands (UNET_PREC_BF16X3): v = hi + lo + O(2^-16 |v|) with
+// hi = bf16(v), lo = bf16(v - hi); a product is taken as hi*hi' + hi*lo' + lo*hi'
+// (three bf16 MFMAs, fp32 accumulation).  lo halves of the pair (a, b) whose
+// packed hi halves are `hi`:
+__device__ __forceinline__ unsigned bf16pack_lo(float a, float b, unsigned hi) {
+  return bf16pack(a - __uint_as_float(hi << 16), b - __uint_as_float(hi & 0xffff0000u));
+}
+__device__ __forceinline__ uint4 bf16pack8_lo(float4 a, float4 b, uint4 hi) {
+  return make_uint4(bf16pack_lo(a.x, a.y, hi.x), bf16pack_lo(a.z, a.w, hi.y), bf16pack_lo(b.x, b.y, hi.z),
+                    bf16pack_lo(b.z, b.w, hi.w));
+}
+// stage8 with the lo half: returns hi, writes lo (0 for raw bf16 data)
+__device__ __forceinline__ uint4 stage8x(float4 r0, float4 r1, bool h16, bool tf, float4 sc0, float4 sc1, float4 sh0,
+                                        float4 sh1, uint4& lo) {
+  if (h16) {
+    const uint4 u = __builtin_bit_cast(uint4, r0);
+    lo = make_uint4(0u, 0u, 0u, 0u);
+    if (!tf) return u;
+    r0 = bf16x4_to_f4(make_uint2(u.x, u.y));
+    r1 = bf16x4_to_f4(make_uint2(u.z, u.w));
+  }
+  if (tf) {
+    r0 = affine_relu4(r0, sc0, sh0);
+    r1 = affine_relu4(r1, sc1, sh1);
+  }
+  const uint4 hi = bf16pack8(r0, r1);
+  lo = bf16pack8_lo(r0, r1, hi);
+  return hi;
+}
+
+// One 16-k step of split operands: hi/lo planes of A (As, Al) and B (Bs, Bl)
+template <int TM, int TN>
+__device__ __forceinline__ void bf_mfma_step_x3(floatx16 (&acc)[TM][TN], const unsigned short* As,
+                                                const unsigned short* Al, const unsigned short* Bs,
+                                                const unsigned short* Bl, int arow, int brow, int koff) {
+  bf16x8_t fa[TM], fal[TM], fb[TN], fbl[TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    fa[i] = *reinterpret_cast<const bf16x8_t*>(As + (arow + 32 * i) * kBfLdr + koff);
+    fal[i] = *reinterpret_cast<const bf16x8_t*>(Al + (arow + 32 * i) * kBfLdr + koff);
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    fb[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (brow + 32 * j) * kBfLdr + koff);
+    fbl[j] = *reinterpret_cast<const bf16x8_t*>(Bl + (brow + 32 * j) * kBfLdr + koff);
+  }
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fal[i], fb[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fbl[j], acc[i][j], 0, 0, 0);
+      acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+}
+
+constexpr int igemm_bf_minw(int BM, int BN, int WM, int WN, int planes = 1) {
+  int blocks = 163840 / (2 * (BM + BN) * kBfLdr * 2 * planes);
   if (blocks > 8) blocks = 8;
   const int w = blocks * WM * WN * 64 / 256;
   return w < 1 ? 1 : (w > 2 ? 2 : w);  // <= 2 waves/SIMD: up to 256 registers, no spills
@@ -74,16 +130,24 @@ constexpr int igemm_bf_minw(int BM, int BN, int WM, int WN) {
 // BN+ReLU), Bh packed bf16 [N][K].  Staging: each lane owns 8 consecutive k
 // (32 B of fp32 A, 16 B of bf16 B) of one row per pass.
 // ---------------------------------------------------------------------------
-template <int BM, int BN, int WM, int WN>
-__global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k_igemm_bf(const IgemmArgs args) {
+// SPLIT: operands as hi/lo bf16 pairs (UNET_PREC_BF16X3), B's lo plane in args.bl;
+// a stage then holds [A hi][B hi][A lo][B lo].  LDS is dynamic (igemm_bf_smem).
+template <int BM, int BN, int SPLIT>
+constexpr size_t igemm_bf_smem() {
+  return (size_t)2 * (BM + BN) * kBfLdr * 2 * (SPLIT ? 2 : 1);
+}
+
+template <int BM, int BN, int WM, int WN, int SPLIT>
+__global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN, SPLIT ? 2 : 1)) void k_igemm_bf(
+    const IgemmArgs args) {
   constexpr int NT = WM * WN * 64, BK = kBfBK, LDR = kBfLdr;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   constexpr int RPP = NT / 4;  // staged rows per pass (4 lanes x 8 k per row)
   constexpr int AV = BM / RPP, BV = BN / RPP;
-  constexpr int STAGE = (BM + BN) * LDR;
+  constexpr int PLANE = (BM + BN) * LDR, STAGE = PLANE * (SPLIT ? 2 : 1);
   static_assert(TM >= 1 && TN >= 1 && AV >= 1 && BV >= 1 && BM % RPP == 0 && BN % RPP == 0, "tile");
   static_assert(WM * 3 * BN * 4 <= 2 * STAGE * 2, "epilogue reduction must fit the LDS ring");
-  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * STAGE];
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -106,9 +170,9 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
     rb0[q] = (n * g.s[0].H + y + g.s[0].oy) * g.s[0].W + x + g.s[0].ox;
     rb1[q] = (n * g.s[1].H + y + g.s[1].oy) * g.s[1].W + x + g.s[1].ox;
   }
-  const uint16_t* bptr[BV];
+  int bptr[BV];  // element offsets into args.bh / args.bl
 #pragma unroll
-  for (int q = 0; q < BV; ++q) bptr[q] = args.bh + (size_t)(n0 + row0 + RPP * q) * K + chunk * 8;
+  for (int q = 0; q < BV; ++q) bptr[q] = (n0 + row0 + RPP * q) * K + chunk * 8;
 
   // K range of this workgroup (split-K slices chunks over blockIdx.z)
   const int nk_all = K / BK;
@@ -130,7 +194,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
   }
 
   float4 ra0[AV], ra1[AV];  // two 1-D arrays: a [N][2] array of vectors is not promoted to registers
-  u32x4 rb[BV];
+  u32x4 rb[BV], rbl[SPLIT ? BV : 1];
   float4 sc0, sc1, sh0, sh1;
   bool tf = false, h16 = false;
   auto issue = [&](int k0) {
@@ -150,7 +214,10 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
       }
     }
 #pragma unroll
-    for (int q = 0; q < BV; ++q) rb[q] = *reinterpret_cast<const u32x4*>(bptr[q] + k0);
+    for (int q = 0; q < BV; ++q) {
+      rb[q] = *reinterpret_cast<const u32x4*>(args.bh + bptr[q] + k0);
+      if constexpr (SPLIT) rbl[q] = *reinterpret_cast<const u32x4*>(args.bl + bptr[q] + k0);
+    }
     tf = s.scale != nullptr;
     if (tf) {
       sc0 = ld4(s.scale + c);
@@ -168,11 +235,22 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
     unsigned short* As = lds + buf * STAGE;
     unsigned short* Bs = As + BM * LDR;
 #pragma unroll
-    for (int q = 0; q < AV; ++q)
-      *reinterpret_cast<uint4*>(As + (row0 + RPP * q) * LDR + chunk * 8) =
-          stage8(ra0[q], ra1[q], h16, tf, sc0, sc1, sh0, sh1);
+    for (int q = 0; q < AV; ++q) {
+      unsigned short* d = As + (row0 + RPP * q) * LDR + chunk * 8;
+      if constexpr (SPLIT) {
+        uint4 lo;
+        *reinterpret_cast<uint4*>(d) = stage8x(ra0[q], ra1[q], h16, tf, sc0, sc1, sh0, sh1, lo);
+        *reinterpret_cast<uint4*>(d + PLANE) = lo;
+      } else {
+        *reinterpret_cast<uint4*>(d) = stage8(ra0[q], ra1[q], h16, tf, sc0, sc1, sh0, sh1);
+      }
+    }
 #pragma unroll
-    for (int q = 0; q < BV; ++q) *reinterpret_cast<u32x4*>(Bs + (row0 + RPP * q) * LDR + chunk * 8) = rb[q];
+    for (int q = 0; q < BV; ++q) {
+      unsigned short* d = Bs + (row0 + RPP * q) * LDR + chunk * 8;
+      *reinterpret_cast<u32x4*>(d) = rb[q];
+      if constexpr (SPLIT) *reinterpret_cast<u32x4*>(d + PLANE) = rbl[q];
+    }
   };
 
   floatx16 acc[TM][TN];
@@ -188,7 +266,13 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
     const unsigned short* As = lds + buf * STAGE;
     const unsigned short* Bs = As + BM * LDR;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) bf_mfma_step<TM, TN>(acc, As, Bs, wm * TM * 32 + li, wn * TN * 32 + li, 16 * s + 8 * h);
+    for (int s = 0; s < 2; ++s) {
+      if constexpr (SPLIT)
+        bf_mfma_step_x3<TM, TN>(acc, As, As + PLANE, Bs, Bs + PLANE, wm * TM * 32 + li, wn * TN * 32 + li,
+                                16 * s + 8 * h);
+      else
+        bf_mfma_step<TM, TN>(acc, As, Bs, wm * TM * 32 + li, wn * TN * 32 + li, 16 * s + 8 * h);
+    }
   };
 
   if (kc0 < kc1) {
@@ -224,12 +308,13 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_bf_minw(BM, BN, WM, WN)) void k
 // MFMA rows = output pixels in row-major tile order (32 per fragment), so a
 // fragment lane reads LDS pixel (ry + ty)(TW+2) + rx + tx: one ds_read_b128.
 // ---------------------------------------------------------------------------
-template <int TH, int TW, int BN>
+// SPLIT (UNET_PREC_BF16X3): halo and weights as hi/lo planes, [A hi][B hi][A lo][B lo].
+template <int TH, int TW, int BN, int SPLIT = 0>
 constexpr size_t conv3_bf_smem(int cg) {
-  return (size_t)((TH + 2) * (TW + 2) + 9 * BN) * kBfLdr * 2 + (size_t)2 * cg * 4;
+  return (size_t)((TH + 2) * (TW + 2) + 9 * BN) * kBfLdr * 2 * (SPLIT ? 2 : 1) + (size_t)2 * cg * 4;
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int MINW>
+template <int TH, int TW, int BN, int WM, int WN, int MINW, int SPLIT>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs args) {
   constexpr int NT = WM * WN * 64, BM = TH * TW, LDR = kBfLdr;
   constexpr int HW2 = TW + 2, PH = (TH + 2) * HW2;  // halo pixels
@@ -240,9 +325,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
   static_assert(BM % 32 == 0 && FM % WM == 0 && TM >= 1 && TN >= 1, "tile");
   static_assert(WM * 3 * BN * 4 <= A_ELEMS * 2, "epilogue reduction must fit the halo buffer");
   extern __shared__ __attribute__((aligned(16))) unsigned short smem[];
+  constexpr int PLANE = A_ELEMS + B_ELEMS;  // offset of the lo plane
   unsigned short* As = smem;
   unsigned short* Bs = smem + A_ELEMS;
-  float* ssc = reinterpret_cast<float*>(smem + A_ELEMS + B_ELEMS);  // [2][Cg]
+  float* ssc = reinterpret_cast<float*>(smem + PLANE * (SPLIT ? 2 : 1));  // [2][Cg]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -296,7 +382,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
   }
 
   float4 ra0[NA], ra1[NA];  // two 1-D arrays: a [N][2] array of vectors is not promoted to registers
-  u32x4 rb[NB];
+  u32x4 rb[NB], rbl[SPLIT ? NB : 1];
   auto issue = [&](int kc) {
     const int c0 = kc * 32;
     const bool second = c0 >= g.c_split;
@@ -316,7 +402,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k)
-      if (tid + k * NT < UB) rb[k] = *reinterpret_cast<const u32x4*>(args.bh + bsrc[k] + c0);
+      if (tid + k * NT < UB) {
+        rb[k] = *reinterpret_cast<const u32x4*>(args.bh + bsrc[k] + c0);
+        if constexpr (SPLIT) rbl[k] = *reinterpret_cast<const u32x4*>(args.bl + bsrc[k] + c0);
+      }
   };
   auto commit = [&](int kc) {
     const int c = kc * 32 + (tid & 3) * 8;
@@ -332,14 +421,25 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
 #pragma unroll
     for (int k = 0; k < NA; ++k) {
       const int u = tid + k * NT;
-      if (u < UA)
-        *reinterpret_cast<uint4*>(As + (u >> 2) * LDR + (u & 3) * 8) =
-            stage8(ra0[k], ra1[k], h16, tf, sc0, sc1, sh0, sh1);
+      if (u < UA) {
+        unsigned short* d = As + (u >> 2) * LDR + (u & 3) * 8;
+        if constexpr (SPLIT) {
+          uint4 lo;
+          *reinterpret_cast<uint4*>(d) = stage8x(ra0[k], ra1[k], h16, tf, sc0, sc1, sh0, sh1, lo);
+          *reinterpret_cast<uint4*>(d + PLANE) = lo;
+        } else {
+          *reinterpret_cast<uint4*>(d) = stage8(ra0[k], ra1[k], h16, tf, sc0, sc1, sh0, sh1);
+        }
+      }
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
       const int u = tid + k * NT;
-      if (u < UB) *reinterpret_cast<u32x4*>(Bs + (u >> 2) * LDR + (u & 3) * 8) = rb[k];
+      if (u < UB) {
+        unsigned short* d = Bs + (u >> 2) * LDR + (u & 3) * 8;
+        *reinterpret_cast<u32x4*>(d) = rb[k];
+        if constexpr (SPLIT) *reinterpret_cast<u32x4*>(d + PLANE) = rbl[k];
+      }
     }
   };
 
@@ -364,18 +464,29 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
       const int off = (tap / 3) * HW2 + tap % 3;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        bf16x8_t fa[TM], fb[TN];
+        bf16x8_t fa[TM], fb[TN], fal[SPLIT ? TM : 1], fbl[SPLIT ? TN : 1];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const unsigned short* p = As + (abase[i] + off) * LDR + 16 * s + 8 * h;
+          fa[i] = *reinterpret_cast<const bf16x8_t*>(p);
+          if constexpr (SPLIT) fal[i] = *reinterpret_cast<const bf16x8_t*>(p + PLANE);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const unsigned short* p = Bs + (tap * BN + wn * TN * 32 + j * 32 + li) * LDR + 16 * s + 8 * h;
+          fb[j] = *reinterpret_cast<const bf16x8_t*>(p);
+          if constexpr (SPLIT) fbl[j] = *reinterpret_cast<const bf16x8_t*>(p + PLANE);
+        }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
-          fa[i] = *reinterpret_cast<const bf16x8_t*>(As + (abase[i] + off) * LDR + 16 * s + 8 * h);
 #pragma unroll
-        for (int j = 0; j < TN; ++j)
-          fb[j] = *reinterpret_cast<const bf16x8_t*>(Bs + (tap * BN + wn * TN * 32 + j * 32 + li) * LDR + 16 * s + 8 * h);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j)
+          for (int j = 0; j < TN; ++j) {
+            if constexpr (SPLIT) {
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fal[i], fb[j], acc[i][j], 0, 0, 0);
+              acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fbl[j], acc[i][j], 0, 0, 0);
+            }
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+          }
       }
     }
   };
@@ -415,15 +526,22 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
 // AH / BH: storage of the A / B sources (0 fp32, 1 bf16, 2 per unit -- the
 // concat gather of an up block's first conv mixes an fp32 skip and a bf16
 // upsampled map); compile-time so that the staging loads carry no branches.
-template <int BM, int BN, int WM, int WN, int AH, int BH>
+// SPLIT (UNET_PREC_BF16X3, fp32 sources only): hi/lo planes per stage, dynamic LDS.
+template <int BM, int BN, int SPLIT>
+constexpr size_t wgrad_bf_smem() {
+  return (size_t)2 * (BM + BN) * kBfLdr * 2 * (SPLIT ? 2 : 1);
+}
+
+template <int BM, int BN, int WM, int WN, int AH, int BH, int SPLIT>
 __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs args) {
   constexpr int NT = WM * WN * 64, BK = kBfBK, LDR = kBfLdr;
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   constexpr int UA = BM, UB = BN;  // units: 4 pixel groups x (rows / 4) quads
   constexpr int UPT = (UA + UB + NT - 1) / NT;
-  constexpr int STAGE = (BM + BN) * LDR;
+  constexpr int PLANE = (BM + BN) * LDR, STAGE = PLANE * (SPLIT ? 2 : 1);
   static_assert(TM >= 1 && TN >= 1 && BM % 64 == 0, "tile");
-  __shared__ __attribute__((aligned(16))) unsigned short lds[2 * STAGE];
+  static_assert(!SPLIT || (AH == 0 && BH == 0), "split operands come from fp32 storage");
+  extern __shared__ __attribute__((aligned(16))) unsigned short lds[];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
@@ -541,18 +659,19 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
         v[k][j] = (valid[k] >> j) & 1 ? t : make_float4(0.f, 0.f, 0.f, 0.f);
       }
       unsigned short* dst = S + lrow[k] * LDR + grp[k] * 8;
-      *reinterpret_cast<uint4*>(dst + 0 * LDR) =
-          make_uint4(bf16pack(v[k][0].x, v[k][1].x), bf16pack(v[k][2].x, v[k][3].x), bf16pack(v[k][4].x, v[k][5].x),
-                     bf16pack(v[k][6].x, v[k][7].x));
-      *reinterpret_cast<uint4*>(dst + 1 * LDR) =
-          make_uint4(bf16pack(v[k][0].y, v[k][1].y), bf16pack(v[k][2].y, v[k][3].y), bf16pack(v[k][4].y, v[k][5].y),
-                     bf16pack(v[k][6].y, v[k][7].y));
-      *reinterpret_cast<uint4*>(dst + 2 * LDR) =
-          make_uint4(bf16pack(v[k][0].z, v[k][1].z), bf16pack(v[k][2].z, v[k][3].z), bf16pack(v[k][4].z, v[k][5].z),
-                     bf16pack(v[k][6].z, v[k][7].z));
-      *reinterpret_cast<uint4*>(dst + 3 * LDR) =
-          make_uint4(bf16pack(v[k][0].w, v[k][1].w), bf16pack(v[k][2].w, v[k][3].w), bf16pack(v[k][4].w, v[k][5].w),
-                     bf16pack(v[k][6].w, v[k][7].w));
+      // row r of the unit's 4: component r of the 8 pixels
+      auto put_row = [&](unsigned short* d, float a0, float a1, float a2, float a3, float a4, float a5, float a6,
+                         float a7) {
+        const uint4 hi = make_uint4(bf16pack(a0, a1), bf16pack(a2, a3), bf16pack(a4, a5), bf16pack(a6, a7));
+        *reinterpret_cast<uint4*>(d) = hi;
+        if constexpr (SPLIT)
+          *reinterpret_cast<uint4*>(d + PLANE) = make_uint4(bf16pack_lo(a0, a1, hi.x), bf16pack_lo(a2, a3, hi.y),
+                                                            bf16pack_lo(a4, a5, hi.z), bf16pack_lo(a6, a7, hi.w));
+      };
+      put_row(dst + 0 * LDR, v[k][0].x, v[k][1].x, v[k][2].x, v[k][3].x, v[k][4].x, v[k][5].x, v[k][6].x, v[k][7].x);
+      put_row(dst + 1 * LDR, v[k][0].y, v[k][1].y, v[k][2].y, v[k][3].y, v[k][4].y, v[k][5].y, v[k][6].y, v[k][7].y);
+      put_row(dst + 2 * LDR, v[k][0].z, v[k][1].z, v[k][2].z, v[k][3].z, v[k][4].z, v[k][5].z, v[k][6].z, v[k][7].z);
+      put_row(dst + 3 * LDR, v[k][0].w, v[k][1].w, v[k][2].w, v[k][3].w, v[k][4].w, v[k][5].w, v[k][6].w, v[k][7].w);
     }
   };
 
@@ -575,7 +694,13 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
     const unsigned short* As = lds + cur * STAGE;
     const unsigned short* Bs = As + BM * LDR;
 #pragma unroll
-    for (int s = 0; s < 2; ++s) bf_mfma_step<TM, TN>(acc, As, Bs, wm * TM * 32 + li, wn * TN * 32 + li, 16 * s + 8 * h);
+    for (int s = 0; s < 2; ++s) {
+      if constexpr (SPLIT)
+        bf_mfma_step_x3<TM, TN>(acc, As, As + PLANE, Bs, Bs + PLANE, wm * TM * 32 + li, wn * TN * 32 + li,
+                                16 * s + 8 * h);
+      else
+        bf_mfma_step<TM, TN>(acc, As, Bs, wm * TM * 32 + li, wn * TN * 32 + li, 16 * s + 8 * h);
+    }
     if (more) commit(cur ^ 1);
     __syncthreads();
   }
@@ -816,12 +941,13 @@ __device__ __forceinline__ bf16x4_t tr_read(const unsigned char* p) {
 }
 __device__ __forceinline__ int wg3_swz(int row, int chunk) { return chunk ^ (((row >> 1) & 1) << 2); }
 
-template <int TH, int TW>
+// SPLIT (UNET_PREC_BF16X3): dY tile and X halo as hi/lo planes ([A][B] hi, then lo).
+template <int TH, int TW, int SPLIT = 0>
 constexpr size_t wgrad3_smem() {
-  return (size_t)(TH * TW + (TH + 2) * (TW + 2)) * 128 + 2 * 64 * 4;
+  return (size_t)(TH * TW + (TH + 2) * (TW + 2)) * 128 * (SPLIT ? 2 : 1) + 2 * 64 * 4;
 }
 
-template <int TH, int TW, int D16>
+template <int TH, int TW, int D16, int SPLIT>
 __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
   constexpr int NT = 512, BC = 64, ROWB = 128, NTAP = 5;
   constexpr int PT = TH * TW, HW2 = TW + 2, PH = (TH + 2) * HW2;
@@ -829,9 +955,11 @@ __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
   constexpr int NA = (UA + NT - 1) / NT, NB = (UB + NT - 1) / NT;
   static_assert(TW % 16 == 0 && UA % NT == 0, "a 16-pixel k-step stays inside one tile row");
   extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
+  static_assert(!SPLIT || !D16, "split operands come from fp32 storage");
+  constexpr int PLANE = (PT + PH) * ROWB;                        // bytes, offset of the lo plane
   unsigned char* Ad = wsm;                                       // dY tile [PT][64]
   unsigned char* Bx = wsm + PT * ROWB;                           // X halo [PH][64]
-  float* ssc = reinterpret_cast<float*>(wsm + (PT + PH) * ROWB);  // [2][64]
+  float* ssc = reinterpret_cast<float*>(wsm + PLANE * (SPLIT ? 2 : 1));  // [2][64]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const Gather& gb = args.gb;
@@ -896,11 +1024,14 @@ __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
     for (int k = 0; k < NA; ++k) {
       const int u = tid + k * NT;
       const int p = u >> 3, ch = u & 7;
-      uint4 o;
+      uint4 o, ol = make_uint4(0u, 0u, 0u, 0u);
       if constexpr (D16) o = rdh[k];
       else o = bf16pack8(rdf[k][0], rdf[k][1]);
-      if (!((dvalid >> k) & 1)) o = make_uint4(0u, 0u, 0u, 0u);  // pixels past the grid add nothing
-      *reinterpret_cast<uint4*>(Ad + p * ROWB + wg3_swz(p, ch) * 16) = o;
+      if constexpr (SPLIT) ol = bf16pack8_lo(rdf[k][0], rdf[k][1], o);
+      if (!((dvalid >> k) & 1)) o = ol = make_uint4(0u, 0u, 0u, 0u);  // pixels past the grid add nothing
+      unsigned char* d = Ad + p * ROWB + wg3_swz(p, ch) * 16;
+      *reinterpret_cast<uint4*>(d) = o;
+      if constexpr (SPLIT) *reinterpret_cast<uint4*>(d + PLANE) = ol;
     }
 #pragma unroll
     for (int k = 0; k < NB; ++k) {
@@ -914,8 +1045,14 @@ __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
           sh0 = ld4(ssc + BC + ch * 8);
           sh1 = ld4(ssc + BC + ch * 8 + 4);
         }
-        *reinterpret_cast<uint4*>(Bx + hp * ROWB + wg3_swz(hp, ch) * 16) =
-            stage8(rx[k][0], rx[k][1], x16, xtf, sc0, sc1, sh0, sh1);
+        unsigned char* d = Bx + hp * ROWB + wg3_swz(hp, ch) * 16;
+        if constexpr (SPLIT) {
+          uint4 lo;
+          *reinterpret_cast<uint4*>(d) = stage8x(rx[k][0], rx[k][1], x16, xtf, sc0, sc1, sh0, sh1, lo);
+          *reinterpret_cast<uint4*>(d + PLANE) = lo;
+        } else {
+          *reinterpret_cast<uint4*>(d) = stage8(rx[k][0], rx[k][1], x16, xtf, sc0, sc1, sh0, sh1);
+        }
       }
     }
   };
@@ -938,21 +1075,27 @@ __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
 #pragma unroll 2
     for (int ks = 0; ks < PT / 16; ++ks) {
       const int prow = (ks * 16) / TW, px0 = (ks * 16) % TW;
-      bf16x8_t fa;
-      {
-        const int pa = ks * 16 + 8 * hk + q;
-        const bf16x4_t lo = tr_read(Ad + pa * ROWB + wg3_swz(pa, cA) * 16 + bA);
-        const bf16x4_t hi = tr_read(Ad + (pa + 4) * ROWB + wg3_swz(pa + 4, cA) * 16 + bA);
-        fa = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
-      }
+      // 8 pixels (k) of one lane: rows r and r + 4 of the transposed read
+      auto frag = [&](const unsigned char* base, int r, int cc, int bo) {
+        const bf16x4_t a = tr_read(base + r * ROWB + wg3_swz(r, cc) * 16 + bo);
+        const bf16x4_t b = tr_read(base + (r + 4) * ROWB + wg3_swz(r + 4, cc) * 16 + bo);
+        return (bf16x8_t)__builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+      const int pa = ks * 16 + 8 * hk + q;
+      const bf16x8_t fa = frag(Ad, pa, cA, bA);
+      bf16x8_t fal;
+      if constexpr (SPLIT) fal = frag(Ad + PLANE, pa, cA, bA);
 #pragma unroll
       for (int j = 0; j < NTAP; ++j) {
         if (j < ntap) {
           const int tap = tap0 + j;
           const int hb = (prow + tap / 3) * HW2 + px0 + tap % 3 + 8 * hk + q;
-          const bf16x4_t lo = tr_read(Bx + hb * ROWB + wg3_swz(hb, cB) * 16 + bB);
-          const bf16x4_t hi = tr_read(Bx + (hb + 4) * ROWB + wg3_swz(hb + 4, cB) * 16 + bB);
-          const bf16x8_t fb = __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+          const bf16x8_t fb = frag(Bx, hb, cB, bB);
+          if constexpr (SPLIT) {
+            const bf16x8_t fbl = frag(Bx + PLANE, hb, cB, bB);
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fal, fb, acc[j], 0, 0, 0);
+            acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fbl, acc[j], 0, 0, 0);
+          }
           acc[j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa, fb, acc[j], 0, 0, 0);
         }
       }
@@ -991,22 +1134,27 @@ __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
   }
 }
 
-template <int TH, int TW, int D16>
+// dynamic LDS above the 64 KiB default needs the attribute once per kernel
+static hipError_t allow_smem(const void* fn, size_t bytes, bool& done) {
+  if (done) return hipSuccess;
+  hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) done = true;
+  return e;
+}
+constexpr size_t kLdsBytes = 160 * 1024;
+
+template <int TH, int TW, int D16, int SPLIT>
 static hipError_t go_wgrad3(const WgradArgs& a, hipStream_t s, int per_cu) {
   static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad3_bf<TH, TW, D16>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)wgrad3_smem<TH, TW>());
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  const size_t smem = wgrad3_smem<TH, TW, SPLIT>();
+  hipError_t e = allow_smem(reinterpret_cast<const void*>(&k_wgrad3_bf<TH, TW, D16, SPLIT>), smem, attr);
+  if (e != hipSuccess) return e;
   const int tiles = a.gb.nimg * ((a.gb.Hg + TH - 1) / TH) * ((a.gb.Wg + TW - 1) / TW);
   const int blocks = (a.Mo / 64) * (a.gb.Cg / 64);
   int splits = (per_cu * num_cus() + blocks - 1) / blocks;
   splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
   dim3 grid(a.Mo / 64, a.gb.Cg / 64, splits);
-  const size_t smem = wgrad3_smem<TH, TW>();
-  hipLaunchKernelGGL((k_wgrad3_bf<TH, TW, D16>), grid, dim3(512), smem, s, a);
+  hipLaunchKernelGGL((k_wgrad3_bf<TH, TW, D16, SPLIT>), grid, dim3(512), smem, s, a);
   return hipGetLastError();
 }
 
@@ -1015,86 +1163,114 @@ bool wgrad3_fits(const WgradArgs& a) {
   const Gather& g = a.gb;
   return a.bf16 && g.taps_h == 3 && g.taps_w == 3 && g.stride == 1 && a.No == 9 * g.Cg && a.Mo % 64 == 0 &&
          g.Cg % 64 == 0 && (g.c_split % 64 == 0 || g.c_split >= g.Cg) && a.ga.Cg == a.Mo && a.ga.taps_h == 1 &&
-         a.ga.taps_w == 1 && g.Hg == a.ga.Hg && g.Wg == a.ga.Wg && g.nimg == a.ga.nimg;
+         a.ga.taps_w == 1 && g.Hg == a.ga.Hg && g.Wg == a.ga.Wg && g.nimg == a.ga.nimg &&
+         !(a.split && a.ga.s[0].h16);
 }
 
 hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu) {
   if (!wgrad3_fits(a)) return hipErrorInvalidValue;
   const bool d16 = a.ga.s[0].h16 != 0;
+  if (a.split) {
+    switch (tile) {
+      case 20: return go_wgrad3<8, 16, 0, 1>(a, s, per_cu);
+      case 21: return go_wgrad3<4, 32, 0, 1>(a, s, per_cu);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (tile * 2 + (d16 ? 1 : 0)) {
-    case 40: return go_wgrad3<8, 16, 0>(a, s, per_cu);
-    case 41: return go_wgrad3<8, 16, 1>(a, s, per_cu);
-    case 42: return go_wgrad3<4, 32, 0>(a, s, per_cu);
-    case 43: return go_wgrad3<4, 32, 1>(a, s, per_cu);
+    case 40: return go_wgrad3<8, 16, 0, 0>(a, s, per_cu);
+    case 41: return go_wgrad3<8, 16, 1, 0>(a, s, per_cu);
+    case 42: return go_wgrad3<4, 32, 0, 0>(a, s, per_cu);
+    case 43: return go_wgrad3<4, 32, 1, 0>(a, s, per_cu);
     default: return hipErrorInvalidValue;
   }
 }
 
 // ---------------------------------------------------------------------------
-// fp32 -> bf16 (RNE) of the packed weight region, 4 elements per lane-step
+// fp32 -> bf16 (RNE) of the packed weight region, 4 elements per lane-step;
+// with `lo` also the residual plane bf16(v - bf16(v)) of split operands
 // ---------------------------------------------------------------------------
-__global__ void k_f2bf(const float* __restrict__ in, uint16_t* __restrict__ out, size_t n4) {
+__global__ void k_f2bf(const float* __restrict__ in, uint16_t* __restrict__ out, uint16_t* __restrict__ lo,
+                       size_t n4) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n4; i += (size_t)gridDim.x * blockDim.x) {
     const float4 v = ld4(in + 4 * i);
-    *reinterpret_cast<uint2*>(out + 4 * i) = make_uint2(bf16pack(v.x, v.y), bf16pack(v.z, v.w));
+    const uint2 h = make_uint2(bf16pack(v.x, v.y), bf16pack(v.z, v.w));
+    *reinterpret_cast<uint2*>(out + 4 * i) = h;
+    if (lo) *reinterpret_cast<uint2*>(lo + 4 * i) = make_uint2(bf16pack_lo(v.x, v.y, h.x), bf16pack_lo(v.z, v.w, h.y));
   }
 }
 
-hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s) {
-  if (n % 4 || (reinterpret_cast<uintptr_t>(in) & 15) || (reinterpret_cast<uintptr_t>(out) & 7))
+hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s, uint16_t* lo) {
+  if (n % 4 || (reinterpret_cast<uintptr_t>(in) & 15) || (reinterpret_cast<uintptr_t>(out) & 7) ||
+      (reinterpret_cast<uintptr_t>(lo) & 7))
     return hipErrorInvalidValue;
   const size_t n4 = n / 4;
   size_t grid = (n4 + 255) / 256;
   if (grid > 8192) grid = 8192;
   if (grid < 1) grid = 1;
-  hipLaunchKernelGGL(k_f2bf, dim3((unsigned)grid), dim3(256), 0, s, in, out, n4);
+  hipLaunchKernelGGL(k_f2bf, dim3((unsigned)grid), dim3(256), 0, s, in, out, lo, n4);
   return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
-// launchers (tile ids: igemm.hip tile_info 21-26, wgrad_tile 10-14)
+// launchers (tile ids: igemm.hip tile_info 21-26, 31-36, 41-44; wgrad_tile
+// 10-14, 20-21).  Split operands (a.bl / a.split) select the SPLIT kernels.
 // ---------------------------------------------------------------------------
+template <int BM, int BN, int WM, int WN, int SPLIT>
+static hipError_t go_bf_t(const IgemmArgs& a, hipStream_t s) {
+  static bool attr = false;
+  const size_t smem = igemm_bf_smem<BM, BN, SPLIT>();
+  hipError_t e = allow_smem(reinterpret_cast<const void*>(&k_igemm_bf<BM, BN, WM, WN, SPLIT>), smem, attr);
+  if (e != hipSuccess) return e;
+  dim3 grid((a.M + BM - 1) / BM, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
+  hipLaunchKernelGGL((k_igemm_bf<BM, BN, WM, WN, SPLIT>), grid, dim3(WM * WN * 64), smem, s, a);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WM, int WN>
 static hipError_t go_bf(const IgemmArgs& a, hipStream_t s) {
   if (a.bh == nullptr || a.N % BN != 0 || a.K % kBfBK != 0 || a.a.Cg % kBfBK != 0 || a.a.c_split % kBfBK != 0)
     return hipErrorInvalidValue;
-  dim3 grid((a.M + BM - 1) / BM, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
-  hipLaunchKernelGGL((k_igemm_bf<BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, s, a);
+  return a.bl ? go_bf_t<BM, BN, WM, WN, 1>(a, s) : go_bf_t<BM, BN, WM, WN, 0>(a, s);
+}
+
+template <int TH, int TW, int BN, int WM, int WN, int MINW, int SPLIT>
+static hipError_t go_halo_t(const IgemmArgs& a, hipStream_t s) {
+  static bool attr = false;
+  hipError_t e = allow_smem(reinterpret_cast<const void*>(&k_conv3_bf<TH, TW, BN, WM, WN, MINW, SPLIT>),
+                            conv3_bf_smem<TH, TW, BN, SPLIT>(1024), attr);
+  if (e != hipSuccess) return e;
+  const long long tiles = (long long)a.a.nimg * ((a.a.Hg + TH - 1) / TH) * ((a.a.Wg + TW - 1) / TW);
+  dim3 grid((unsigned)tiles, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
+  const size_t smem = conv3_bf_smem<TH, TW, BN, SPLIT>(a.a.Cg);
+  hipLaunchKernelGGL((k_conv3_bf<TH, TW, BN, WM, WN, MINW, SPLIT>), grid, dim3(WM * WN * 64), smem, s, a);
   return hipGetLastError();
 }
 
+// split variants run at <= 2 waves/SIMD (their LDS holds one workgroup per CU)
 template <int TH, int TW, int BN, int WM, int WN, int MINW>
 static hipError_t go_halo(const IgemmArgs& a, hipStream_t s) {
   if (a.bh == nullptr || a.N % BN != 0 || a.a.Cg % 32 != 0 || a.a.c_split % 32 != 0 || a.a.taps_h != 3 ||
       a.a.taps_w != 3 || a.a.stride != 1 || a.K != 9 * a.a.Cg || a.a.Cg > 1024)
     return hipErrorInvalidValue;
-  static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3_bf<TH, TW, BN, WM, WN, MINW>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize,
-                                       (int)conv3_bf_smem<TH, TW, BN>(1024));
-    if (e != hipSuccess) return e;
-    attr = true;
+  if (a.bl) {
+    // the lo fragments double the operand registers: at most 2 accumulator tiles per wave
+    constexpr int TM = TH * TW / 32 / WM, TN = BN / (WN * 32);
+    if constexpr (conv3_bf_smem<TH, TW, BN, 1>(1024) <= kLdsBytes && TM * TN <= 2)
+      return go_halo_t<TH, TW, BN, WM, WN, (MINW < 2 ? MINW : 2), 1>(a, s);
+    return hipErrorInvalidValue;
   }
-  const long long tiles = (long long)a.a.nimg * ((a.a.Hg + TH - 1) / TH) * ((a.a.Wg + TW - 1) / TW);
-  dim3 grid((unsigned)tiles, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
-  const size_t smem = conv3_bf_smem<TH, TW, BN>(a.a.Cg);
-  hipLaunchKernelGGL((k_conv3_bf<TH, TW, BN, WM, WN, MINW>), grid, dim3(WM * WN * 64), smem, s, a);
-  return hipGetLastError();
+  return go_halo_t<TH, TW, BN, WM, WN, MINW, 0>(a, s);
 }
 
 template <int TH, int TW>
 static hipError_t go_halo_p(const IgemmArgs& a, hipStream_t s, int waves_of_cus) {
-  if (a.bh == nullptr || a.N % 64 != 0 || a.a.Cg % 32 != 0 || a.a.c_split % 32 != 0 || a.a.taps_h != 3 ||
-      a.a.taps_w != 3 || a.a.stride != 1 || a.K != 9 * a.a.Cg || a.a.Cg > 1024)
+  if (a.bh == nullptr || a.bl != nullptr || a.N % 64 != 0 || a.a.Cg % 32 != 0 || a.a.c_split % 32 != 0 ||
+      a.a.taps_h != 3 || a.a.taps_w != 3 || a.a.stride != 1 || a.K != 9 * a.a.Cg || a.a.Cg > 1024)
     return hipErrorInvalidValue;
   static bool attr = false;
-  if (!attr) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3p_bf<TH, TW>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)conv3p_smem<TH, TW>(1024));
-    if (e != hipSuccess) return e;
-    attr = true;
-  }
+  hipError_t e = allow_smem(reinterpret_cast<const void*>(&k_conv3p_bf<TH, TW>), conv3p_smem<TH, TW>(1024), attr);
+  if (e != hipSuccess) return e;
   const long long tiles = (long long)a.a.nimg * ((a.a.Hg + TH - 1) / TH) * ((a.a.Wg + TW - 1) / TW);
   const int ks = a.ksplit > 1 ? a.ksplit : 1;
   const long long cols = (long long)(a.N / 64) * ks;
@@ -1121,7 +1297,13 @@ bool halo_tile_shape(int tile, int& th, int& tw, int& bn) {
   }
 }
 
+// tiles with a split-operand kernel (the LDS of 34/36 and the persistent
+// kernel's double buffer do not hold the lo planes; 32's 4 accumulator tiles
+// per wave would spill)
+bool bf16_tile_splits(int tile) { return (tile >= 21 && tile <= 26) || tile == 31 || tile == 33 || tile == 35; }
+
 hipError_t go_igemm_bf16(const IgemmArgs& a, hipStream_t s, int tile) {
+  if (a.bl && !bf16_tile_splits(tile)) return hipErrorInvalidValue;
   switch (tile) {
     case 31: return go_halo<8, 32, 64, 8, 1, 4>(a, s);
     case 32: return go_halo<8, 32, 64, 4, 1, 2>(a, s);
@@ -1144,17 +1326,26 @@ hipError_t go_igemm_bf16(const IgemmArgs& a, hipStream_t s, int tile) {
   }
 }
 
-template <int AH, int BH>
+template <int BM, int BN, int WM, int WN, int AH, int BH, int SPLIT>
+static hipError_t go_wgrad_bf_t(const WgradArgs& a, hipStream_t s, dim3 grid) {
+  static bool attr = false;
+  const size_t smem = wgrad_bf_smem<BM, BN, SPLIT>();
+  hipError_t e = allow_smem(reinterpret_cast<const void*>(&k_wgrad_bf<BM, BN, WM, WN, AH, BH, SPLIT>), smem, attr);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((k_wgrad_bf<BM, BN, WM, WN, AH, BH, SPLIT>), grid, dim3(WM * WN * 64), smem, s, a);
+  return hipGetLastError();
+}
+
+template <int AH, int BH, int SPLIT>
 static hipError_t wgrad_bf_tile(const WgradArgs& a, hipStream_t s, int tile, dim3 grid) {
   switch (tile) {
-    case 10: hipLaunchKernelGGL((k_wgrad_bf<128, 128, 2, 2, AH, BH>), grid, dim3(256), 0, s, a); break;
-    case 11: hipLaunchKernelGGL((k_wgrad_bf<128, 192, 2, 2, AH, BH>), grid, dim3(256), 0, s, a); break;
-    case 12: hipLaunchKernelGGL((k_wgrad_bf<64, 128, 2, 2, AH, BH>), grid, dim3(256), 0, s, a); break;
-    case 13: hipLaunchKernelGGL((k_wgrad_bf<64, 64, 2, 2, AH, BH>), grid, dim3(256), 0, s, a); break;
-    case 14: hipLaunchKernelGGL((k_wgrad_bf<256, 128, 4, 2, AH, BH>), grid, dim3(512), 0, s, a); break;
+    case 10: return go_wgrad_bf_t<128, 128, 2, 2, AH, BH, SPLIT>(a, s, grid);
+    case 11: return go_wgrad_bf_t<128, 192, 2, 2, AH, BH, SPLIT>(a, s, grid);
+    case 12: return go_wgrad_bf_t<64, 128, 2, 2, AH, BH, SPLIT>(a, s, grid);
+    case 13: return go_wgrad_bf_t<64, 64, 2, 2, AH, BH, SPLIT>(a, s, grid);
+    case 14: return go_wgrad_bf_t<256, 128, 4, 2, AH, BH, SPLIT>(a, s, grid);
     default: return hipErrorInvalidValue;
   }
-  return hipGetLastError();
 }
 
 hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid) {
@@ -1162,13 +1353,14 @@ hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid)
   const int ah = a.ga.s[0].h16;
   const bool two = a.gb.c_split < a.gb.Cg;
   const int bh = two && a.gb.s[0].h16 != a.gb.s[1].h16 ? 2 : a.gb.s[0].h16;
+  if (a.split) return ah == 0 && bh == 0 ? wgrad_bf_tile<0, 0, 1>(a, s, tile, grid) : hipErrorInvalidValue;
   switch (ah * 3 + bh) {
-    case 0: return wgrad_bf_tile<0, 0>(a, s, tile, grid);
-    case 1: return wgrad_bf_tile<0, 1>(a, s, tile, grid);
-    case 2: return wgrad_bf_tile<0, 2>(a, s, tile, grid);
-    case 3: return wgrad_bf_tile<1, 0>(a, s, tile, grid);
-    case 4: return wgrad_bf_tile<1, 1>(a, s, tile, grid);
-    default: return wgrad_bf_tile<1, 2>(a, s, tile, grid);
+    case 0: return wgrad_bf_tile<0, 0, 0>(a, s, tile, grid);
+    case 1: return wgrad_bf_tile<0, 1, 0>(a, s, tile, grid);
+    case 2: return wgrad_bf_tile<0, 2, 0>(a, s, tile, grid);
+    case 3: return wgrad_bf_tile<1, 0, 0>(a, s, tile, grid);
+    case 4: return wgrad_bf_tile<1, 1, 0>(a, s, tile, grid);
+    default: return wgrad_bf_tile<1, 2, 0>(a, s, tile, grid);
   }
 }
 

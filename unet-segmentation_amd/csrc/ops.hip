@@ -23,13 +23,16 @@ inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 // entry points (the plan has its own, unet_plan_create_ex)
 int g_op_prec = UNET_PREC_FP32;
 
-// bf16 per-op GEMMs: round the packed fp32 B (n elements) into `scratch` and
-// point the GEMM at it
+// bf16 / split per-op GEMMs: round the packed fp32 B (n elements) into
+// `scratch` (4n bytes: hi plane, then the lo plane of split operands) and point
+// the GEMM at it
 hipError_t op_b_to_bf16(IgemmArgs& a, size_t n, void* scratch, hipStream_t s) {
-  if (g_op_prec != UNET_PREC_BF16) return hipSuccess;
+  if (g_op_prec == UNET_PREC_FP32) return hipSuccess;
   uint16_t* bh = reinterpret_cast<uint16_t*>(scratch);
-  hipError_t e = launch_f2bf(a.b, bh, n, s);
+  uint16_t* bl = g_op_prec == UNET_PREC_BF16X3 ? bh + n : nullptr;
+  hipError_t e = launch_f2bf(a.b, bh, n, s, bl);
   a.bh = bh;
+  a.bl = bl;
   a.b = nullptr;
   return e;
 }
@@ -155,7 +158,8 @@ int unet_conv3x3_wgrad(const float* x, const float* dy, int n, int h, int w, int
   a.No = 9 * ci;
   a.P = n * (h - 2) * (w - 2);
   a.out = dwp;
-  a.bf16 = g_op_prec == UNET_PREC_BF16;
+  a.bf16 = g_op_prec != UNET_PREC_FP32;
+  a.split = g_op_prec == UNET_PREC_BF16X3;
   OPCK(launch_wgrad(a, s));
   OPCK(launch_permute_last2(dwp, co, 9, ci, dw, s));
   if (db) {
@@ -226,7 +230,7 @@ int unet_convT2_bwd(const float* x, const float* dy, int n, int h, int w, int ci
   a.N = ci;
   a.K = 4 * co;
   a.e.d[0] = Dst{dx, h, w, ci, 0, 0};
-  OPCK(op_b_to_bf16(a, 4 * (size_t)ci * co, p + 3 * wb + al256(sizeof(double) * kStatGroups * 2 * co), s));
+  OPCK(op_b_to_bf16(a, 4 * (size_t)ci * co, wf, s));  // wf (4n bytes) is not read again
   OPCK(launch_igemm(a, s));
   OPCK(hipMemsetAsync(dwp, 0, sizeof(float) * 4 * (size_t)ci * co, s));
   WgradArgs g;
@@ -251,7 +255,8 @@ int unet_convT2_bwd(const float* x, const float* dy, int n, int h, int w, int ci
   g.No = 4 * co;
   g.P = n * h * w;
   g.out = dwp;
-  g.bf16 = g_op_prec == UNET_PREC_BF16;
+  g.bf16 = g_op_prec != UNET_PREC_FP32;
+  g.split = g_op_prec == UNET_PREC_BF16X3;
   OPCK(launch_wgrad(g, s));
   OPCK(launch_permute_last2(dwp, ci, 4, co, dw, s));
   OPCK(hipMemsetAsync(st2, 0, sizeof(double) * kStatGroups * 2 * co, s));
@@ -344,7 +349,7 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "force_tile") g_force_tile = value;
   else if (k == "concurrent") g_concurrent = value;
   else if (k == "op_precision") {
-    if (value != UNET_PREC_FP32 && value != UNET_PREC_BF16) return -EINVAL;
+    if (value != UNET_PREC_FP32 && value != UNET_PREC_BF16 && value != UNET_PREC_BF16X3) return -EINVAL;
     g_op_prec = value;
   } else return -EINVAL;
   return 0;

@@ -184,14 +184,16 @@ std::string igemm_key(const IgemmArgs& a) {
   const Epilogue& e = a.e;
   const int epi = (e.shuffle_co ? 1 : 0) | (e.stats ? 2 : 0) | (e.yref ? 4 : 0) | (e.colsum1 ? 8 : 0) |
                   (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0);
-  snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d", a.bh ? "_bf16" : "", a.M,
+  snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d",
+           a.bl ? "_bf16x3" : a.bh ? "_bf16" : "", a.M,
            a.N, a.K, a.a.Cg, a.a.taps_h, a.a.taps_w, a.a.stride, a.a.Hg, a.a.Wg, epi);
   return b;
 }
 
 std::string wgrad_key(const WgradArgs& a) {
   char b[192];
-  snprintf(b, sizeof b, "wgrad%s Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d", a.bf16 ? "_bf16" : "", a.Mo,
+  snprintf(b, sizeof b, "wgrad%s Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d",
+           a.split ? "_bf16x3" : a.bf16 ? "_bf16" : "", a.Mo,
            a.No, a.P, a.gb.Cg, a.gb.taps_h, a.gb.taps_w, a.gb.stride, a.gb.Hg, a.gb.Wg);
   return b;
 }
@@ -330,18 +332,22 @@ GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
 
 hipError_t run_igemm(const Ctx& c, IgemmArgs a) {
   a.slab = c.f(c.p->slab);
-  if (c.p->prec == UNET_PREC_BF16) {  // B -> its bf16 copy at the same element offset
+  if (c.p->prec != UNET_PREC_FP32) {  // B -> its bf16 copy (and lo plane) at the same element offset
     const char* b = reinterpret_cast<const char*>(a.b);
     const char* base = c.ws + c.p->pack_region.off;
     if (b < base || b >= base + c.p->pack_region.bytes) return hipErrorInvalidValue;
-    a.bh = reinterpret_cast<const uint16_t*>(c.ws + c.p->pack16.off) + (b - base) / sizeof(float);
+    const size_t el = (b - base) / sizeof(float);
+    const uint16_t* hi = reinterpret_cast<const uint16_t*>(c.ws + c.p->pack16.off);
+    a.bh = hi + el;
+    if (c.p->prec == UNET_PREC_BF16X3) a.bl = hi + c.p->pack_region.bytes / 4 + el;
     a.b = nullptr;
   }
   return launch_igemm_v(a, c.s, choose_igemm(c, a));
 }
 
 hipError_t run_wgrad(const Ctx& c, WgradArgs a) {
-  a.bf16 = c.p->prec == UNET_PREC_BF16;
+  a.bf16 = c.p->prec != UNET_PREC_FP32;
+  a.split = c.p->prec == UNET_PREC_BF16X3;
   return launch_wgrad_v(a, c.s, choose_wgrad(c, a));
 }
 
@@ -423,8 +429,11 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       ConvT& T = p->T[k];
       CK(launch_pack_convT(P<float>(prm, T.pw), T.ci, T.co, c.f(T.wf), c.f(T.wd), s));
     }
-    if (p->prec == UNET_PREC_BF16)
-      CK(launch_f2bf(c.f(p->pack_region), reinterpret_cast<uint16_t*>(c.u8(p->pack16)), p->pack_region.bytes / 4, s));
+    if (p->prec != UNET_PREC_FP32) {
+      uint16_t* hi = reinterpret_cast<uint16_t*>(c.u8(p->pack16));
+      const size_t ne = p->pack_region.bytes / 4;
+      CK(launch_f2bf(c.f(p->pack_region), hi, ne, s, p->prec == UNET_PREC_BF16X3 ? hi + ne : nullptr));
+    }
   }
   if (!train) {
     for (int l = 0; l < 18; ++l) {
@@ -727,7 +736,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
 // =========================== C-ABI =======================================
 extern "C" {
 
-const char* unet_version(void) { return "unet_hip 0.2 gfx950 fp32/bf16-mfma"; }
+const char* unet_version(void) { return "unet_hip 0.3 gfx950 fp32/bf16/bf16x3-mfma"; }
 const char* unet_last_error(void) { return g_err.c_str(); }
 
 unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
@@ -741,8 +750,8 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     set_err("unet_plan_create: need n>=1, 1<=c_in<=4, 1<=n_classes<=4");
     return nullptr;
   }
-  if (prec != UNET_PREC_FP32 && prec != UNET_PREC_BF16) {
-    set_err("unet_plan_create_ex: precision must be UNET_PREC_FP32 or UNET_PREC_BF16");
+  if (prec != UNET_PREC_FP32 && prec != UNET_PREC_BF16 && prec != UNET_PREC_BF16X3) {
+    set_err("unet_plan_create_ex: precision must be UNET_PREC_FP32, UNET_PREC_BF16 or UNET_PREC_BF16X3");
     return nullptr;
   }
   auto* p = new unet_plan();
@@ -881,7 +890,8 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     }
     p->pack_region.off = pack_start;
     p->pack_region.bytes = al.top - pack_start;
-    if (prec == UNET_PREC_BF16) p->pack16 = al.take(p->pack_region.bytes / 2);
+    if (prec != UNET_PREC_FP32)  // hi plane (+ lo plane for split operands)
+      p->pack16 = al.take(p->pack_region.bytes / 2 * (prec == UNET_PREC_BF16X3 ? 2 : 1));
   }
   for (int l = 0; l < 18; ++l) {
     Conv& L = p->L[l];

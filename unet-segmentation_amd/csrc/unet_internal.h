@@ -75,6 +75,8 @@ struct IgemmArgs {
   const float* b = nullptr;      // packed B[N][K] (k contiguous), fp32 tiles
   const uint16_t* bh = nullptr;  // the same packed B in bf16, bf16 tiles (A is
                                  // rounded to bf16 when staged)
+  const uint16_t* bl = nullptr;  // split operands (UNET_PREC_BF16X3): B's residual
+                                 // plane bf16(B - bh); A is staged as hi/lo too
   int M, N, K;
   Epilogue e;
   // split-K: > 1 slices the K chunks over blockIdx.z; raw partial tiles go to
@@ -92,6 +94,7 @@ struct WgradArgs {
   int pix_per_split;
   float* out;        // [Mo][No] fp32, accumulated with atomics (zeroed by caller)
   int bf16 = 0;      // 1: operands rounded to bf16 when staged (bf16 tiles 10-14)
+  int split = 0;     // 1 (with bf16): operands as hi/lo bf16 pairs (UNET_PREC_BF16X3)
 };
 
 // ---------------- launchers (kernels.hip) ----------------
@@ -123,8 +126,11 @@ hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid)
 // halo-tiled 3x3 weight gradient (wgrad tiles 20, 21): all 9 taps per workgroup
 bool wgrad3_fits(const WgradArgs& a);
 hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
-// out[i] = bf16(in[i]) (RNE), n a multiple of 4, both 16-B aligned
-hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s);
+// tiles 21-26 / 31-36 / 41-44 that have a split-operand kernel
+bool bf16_tile_splits(int tile);
+// out[i] = bf16(in[i]) (RNE), n a multiple of 4, in 16-B / out 8-B aligned;
+// lo (optional): lo[i] = bf16(in[i] - out[i]), the residual plane of split operands
+hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s, uint16_t* lo = nullptr);
 
 // inc.c0: Ci in {1,2,3,4} direct conv from an NCHW input; y NHWC (Co = 64 multiple).
 hipError_t launch_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w,

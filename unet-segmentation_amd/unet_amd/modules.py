@@ -10,8 +10,9 @@ Mirrors the reference interface:
   (NHWC activations, MFMA implicit GEMM) inside one autograd node.
   GEMM precision: fp32 by default; bf16 operands with fp32 accumulation inside
   ``torch.autocast("cuda", dtype=torch.bfloat16)`` (the reference's convs under
-  autocast) or when ``model.precision = "bf16"``.  Activations, BatchNorm,
-  logits and gradients stay fp32 either way.
+  autocast) or when ``model.precision = "bf16"``; ``"bf16x3"`` = fp32-accurate
+  GEMMs from three bf16 MFMA products per operand pair (hi/lo split).
+  Activations, BatchNorm, logits and gradients stay fp32 in all of them.
 * ``WeightedCrossEntropyLoss()(inputs, targets, weight_maps)`` --
   utils/losses.py:29-57, fused forward+backward kernel.
 
@@ -26,7 +27,7 @@ import torch
 import torch.nn as nn
 
 from . import _lib
-from .plan import Plan
+from .plan import PRECISIONS, Plan
 
 
 def _param_holder_forward(self, *a, **k):
@@ -184,7 +185,7 @@ class UNet(nn.Module):
         self.outc = OutConv(64, n_classes)
         self._runner = _Runner()
         # GEMM precision: None = follow torch.autocast (bf16 inside a cuda
-        # bfloat16 autocast region, else fp32); "fp32" / "bf16" force it
+        # bfloat16 autocast region, else fp32); "fp32" / "bf16" / "bf16x3" force it
         self.precision = None
 
     # reference helper (models/unet_model.py:88-102), kept for API parity
@@ -207,10 +208,10 @@ class UNet(nn.Module):
         return _UNetFunction.apply(x, self, bool(self.training), self.gemm_precision(), *params)
 
     def gemm_precision(self):
-        """GEMM precision the next forward uses ("fp32" or "bf16")."""
+        """GEMM precision the next forward uses ("fp32", "bf16" or "bf16x3")."""
         if self.precision is not None:
-            if self.precision not in ("fp32", "bf16"):
-                raise ValueError(f"precision must be None, 'fp32' or 'bf16', got {self.precision!r}")
+            if self.precision not in PRECISIONS:
+                raise ValueError(f"precision must be None or one of {sorted(PRECISIONS)}, got {self.precision!r}")
             return self.precision
         if torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16:
             return "bf16"

@@ -8,14 +8,15 @@ from . import _lib
 N_PARAMS = 136   # state_dict entries (parameters + BN buffers)
 N_GRADS = 82     # named_parameters
 N_SEGMENTS = 9   # backward segments: head+up4, up3, up2, up1, down4, down3, down2, down1, inc
-# GEMM arithmetic (include/unet_hip.h UNET_PREC_*): fp32 operands, or bf16
-# operands with fp32 accumulation (configs C3/C5, torch.autocast(bfloat16))
-PRECISIONS = {"fp32": 0, "bf16": 1}
+# GEMM arithmetic (include/unet_hip.h UNET_PREC_*): fp32 operands; bf16
+# operands with fp32 accumulation (configs C3/C5, torch.autocast(bfloat16));
+# fp32-accurate split operands on the bf16 MFMA (hi*hi + hi*lo + lo*hi)
+PRECISIONS = {"fp32": 0, "bf16": 1, "bf16x3": 2}
 
 
 class Plan:
     """One compiled schedule for input shape (n, c, h, w), n_classes and GEMM
-    precision ("fp32" or "bf16")."""
+    precision ("fp32", "bf16" or "bf16x3")."""
 
     def __init__(self, n, c, h, w, n_classes, precision="fp32"):
         if precision not in PRECISIONS:

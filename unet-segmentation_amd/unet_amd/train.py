@@ -10,7 +10,9 @@ SGD(lr, momentum=0.99).step() -- with the same arithmetic as the drop-in
 * one persistent plan workspace (no per-step allocation);
 * the optimizer is one fused kernel over the flat buffer;
 * ``precision="bf16"`` runs the convolution GEMMs on bf16 operands with fp32
-  accumulation (configs C3/C5); weights, gradients and the optimizer stay fp32;
+  accumulation (configs C3/C5); ``"bf16x3"`` runs them fp32-accurate on the
+  bf16 matrix cores (operands split into bf16 hi/lo pairs, three products);
+  weights, gradients and the optimizer stay fp32 in every mode;
 * with a process group, the backward runs in 9 segments and each segment's
   gradient bucket is all-reduced (RCCL over xGMI) while later segments compute.
 """
