@@ -56,9 +56,23 @@ def ck(rc):
     _lib.check(rc, "op")
 
 
+@pytest.fixture
+def variant(request, lib):
+    """Forced igemm tile for the per-op entry points (-1 = built-in choice;
+    51-54 = the fp32 halo-tiled k_conv3_f32: 8x32, 16x16, 8x32 with 4 waves, 8x16)."""
+    lib.unet_set_tuning(b"igemm_variant", request.param)
+    yield request.param
+    lib.unet_set_tuning(b"igemm_variant", -1)
+
+
+HALO32 = [-1, 51, 52, 53, 54]
+
+
+@pytest.mark.parametrize("variant", HALO32, indirect=True)
 @pytest.mark.parametrize("n,h,w,ci,co,tf", [(2, 14, 13, 64, 128, False), (2, 11, 17, 64, 64, True),
-                                              (1, 30, 29, 128, 256, True), (3, 7, 9, 32, 64, False)])
-def test_conv3x3_fwd(lib, n, h, w, ci, co, tf):
+                                              (1, 30, 29, 128, 256, True), (3, 7, 9, 32, 64, False),
+                                              (1, 37, 70, 16, 64, True)])
+def test_conv3x3_fwd(lib, n, h, w, ci, co, tf, variant):
     rng = np.random.default_rng(0)
     x = rng.standard_normal((n, h, w, ci))
     wt = rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci)
@@ -76,8 +90,9 @@ def test_conv3x3_fwd(lib, n, h, w, ci, co, tf):
     assert rel_err(host(y), ref) < 2e-5
 
 
+@pytest.mark.parametrize("variant", HALO32, indirect=True)
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 9, 14, 128, 64), (2, 8, 8, 64, 256)])
-def test_conv3x3_dgrad(lib, n, h, w, ci, co):
+def test_conv3x3_dgrad(lib, n, h, w, ci, co, variant):
     rng = np.random.default_rng(1)
     x = rng.standard_normal((n, h, w, ci))
     wt = rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci)

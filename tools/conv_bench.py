@@ -36,11 +36,12 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--dgrad", action="store_true")
-    ap.add_argument("--prec", type=int, default=1, help="1 = bf16 operands, 2 = bf16x3 split operands")
+    ap.add_argument("--prec", type=int, default=1, help="0 = fp32, 1 = bf16 operands, 2 = bf16x3 split operands")
     args = ap.parse_args()
     lib = _lib.load()
     lib.unet_set_tuning(b"op_precision", args.prec)
-    variants = VARIANTS if args.prec == 1 else [-1, 21, 22, 23, 24, 25, 26, 31, 33, 35]
+    variants = {0: [-1, 1, 2, 3, 4, 8, 11, 12, 13, 14, 51, 52, 53, 54], 1: VARIANTS,
+                2: [-1, 21, 22, 23, 24, 25, 26, 31, 33, 35]}[args.prec]
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for name, n, h, w, ci, co in SHAPES:
         g = torch.Generator(device="cuda").manual_seed(0)

@@ -449,6 +449,172 @@ constexpr size_t igemm_g_smem(int cg) {
 }
 
 // ---------------------------------------------------------------------------
+// k_conv3_f32: halo-tiled 3x3 stride-1 implicit GEMM in fp32 (conv forward and
+// conv input gradient), the fp32 twin of k_conv3_bf (igemm_bf16.hip).  A
+// workgroup owns a TH x TW tile of one image's output grid and BN output
+// columns; per 16-channel chunk it stages the (TH+2) x (TW+2) input halo once
+// (consumer BN+ReLU applied) and the chunk's weights for all 9 taps, and each
+// tap reads a shifted window of the same halo.  Against k_igemm's pixel-row
+// gather (one barrier and one staging pass per 16-k step, A fetched once per
+// tap) a chunk carries 9 taps x 8 MFMA k-steps between its two barriers.
+// LDS rows: 16 floats + 4 pad (80 B, ds_read_b128 conflict-free); fragment
+// k-order as k_igemm (lane half h holds k = 8h .. 8h+7, MFMA s pairs k = s and
+// 8 + s in both operands).  BN scale/shift are read per staged unit from global
+// (L1/L2 hits), so the LDS holds only the operands: 8x32 x BN64 = 73 KiB, two
+// workgroups per CU.
+// ---------------------------------------------------------------------------
+template <int TH, int TW, int BN>
+constexpr size_t conv3_f32_smem() {
+  return (size_t)((TH + 2) * (TW + 2) + 9 * BN) * 20 * 4;
+}
+
+template <int TH, int TW, int BN, int WM, int WN, int MINW>
+__global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_f32(const IgemmArgs args) {
+  constexpr int NT = WM * WN * 64, BM = TH * TW, LDR = 20;
+  constexpr int HW2 = TW + 2, PH = (TH + 2) * HW2;
+  constexpr int FM = BM / 32, TM = FM / WM, TN = BN / (WN * 32);
+  constexpr int UA = PH * 4, UB = 9 * BN * 4;  // 16-B staging units (4 channels / 4 k each)
+  constexpr int NA = (UA + NT - 1) / NT, NB = (UB + NT - 1) / NT;
+  constexpr int A_EL = PH * LDR;
+  static_assert(BM % 32 == 0 && FM % WM == 0 && TM >= 1 && TN >= 1, "tile");
+  static_assert(WM * 3 * BN <= A_EL, "epilogue reduction must fit the halo buffer");
+  extern __shared__ __attribute__((aligned(16))) float hsm[];
+  float* As = hsm;
+  float* Bs = hsm + A_EL;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const Gather& g = args.a;
+  const int Cg = g.Cg, K = args.K, Hg = g.Hg, Wg = g.Wg;
+  const int tiles_x = (Wg + TW - 1) / TW, tiles_y = (Hg + TH - 1) / TH;
+  int t = blockIdx.x;
+  const int x0 = (t % tiles_x) * TW;
+  t /= tiles_x;
+  const int y0 = (t % tiles_y) * TH;
+  const int n = t / tiles_y;
+  const int n0 = blockIdx.y * BN;
+
+  // staging units: A = (halo pixel, 4-channel piece), B = (tap, row, 4-k piece)
+  int pi0[NA], pi1[NA];
+#pragma unroll
+  for (int k = 0; k < NA; ++k) {
+    const int u = min(tid + k * NT, UA - 1);
+    const int ph = u >> 2;
+    const int hy = ph / HW2, hx = ph - hy * HW2;
+    const int yy = min(y0 + hy, Hg + 1), xx = min(x0 + hx, Wg + 1);  // overhang: any in-range pixel
+    pi0[k] = (n * g.s[0].H + yy + g.s[0].oy) * g.s[0].W + xx + g.s[0].ox;
+    pi1[k] = (n * g.s[1].H + yy + g.s[1].oy) * g.s[1].W + xx + g.s[1].ox;
+  }
+  int bsrc[NB];  // element offsets into args.b
+#pragma unroll
+  for (int k = 0; k < NB; ++k) {
+    const int u = min(tid + k * NT, UB - 1);
+    const int r = (u >> 2) % BN, tap = (u >> 2) / BN;
+    bsrc[k] = (n0 + r) * K + tap * Cg + (u & 3) * 4;
+  }
+
+  const int nk_all = Cg / 16;
+  int kc0 = 0, kc1 = nk_all;
+  if (args.ksplit > 1) {
+    const int per = (nk_all + args.ksplit - 1) / args.ksplit;
+    kc0 = blockIdx.z * per;
+    kc1 = min(nk_all, kc0 + per);
+  }
+
+  float4 ra[NA], rb[NB], sc, sh;
+  bool tf = false;
+  auto issue = [&](int kc) {
+    const int c0 = kc * 16;
+    const bool second = c0 >= g.c_split;
+    const Src s = pick_src(g, second);
+    const int cl = (second ? c0 - g.c_split : c0) + (tid & 3) * 4;
+#pragma unroll
+    for (int k = 0; k < NA; ++k)
+      if (tid + k * NT < UA) ra[k] = ld4(s.ptr + (size_t)(second ? pi1[k] : pi0[k]) * s.C + cl);
+#pragma unroll
+    for (int k = 0; k < NB; ++k)
+      if (tid + k * NT < UB) rb[k] = ld4(args.b + bsrc[k] + c0);
+    tf = s.scale != nullptr;
+    if (tf) {  // the unit's 4 channels are the same for every A unit of this lane
+      sc = ld4(s.scale + cl);
+      sh = ld4(s.shift + cl);
+    }
+  };
+  auto commit = [&] {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      if (u < UA) st4(As + (u >> 2) * LDR + (u & 3) * 4, tf ? affine_relu4(ra[k], sc, sh) : ra[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int u = tid + k * NT;
+      if (u < UB) st4(Bs + (u >> 2) * LDR + (u & 3) * 4, rb[k]);
+    }
+  };
+
+  floatx16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int h = lane >> 5, li = lane & 31;
+  int abase[TM];
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int p = (wm * TM + i) * 32 + li;
+    abase[i] = (p / TW) * HW2 + p % TW;
+  }
+  auto compute = [&] {
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int off = (tap / 3) * HW2 + tap % 3;
+      float4 fa[TM][2], fb[TN][2];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const float* p = As + (abase[i] + off) * LDR + 8 * h;
+        fa[i][0] = ld4(p);
+        fa[i][1] = ld4(p + 4);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const float* p = Bs + (tap * BN + wn * TN * 32 + j * 32 + li) * LDR + 8 * h;
+        fb[j][0] = ld4(p);
+        fb[j][1] = ld4(p + 4);
+      }
+#pragma unroll
+      for (int s = 0; s < 8; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(getc(fa[i][s >> 2], s & 3), getc(fb[j][s >> 2], s & 3),
+                                                             acc[i][j], 0, 0, 0);
+    }
+  };
+
+  if (kc0 < kc1) {
+    issue(kc0);
+    commit();
+  }
+  __syncthreads();
+  for (int kc = kc0; kc < kc1; ++kc) {
+    const bool more = kc + 1 < kc1;
+    if (more) issue(kc + 1);
+    compute();
+    __syncthreads();
+    if (more) {
+      commit();
+      __syncthreads();
+    }
+  }
+  igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, hsm, HaloRows<TW>{n, y0, x0, Hg, Wg});
+}
+
+// ---------------------------------------------------------------------------
 // k_splitk_epi: out = sum_z slab[z] + the k_igemm epilogue (bias, pixel-shuffle
 // or cropped destination, ReLU-mask + BN-bwd stats, BN stats, concat colsum).
 // 256 threads = 16 column quads x 16 row lanes over a 128-row x 64-column
@@ -757,12 +923,18 @@ static TileInfo tile_info(int id) {
     case 35: return {128, 64, 288, 2};
     case 36: return {256, 128, 288, 1};
     case 41: case 42: case 43: case 44: return {256, 64, 288, 1};  // persistent k_conv3p_bf
+    // fp32 halo-tiled 3x3 (k_conv3_f32): bk = one 16-channel chunk x 9 taps
+    case 51: return {256, 64, 144, 2};
+    case 52: return {256, 64, 144, 2};
+    case 53: return {256, 64, 144, 2};
+    case 54: return {128, 64, 144, 2};
     default: return {0, 0, 0, 0};
   }
 }
 
 static bool is_halo_tile(int tile) { return (tile >= 31 && tile <= 36) || (tile >= 41 && tile <= 44); }
 static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_halo_tile(tile); }
+static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 
 // A tile applies when the shape divides and the packed B operand is in the
 // tile's precision (fp32 `b` for tiles 1-14, bf16 `bh` for 21-26).
@@ -773,6 +945,9 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   if (is_halo_tile(tile))  // 3x3 stride-1 gathers only (conv fwd / dgrad), K = 9 x Cg
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
+  if (is_halo32_tile(tile))
+    return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
+           a.K == 9 * a.a.Cg && a.a.Cg % 16 == 0 && a.a.c_split % 16 == 0;
   return t.bm > 0 && prec_ok && a.N % t.bn == 0 && a.K % t.bk == 0 && a.a.Cg % t.bk == 0 &&
          a.a.c_split % t.bk == 0;
 }
@@ -816,6 +991,25 @@ static hipError_t go_igemm_g(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+template <int TH, int TW, int BN, int WM, int WN, int MINW>
+static hipError_t go_halo32(const IgemmArgs& a, hipStream_t s) {
+  if (a.b == nullptr || a.N % BN != 0 || a.a.Cg % 16 != 0 || a.a.c_split % 16 != 0 || a.a.taps_h != 3 ||
+      a.a.taps_w != 3 || a.a.stride != 1 || a.K != 9 * a.a.Cg)
+    return hipErrorInvalidValue;
+  constexpr size_t smem = conv3_f32_smem<TH, TW, BN>();
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_conv3_f32<TH, TW, BN, WM, WN, MINW>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const long long tiles = (long long)a.a.nimg * ((a.a.Hg + TH - 1) / TH) * ((a.a.Wg + TW - 1) / TW);
+  dim3 grid((unsigned)tiles, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
+  hipLaunchKernelGGL((k_conv3_f32<TH, TW, BN, WM, WN, MINW>), grid, dim3(WM * WN * 64), smem, s, a);
+  return hipGetLastError();
+}
+
 static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
   switch (tile) {
     case 1: return go_igemm<128, 128, 2, 2, 16>(a, s);
@@ -833,6 +1027,10 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 21: case 22: case 23: case 24: case 25: case 26:
     case 31: case 32: case 33: case 34: case 35: case 36:
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
+    case 51: return go_halo32<8, 32, 64, 8, 1, 4>(a, s);
+    case 52: return go_halo32<16, 16, 64, 8, 1, 4>(a, s);
+    case 53: return go_halo32<8, 32, 64, 4, 1, 2>(a, s);
+    case 54: return go_halo32<8, 16, 64, 4, 1, 2>(a, s);
     default: return hipErrorInvalidValue;
   }
 }

@@ -1293,6 +1293,10 @@ bool halo_tile_shape(int tile, int& th, int& tw, int& bn) {
     case 36: th = 8; tw = 32; bn = 128; return true;
     case 41: case 43: th = 8; tw = 32; bn = 64; return true;
     case 42: case 44: th = 16; tw = 16; bn = 64; return true;
+    // fp32 k_conv3_f32 (igemm.hip)
+    case 51: case 53: th = 8; tw = 32; bn = 64; return true;
+    case 52: th = 16; tw = 16; bn = 64; return true;
+    case 54: th = 8; tw = 16; bn = 64; return true;
     default: return false;
   }
 }
