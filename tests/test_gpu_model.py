@@ -97,7 +97,10 @@ def gemm_mode(request):
             lib.unet_set_tuning(b"force_split", int(part[5:]))
         elif part.startswith("tile"):
             lib.unet_set_tuning(b"force_tile", int(part[4:]))
+        elif part.startswith("wgrad"):
+            lib.unet_set_tuning(b"wgrad_variant", int(part[5:]))
     yield mode
+    lib.unet_set_tuning(b"wgrad_variant", -1)
     lib.unet_set_tuning(b"autotune", 1)
     lib.unet_set_tuning(b"force_split", 0)
     lib.unet_set_tuning(b"force_tile", 0)
@@ -106,7 +109,8 @@ def gemm_mode(request):
 
 @pytest.mark.parametrize("gemm_mode", ["heuristic", "split3", "split8", "tile11", "tile12", "tile13", "tile14",
                                        "tile12+split4", "tile14+split3", "tile3", "tile6", "tile51", "tile52",
-                                       "tile53", "tile54", "tile51+split3"], indirect=True)
+                                       "tile53", "tile54", "tile51+split3", "heuristic+wgrad22",
+                                       "heuristic+wgrad23"], indirect=True)
 def test_train_step_gemm_variants_vs_oracle(gemm_mode):
     """Built-in tiles, the LDS-DMA staged tiles (11-14), the fp32 halo-tiled 3x3
     tiles (51-54; convT GEMMs fall back to the built-in tile) and split-K

@@ -106,8 +106,20 @@ def test_conv3x3_dgrad(lib, n, h, w, ci, co, variant):
     assert rel_err(host(dx), ref) < 2e-5
 
 
-@pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 40, 37, 128, 128), (2, 10, 9, 64, 128)])
-def test_conv3x3_wgrad(lib, n, h, w, ci, co):
+@pytest.fixture
+def wvariant(request, lib):
+    """Forced weight-gradient tile (-1 = built-in; 22 / 23 = the fp32 halo-tiled
+    all-taps k_wgrad3_f32, 8x16 / 4x32 pixel tiles)."""
+    lib.unet_set_tuning(b"wgrad_variant", request.param)
+    yield request.param
+    lib.unet_set_tuning(b"wgrad_variant", -1)
+
+
+@pytest.mark.parametrize("wvariant", [-1, 22, 23], indirect=True)
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 40, 37, 128, 128), (2, 10, 9, 64, 128),
+                                         (1, 7, 5, 64, 64), (2, 21, 44, 192, 128)])
+def test_conv3x3_wgrad(lib, n, h, w, ci, co, wvariant):
+    """Ragged pixel counts and grids that are not multiples of the halo tiles."""
     rng = np.random.default_rng(2)
     x = rng.standard_normal((n, h, w, ci))
     wt = rng.standard_normal((co, ci, 3, 3))

@@ -36,12 +36,17 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--dgrad", action="store_true")
+    ap.add_argument("--wgrad", action="store_true", help="time the weight gradient over wgrad variants")
     ap.add_argument("--prec", type=int, default=1, help="0 = fp32, 1 = bf16 operands, 2 = bf16x3 split operands")
     args = ap.parse_args()
     lib = _lib.load()
     lib.unet_set_tuning(b"op_precision", args.prec)
     variants = {0: [-1, 1, 2, 3, 4, 8, 11, 12, 13, 14, 51, 52, 53, 54], 1: VARIANTS,
                 2: [-1, 21, 22, 23, 24, 25, 26, 31, 33, 35]}[args.prec]
+    knob = b"igemm_variant"
+    if args.wgrad:  # -1 built-in; fp32 22/23 halo; bf16 / bf16x3 10-14 pixel-column, 20/21 halo
+        knob = b"wgrad_variant"
+        variants = [-1, 1, 22, 23] if args.prec == 0 else [-1, 10, 12, 13, 20, 21]
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for name, n, h, w, ci, co in SHAPES:
         g = torch.Generator(device="cuda").manual_seed(0)
@@ -56,8 +61,14 @@ def main():
         ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
         flops = 2.0 * n * (h - 2) * (w - 2) * ci * co * 9
 
+        dw = torch.empty((co, ci, 3, 3), device="cuda")
+        db = torch.empty(co, device="cuda")
+
         def run():
-            if args.dgrad:
+            if args.wgrad:
+                rc = lib.unet_conv3x3_wgrad(x.data_ptr(), dy.data_ptr(), n, h, w, ci, co, dw.data_ptr(),
+                                            db.data_ptr(), ws.data_ptr(), st)
+            elif args.dgrad:
                 rc = lib.unet_conv3x3_dgrad(dy.data_ptr(), n, h, w, ci, wt.data_ptr(), co, dx.data_ptr(),
                                             ws.data_ptr(), st)
             else:
@@ -68,27 +79,28 @@ def main():
         times = {v: [] for v in variants}
         ok = {}
         for v in variants:
-            lib.unet_set_tuning(b"igemm_variant", v)
+            lib.unet_set_tuning(knob, v)
             ok[v] = run() == 0
         torch.cuda.synchronize()
         for _ in range(args.reps):
             for v in variants:
                 if not ok[v]:
                     continue
-                lib.unet_set_tuning(b"igemm_variant", v)
+                lib.unet_set_tuning(knob, v)
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 run()
                 e1.record()
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) * 1e3)
-        line = f"{name:9s} {'dgrad' if args.dgrad else 'fwd':5s}"
+        line = f"{name:9s} {'wgrad' if args.wgrad else 'dgrad' if args.dgrad else 'fwd':5s}"
         for v in variants:
             if ok[v]:
                 t = sorted(times[v])[len(times[v]) // 2]
                 line += f" | {v}:{t:7.1f}us {flops / t / 1e6:6.1f}TF"
         print(line, flush=True)
     lib.unet_set_tuning(b"igemm_variant", -1)
+    lib.unet_set_tuning(b"wgrad_variant", -1)
     lib.unet_set_tuning(b"op_precision", 0)
 
 

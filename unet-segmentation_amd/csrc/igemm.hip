@@ -615,6 +615,187 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_f32(const IgemmArg
 }
 
 // ---------------------------------------------------------------------------
+// k_wgrad3_f32: halo-tiled weight gradient of a 3x3 stride-1 conv in fp32, the
+// fp32 twin of k_wgrad3_bf.  dW[co][tap][ci] = sum_p dY[p][co] * X[p + tap][ci]
+// for a 64 (co) x 64 (ci) block and all 9 taps per workgroup, walking TH x TW
+// output-pixel tiles strided over blockIdx.z; per tile the dY tile and the
+// (TH+2) x (TW+2) X halo are staged once (X with the consumer BN+ReLU) and every
+// tap reads a shifted pixel window of the halo.  The MFMA k is the pixel: in
+// v_mfma_f32_32x32x2_f32 lane half h holds pixel 2s + h of k-step s, so each
+// operand is one ds_read_b32 per lane from the natural [pixel][64 ch] image
+// (256-B rows).  Rows of odd pixels store their two 32-channel halves swapped,
+// so the two lane halves (adjacent pixels) always sit in opposite bank halves:
+// conflict-free for every tap shift.  LDS (8x16 tile): (128 + 180) x 256 B =
+// 77 KiB, two workgroups per CU.  Waves (8): co tile w & 1, ci tile (w >> 1) & 1,
+// tap group w >> 2 (taps 0-4 / 5-8), one accumulator per tap.
+// ---------------------------------------------------------------------------
+template <int TH, int TW>
+constexpr size_t wgrad3_f32_smem() {
+  return (size_t)(TH * TW + (TH + 2) * (TW + 2)) * 256 + 2 * 64 * 4;
+}
+__device__ __forceinline__ int w3f_idx(int p, int c) { return p * 64 + (c ^ ((p & 1) << 5)); }
+
+template <int TH, int TW>
+__global__ __launch_bounds__(512, 2) void k_wgrad3_f32(const WgradArgs args) {
+  constexpr int NT = 512, BC = 64, NTAP = 5;
+  constexpr int PT = TH * TW, HW2 = TW + 2, PH = (TH + 2) * HW2;
+  constexpr int UA = PT * 16, UB = PH * 16;  // 16-B units: (pixel, 4-channel piece)
+  constexpr int NA = (UA + NT - 1) / NT, NB = (UB + NT - 1) / NT;
+  static_assert(TW % 2 == 0 && UA % NT == 0 && NA <= 32, "a k-step's pixel pair stays inside one tile row");
+  extern __shared__ __attribute__((aligned(16))) float wsf[];
+  float* Ad = wsf;                   // dY tile [PT][64]
+  float* Bx = wsf + PT * 64;         // X halo [PH][64]
+  float* ssc = wsf + (PT + PH) * 64;  // [2][64]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const Gather& gb = args.gb;
+  const Src& ds = args.ga.s[0];
+  const int i0 = blockIdx.x * 64;  // co block
+  const int cb = blockIdx.y * BC;  // ci block (gather channel index)
+  const int Hg = gb.Hg, Wg = gb.Wg, Ci = gb.Cg;
+  const bool second = cb >= gb.c_split;  // a 64-channel block never straddles the concat split
+  const Src xs = pick_src(gb, second);
+  const int xc = second ? cb - gb.c_split : cb;
+  const bool xtf = xs.scale != nullptr;
+  if (xtf) {
+    for (int c = tid; c < BC; c += NT) {
+      ssc[c] = xs.scale[xc + c];
+      ssc[BC + c] = xs.shift[xc + c];
+    }
+  }
+  const int tiles_x = (Wg + TW - 1) / TW, tiles_y = (Hg + TH - 1) / TH;
+  const int tiles = gb.nimg * tiles_x * tiles_y;
+
+  float4 rd[NA], rx[NB];
+  unsigned dvalid = 0;
+  auto issue = [&](int t) {
+    const int x0 = (t % tiles_x) * TW;
+    const int r = t / tiles_x;
+    const int y0 = (r % tiles_y) * TH, n = r / tiles_y;
+    dvalid = 0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      const int p = u >> 4, ch = u & 15;
+      const int y = y0 + p / TW, x = x0 + p % TW;
+      dvalid |= (y < Hg && x < Wg) ? (1u << k) : 0u;
+      const int yy = min(y, Hg - 1), xx = min(x, Wg - 1);
+      rd[k] = ld4(ds.ptr + (size_t)((n * ds.H + yy + ds.oy) * ds.W + xx + ds.ox) * ds.C + i0 + ch * 4);
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int u = min(tid + k * NT, UB - 1);
+      const int hp = u >> 4, ch = u & 15;
+      const int yy = min(y0 + hp / HW2, Hg + 1), xx = min(x0 + hp % HW2, Wg + 1);
+      rx[k] = ld4(xs.ptr + (size_t)((n * xs.H + yy + xs.oy) * xs.W + xx + xs.ox) * xs.C + xc + ch * 4);
+    }
+  };
+  auto commit = [&] {
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      const int p = u >> 4, ch = u & 15;
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      st4(Ad + w3f_idx(p, ch * 4), (dvalid >> k) & 1 ? rd[k] : z);  // pixels past the grid add nothing
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int u = tid + k * NT;
+      if (u < UB) {
+        const int hp = u >> 4, ch = u & 15;
+        float4 v = rx[k];
+        if (xtf) v = affine_relu4(v, ld4(ssc + ch * 4), ld4(ssc + BC + ch * 4));
+        st4(Bx + w3f_idx(hp, ch * 4), v);
+      }
+    }
+  };
+
+  floatx16 acc[NTAP];
+#pragma unroll
+  for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[t][r] = 0.f;
+
+  const int h = lane >> 5, li = lane & 31;
+  const int ct = wave & 1, it_ = (wave >> 1) & 1, tap0 = (wave >> 2) * NTAP;
+  const int ntap = wave >> 2 ? 9 - NTAP : NTAP;  // wave-uniform
+  const int ca = ct * 32 + li, cbb = it_ * 32 + li;
+  auto compute = [&] {
+#pragma unroll 4
+    for (int ks = 0; ks < PT / 2; ++ks) {
+      const int p = 2 * ks + h;  // this lane's pixel (k)
+      const int prow = p / TW, px = p % TW;
+      const float a = Ad[w3f_idx(p, ca)];
+#pragma unroll
+      for (int j = 0; j < NTAP; ++j) {
+        if (j < ntap) {
+          const int tap = tap0 + j;
+          const int hb = (prow + tap / 3) * HW2 + px + tap % 3;
+          acc[j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, Bx[w3f_idx(hb, cbb)], acc[j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  if (xtf) __syncthreads();  // scale/shift table before the first commit
+  int t = blockIdx.z;
+  if (t < tiles) {
+    issue(t);
+    commit();
+  }
+  __syncthreads();
+  for (; t < tiles; t += gridDim.z) {
+    const bool more = t + (int)gridDim.z < tiles;
+    if (more) issue(t + gridDim.z);
+    compute();
+    __syncthreads();
+    if (more) {
+      commit();
+      __syncthreads();
+    }
+  }
+  // accumulate into out[co][tap * Ci + ci] (fp32 atomics, one per element per workgroup)
+#pragma unroll
+  for (int j = 0; j < NTAP; ++j) {
+    if (j < ntap) {
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int row = i0 + ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+        const int col = (tap0 + j) * Ci + cb + it_ * 32 + li;
+        atomicAdd(args.out + (size_t)row * args.No + col, acc[j][r]);
+      }
+    }
+  }
+}
+
+static bool wgrad3_f32_fits(const WgradArgs& a) {
+  const Gather& g = a.gb;
+  return !a.bf16 && g.taps_h == 3 && g.taps_w == 3 && g.stride == 1 && a.No == 9 * g.Cg && a.Mo % 64 == 0 &&
+         g.Cg % 64 == 0 && (g.c_split % 64 == 0 || g.c_split >= g.Cg) && a.ga.Cg == a.Mo && a.ga.taps_h == 1 &&
+         a.ga.taps_w == 1 && g.Hg == a.ga.Hg && g.Wg == a.ga.Wg && g.nimg == a.ga.nimg && a.ga.s[0].h16 == 0 &&
+         g.s[0].h16 == 0 && g.s[1].h16 == 0;
+}
+
+template <int TH, int TW>
+static hipError_t go_wgrad3_f32(const WgradArgs& a, hipStream_t s, int per_cu) {
+  constexpr size_t smem = wgrad3_f32_smem<TH, TW>();
+  static bool attr = false;
+  if (!attr) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_wgrad3_f32<TH, TW>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    if (e != hipSuccess) return e;
+    attr = true;
+  }
+  const int tiles = a.gb.nimg * ((a.gb.Hg + TH - 1) / TH) * ((a.gb.Wg + TW - 1) / TW);
+  const int blocks = (a.Mo / 64) * (a.gb.Cg / 64);
+  int splits = (per_cu * num_cus() + blocks - 1) / blocks;
+  splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
+  dim3 grid(a.Mo / 64, a.gb.Cg / 64, splits);
+  hipLaunchKernelGGL((k_wgrad3_f32<TH, TW>), grid, dim3(512), smem, s, a);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // k_splitk_epi: out = sum_z slab[z] + the k_igemm epilogue (bias, pixel-shuffle
 // or cropped destination, ReLU-mask + BN-bwd stats, BN stats, concat colsum).
 // 256 threads = 16 column quads x 16 row lanes over a 128-row x 64-column
@@ -1106,6 +1287,7 @@ static void wgrad_tile(int id, int& bm, int& bn) {
 }
 bool wgrad_tile_fits(const WgradArgs& a, int tile) {
   if (tile == 20 || tile == 21) return wgrad3_fits(a);  // halo-tiled 3x3, all taps
+  if (tile == 22 || tile == 23) return wgrad3_f32_fits(a);  // fp32 twin
   int bm, bn;
   wgrad_tile(tile, bm, bn);
   return bm > 0 && (tile >= 10) == (a.bf16 != 0) && a.Mo % bm == 0 && a.No % bn == 0;
@@ -1123,7 +1305,9 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     else if (a.No % 128 == 0) tile = 12;
     else tile = 13;
   } else if (tile < 0) {
-    if (g_tune_wgrad == 1) tile = 4;  // force the small tile (A/B tests)
+    if ((g_tune_wgrad == 22 || g_tune_wgrad == 23) && wgrad_tile_fits(a, g_tune_wgrad))
+      tile = g_tune_wgrad;  // forced fp32 halo tile (tests)
+    else if (g_tune_wgrad == 1) tile = 4;  // force the small tile (A/B tests)
     else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 0;
     else if (a.Mo % 128 == 0 && a.No % 192 == 0) tile = 1;
     else if (a.No % 192 == 0) tile = 2;
@@ -1132,6 +1316,8 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   }
   if (!wgrad_tile_fits(a, tile)) return hipErrorInvalidValue;
   if (tile == 20 || tile == 21) return go_wgrad3_bf16(a, s, tile, c.split > 0 ? c.split : 4);
+  if (tile == 22) return go_wgrad3_f32<8, 16>(a, s, c.split > 0 ? c.split : 4);
+  if (tile == 23) return go_wgrad3_f32<4, 32>(a, s, c.split > 0 ? c.split : 4);
   int bm, bn;
   wgrad_tile(tile, bm, bn);
   const int tiles = (a.Mo / bm) * (a.No / bn);

@@ -218,7 +218,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
 
 std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   std::vector<GemmChoice> v;
-  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21}) {  // fits() filters by precision
+  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23}) {  // fits() filters by precision
     if (!wgrad_tile_fits(a, t)) continue;
     if (t >= 20) {  // halo-tiled: workgroups per CU (2 resident)
       for (int per_cu : {2, 4, 8}) v.push_back({t, per_cu});
