@@ -314,7 +314,9 @@ constexpr size_t conv3_bf_smem(int cg) {
   return (size_t)((TH + 2) * (TW + 2) + 9 * BN) * kBfLdr * 2 * (SPLIT ? 2 : 1) + (size_t)2 * cg * 4;
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int MINW, int SPLIT>
+// A16: every A source is stored bf16 (the usual case in a bf16 plan): no fp32
+// staging registers, no per-source storage branch.
+template <int TH, int TW, int BN, int WM, int WN, int MINW, int SPLIT, int A16>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs args) {
   constexpr int NT = WM * WN * 64, BM = TH * TW, LDR = kBfLdr;
   constexpr int HW2 = TW + 2, PH = (TH + 2) * HW2;  // halo pixels
@@ -381,7 +383,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     kc1 = min(nk_all, kc0 + per);
   }
 
-  float4 ra0[NA], ra1[NA];  // two 1-D arrays: a [N][2] array of vectors is not promoted to registers
+  float4 ra0[NA], ra1[A16 ? 1 : NA];  // two 1-D arrays: a [N][2] array of vectors is not promoted to registers
   u32x4 rb[NB], rbl[SPLIT ? NB : 1];
   auto issue = [&](int kc) {
     const int c0 = kc * 32;
@@ -392,9 +394,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     for (int k = 0; k < NA; ++k) {
       if (tid + k * NT < UA) {
         const size_t e = (size_t)(second ? pi1[k] : pi0[k]) * s.C + cl;
-        if (s.h16) {  // stored bf16: staged as is
+        if (A16 || s.h16) {  // stored bf16: staged as is
           ra0[k] = __builtin_bit_cast(float4, *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(s.ptr) + e));
-        } else {
+        } else if constexpr (!A16) {
           ra0[k] = ld4(s.ptr + e);
           ra1[k] = ld4(s.ptr + e + 4);
         }
@@ -410,7 +412,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
   auto commit = [&](int kc) {
     const int c = kc * 32 + (tid & 3) * 8;
     const Src sc_src = pick_src(g, c >= g.c_split);
-    const bool tf = sc_src.scale != nullptr, h16 = sc_src.h16 != 0;
+    const bool tf = sc_src.scale != nullptr, h16 = A16 || sc_src.h16 != 0;
     float4 sc0, sc1, sh0, sh1;
     if (tf) {
       sc0 = ld4(ssc + c);
@@ -423,12 +425,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
       const int u = tid + k * NT;
       if (u < UA) {
         unsigned short* d = As + (u >> 2) * LDR + (u & 3) * 8;
+        const float4 r1 = ra1[A16 ? 0 : k];
         if constexpr (SPLIT) {
           uint4 lo;
-          *reinterpret_cast<uint4*>(d) = stage8x(ra0[k], ra1[k], h16, tf, sc0, sc1, sh0, sh1, lo);
+          *reinterpret_cast<uint4*>(d) = stage8x(ra0[k], r1, h16, tf, sc0, sc1, sh0, sh1, lo);
           *reinterpret_cast<uint4*>(d + PLANE) = lo;
         } else {
-          *reinterpret_cast<uint4*>(d) = stage8(ra0[k], ra1[k], h16, tf, sc0, sc1, sh0, sh1);
+          *reinterpret_cast<uint4*>(d) = stage8(ra0[k], r1, h16, tf, sc0, sc1, sh0, sh1);
         }
       }
     }
@@ -1234,16 +1237,16 @@ static hipError_t go_bf(const IgemmArgs& a, hipStream_t s) {
   return a.bl ? go_bf_t<BM, BN, WM, WN, 1>(a, s) : go_bf_t<BM, BN, WM, WN, 0>(a, s);
 }
 
-template <int TH, int TW, int BN, int WM, int WN, int MINW, int SPLIT>
+template <int TH, int TW, int BN, int WM, int WN, int MINW, int SPLIT, int A16>
 static hipError_t go_halo_t(const IgemmArgs& a, hipStream_t s) {
   static bool attr = false;
-  hipError_t e = allow_smem(reinterpret_cast<const void*>(&k_conv3_bf<TH, TW, BN, WM, WN, MINW, SPLIT>),
+  hipError_t e = allow_smem(reinterpret_cast<const void*>(&k_conv3_bf<TH, TW, BN, WM, WN, MINW, SPLIT, A16>),
                             conv3_bf_smem<TH, TW, BN, SPLIT>(1024), attr);
   if (e != hipSuccess) return e;
   const long long tiles = (long long)a.a.nimg * ((a.a.Hg + TH - 1) / TH) * ((a.a.Wg + TW - 1) / TW);
   dim3 grid((unsigned)tiles, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
   const size_t smem = conv3_bf_smem<TH, TW, BN, SPLIT>(a.a.Cg);
-  hipLaunchKernelGGL((k_conv3_bf<TH, TW, BN, WM, WN, MINW, SPLIT>), grid, dim3(WM * WN * 64), smem, s, a);
+  hipLaunchKernelGGL((k_conv3_bf<TH, TW, BN, WM, WN, MINW, SPLIT, A16>), grid, dim3(WM * WN * 64), smem, s, a);
   return hipGetLastError();
 }
 
@@ -1257,10 +1260,11 @@ static hipError_t go_halo(const IgemmArgs& a, hipStream_t s) {
     // the lo fragments double the operand registers: at most 2 accumulator tiles per wave
     constexpr int TM = TH * TW / 32 / WM, TN = BN / (WN * 32);
     if constexpr (conv3_bf_smem<TH, TW, BN, 1>(1024) <= kLdsBytes && TM * TN <= 2)
-      return go_halo_t<TH, TW, BN, WM, WN, (MINW < 2 ? MINW : 2), 1>(a, s);
+      return go_halo_t<TH, TW, BN, WM, WN, (MINW < 2 ? MINW : 2), 1, 0>(a, s);
     return hipErrorInvalidValue;
   }
-  return go_halo_t<TH, TW, BN, WM, WN, MINW, 0>(a, s);
+  const bool a16 = a.a.s[0].h16 && (a.a.c_split >= a.a.Cg || a.a.s[1].h16);
+  return a16 ? go_halo_t<TH, TW, BN, WM, WN, MINW, 0, 1>(a, s) : go_halo_t<TH, TW, BN, WM, WN, MINW, 0, 0>(a, s);
 }
 
 template <int TH, int TW>
