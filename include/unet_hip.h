@@ -145,6 +145,25 @@ int unet_iou_counts(const uint8_t* pred, const uint8_t* gt, size_t n, unsigned l
 int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int w,
                           unet_stream_t stream);
 
+/* Elastic-deformation input pipeline: the
+ * utils/augmentations.py:4-39 warp and the utils/dataset.py:84-111 steps around
+ * it for a batch of n samples (h x w each):
+ *   noise  (n, 2, h, w) fp64 uniform [0, 1) -- field 0 drives dx, field 1 dy
+ *          (the reference draws them as RandomState(seed).rand(h, w), dx first);
+ *   dx|dy = alpha * gaussian_filter(2 noise - 1, sigma, mode="constant")
+ *          (truncate 4: radius int(4 sigma + 0.5) <= 160);
+ *   image' = map_coordinates(image, (y + dy, x + dx), order=1, mode="reflect"),
+ *   label' = same with order=0, both rounded to their integer type;
+ *   x_out  (n, h, w) fp32 = uint8(image') / 255   (ToTensor, NCHW with C = 1),
+ *   target_out (n, h, w) uint8 = uint8(label') > 0 (the weight map is not
+ *          warped, as in the reference);
+ *   image_out (optional, may be NULL) = uint8(image').
+ * ws >= unet_elastic_ws_bytes(n, h, w), 8-byte aligned. */
+size_t unet_elastic_ws_bytes(int n, int h, int w);
+int unet_elastic_deform(const uint8_t* image, const uint16_t* labels, int n, int h, int w,
+                        const double* noise, double alpha, double sigma, float* x_out,
+                        uint8_t* target_out, uint8_t* image_out, void* ws, unet_stream_t stream);
+
 /* Tuning hooks, process-global:
  *  "autotune"      1 (default, or env UNET_AUTOTUNE) = the plan times the
  *                  applicable GEMM variants (tile shape, split-K, wgrad pixel

@@ -43,3 +43,14 @@ def sample_indices(name: str, size: int, k: int = 32) -> np.ndarray:
     s = zlib.crc32(name.encode())
     u = O.hash_uniform(s, 77, k)
     return np.unique((u * size).astype(np.int64).clip(0, size - 1))
+
+
+def elastic_synthetic_case():
+    """Inputs of the synthetic elastic-deformation fixture
+    (tests/golden/make_golden_elastic.py): a ragged 61 x 77 uint8 image and
+    uint16 labels up to 300 (40 % background)."""
+    g = np.random.default_rng(2024)
+    img = g.integers(0, 256, (61, 77)).astype(np.uint8)
+    lab = g.integers(0, 301, (61, 77)).astype(np.uint16)
+    lab[g.random((61, 77)) < 0.4] = 0
+    return img, lab

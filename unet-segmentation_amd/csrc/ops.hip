@@ -355,6 +355,17 @@ int unet_set_tuning(const char* key, int value) {
   return 0;
 }
 
+size_t unet_elastic_ws_bytes(int n, int h, int w) { return n > 0 && h > 0 && w > 0 ? elastic_ws_bytes(n, h, w) : 0; }
+
+int unet_elastic_deform(const uint8_t* image, const uint16_t* labels, int n, int h, int w, const double* noise,
+                        double alpha, double sigma, float* x_out, uint8_t* target_out, uint8_t* image_out, void* ws,
+                        unet_stream_t st) {
+  if (!image || !labels || !noise || !x_out || !target_out || !ws || (reinterpret_cast<uintptr_t>(ws) & 7)) return -EINVAL;
+  OPCK(launch_elastic(image, labels, n, h, w, noise, alpha, sigma, x_out, target_out, image_out, ws,
+                      reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
 int unet_mask_from_logits(const float* logits, uint8_t* mask, int n, int h, int w, unet_stream_t st) {
   OPCK(launch_mask(logits, mask, n, h, w, reinterpret_cast<hipStream_t>(st)));
   return 0;

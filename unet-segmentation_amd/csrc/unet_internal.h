@@ -132,6 +132,12 @@ bool bf16_tile_splits(int tile);
 // lo (optional): lo[i] = bf16(in[i] - out[i]), the residual plane of split operands
 hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s, uint16_t* lo = nullptr);
 
+// elastic-deformation input pipeline (elastic.hip)
+size_t elastic_ws_bytes(int n, int h, int w);
+hipError_t launch_elastic(const uint8_t* img, const uint16_t* lab, int n, int h, int w, const double* noise,
+                          double alpha, double sigma, float* x_out, uint8_t* t_out, uint8_t* img_out, void* ws,
+                          hipStream_t s);
+
 // inc.c0: Ci in {1,2,3,4} direct conv from an NCHW input; y NHWC (Co = 64 multiple).
 hipError_t launch_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w,
                                  const float* wt_oihw, const float* bias, int co, float* y,
