@@ -164,6 +164,22 @@ int unet_elastic_deform(const uint8_t* image, const uint16_t* labels, int n, int
                         const double* noise, double alpha, double sigma, float* x_out,
                         uint8_t* target_out, uint8_t* image_out, void* ws, unet_stream_t stream);
 
+/* Overlap-tile inference (scripts/predict1.py:35-49
+ * margin rule): tile t of an nx-wide tile grid has its input origin at
+ * ((t / nx) * tile_out - top, (t % nx) * tile_out - left) in the image; a call
+ * covers tiles first + b * stride, b < ntiles (stride = world for a round-robin deal).
+ * unet_tile_gather: tiles (ntiles, c, tile_in, tile_in) fp32, read from image (c, h, w) with the mirror
+ *   padding ("reflect", np.pad semantics incl. pads beyond the image) folded
+ *   into the index.
+ * unet_tile_scatter: tile logits (ntiles, k, tile_out, tile_out) into the full
+ *   logits (k, h, w) (may be NULL) and / or the mask (h, w) uint8 =
+ *   255 * (l1 > l0) (k == 2; scripts/predict.py:85-92; may be NULL); output
+ *   pixels past the image are dropped. */
+int unet_tile_gather(const float* image, int c, int h, int w, int tile_in, int tile_out, int top, int left,
+                     int nx, int first, int stride, int ntiles, float* tiles, unet_stream_t stream);
+int unet_tile_scatter(const float* tile_logits, int k, int tile_out, int nx, int first, int stride, int ntiles,
+                      int h, int w, float* logits, uint8_t* mask, unet_stream_t stream);
+
 /* Tuning hooks, process-global:
  *  "autotune"      1 (default, or env UNET_AUTOTUNE) = the plan times the
  *                  applicable GEMM variants (tile shape, split-K, wgrad pixel

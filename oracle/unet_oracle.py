@@ -598,8 +598,9 @@ def mirror_pad(img, pads):
     out = img
     while top or bottom or left or right:
         H, W = out.shape[-2:]
-        t, b = min(top, H - 1), min(bottom, H - 1)
-        l, r = min(left, W - 1), min(right, W - 1)
+        # a length-1 axis reflects onto itself (np.pad repeats the sample)
+        t, b = (top, bottom) if H == 1 else (min(top, H - 1), min(bottom, H - 1))
+        l, r = (left, right) if W == 1 else (min(left, W - 1), min(right, W - 1))
         pad = [(0, 0)] * (out.ndim - 2) + [(t, b), (l, r)]
         out = np.pad(out, pad, mode="reflect")
         top, bottom, left, right = top - t, bottom - b, left - l, right - r

@@ -60,6 +60,11 @@ def test_tile_farm_vs_oracle():
     img = (rng.uniform(size=(H, W)) * 2 - 1).astype(np.float32)
     farm = TileFarm(m, devices=[0], tile_in=tile, batch=4)
     logits = farm.predict(torch.from_numpy(img)).numpy()
+    # two replicas on the one device: the round-robin deal (stride 2) and the
+    # merge; batch 3 runs other GEMM shapes, so equal to fp32 noise, not bits
+    farm2 = TileFarm(m, devices=[0, 0], tile_in=tile, batch=3)
+    np.testing.assert_allclose(farm2.predict(torch.from_numpy(img)).numpy(), logits, rtol=0, atol=1e-4)
+    mask2 = farm2.predict(torch.from_numpy(img), return_mask=True).numpy()
     # oracle: mirror pad, eval forward per tile, stitch
     g = TileGeometry(H, W, tile)
     padded = O.mirror_pad(img[None], g.pads)
@@ -73,3 +78,50 @@ def test_tile_farm_vs_oracle():
     mk = mask_from_logits(torch.from_numpy(logits)).numpy()
     sure = np.abs(ref[1] - ref[0]) > 1e-3
     np.testing.assert_array_equal(mk[sure], ((ref[1] > ref[0]) * 255).astype(np.uint8)[sure])
+    np.testing.assert_array_equal(mask2[sure], mk[sure])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("c,h,w,tile,world,rank", [(1, 100, 90, 220, 1, 0), (3, 5, 7, 220, 2, 1),
+                                                   (2, 300, 41, 220, 3, 2), (1, 1, 9, 220, 1, 0)])
+def test_tile_gather_scatter_kernels(c, h, w, tile, world, rank):
+    """unet_tile_gather vs the oracle's mirror padding (pads far beyond the
+    image: repeated reflection; single-row image), unet_tile_scatter vs a
+    host stitch, for one rank of a round-robin deal."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import ctypes
+    from unet_amd import _lib
+    from unet_amd.tiling import TileGeometry, rank_share
+    lib = _lib.load()
+    g = TileGeometry(h, w, tile)
+    img = np.random.default_rng(h * w).standard_normal((c, h, w)).astype(np.float32)
+    padded = O.mirror_pad(img, g.pads)
+    mine = rank_share(g, rank, world)
+    if not mine:
+        pytest.skip("no tile for this rank")
+    st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+    dimg = torch.from_numpy(img).cuda()
+    tiles = torch.empty((len(mine), c, tile, tile), device="cuda")
+    _lib.check(lib.unet_tile_gather(dimg.data_ptr(), c, h, w, tile, g.tile_out, g.pads[0], g.pads[2], g.nx, mine[0],
+                                    world, len(mine), tiles.data_ptr(), st), "gather")
+    got = tiles.cpu().numpy()
+    for b, t in enumerate(mine):
+        y, x = g.origins[t]
+        np.testing.assert_array_equal(got[b], padded[:, y:y + tile, x:x + tile])
+    to = g.tile_out
+    lt = np.random.default_rng(1).standard_normal((len(mine), 2, to, to)).astype(np.float32)
+    full = torch.full((2, h, w), 7.0, device="cuda")
+    mask = torch.full((h, w), 3, dtype=torch.uint8, device="cuda")
+    _lib.check(lib.unet_tile_scatter(torch.from_numpy(lt).cuda().data_ptr(), 2, to, g.nx, mine[0], world, len(mine),
+                                     h, w, full.data_ptr(), mask.data_ptr(), st), "scatter")
+    ref = np.full((2, g.ny * to, g.nx * to), 7.0, np.float32)
+    for b, t in enumerate(mine):
+        y, x = g.origins[t]
+        ref[:, y:y + to, x:x + to] = lt[b]
+    ref = ref[:, :h, :w]
+    np.testing.assert_array_equal(full.cpu().numpy(), ref)
+    covered = ref[0] != 7.0
+    mk = mask.cpu().numpy()
+    np.testing.assert_array_equal(mk[covered], ((ref[1] > ref[0]) * 255).astype(np.uint8)[covered])
+    assert (mk[~covered] == 3).all()

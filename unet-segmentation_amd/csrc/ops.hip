@@ -355,6 +355,22 @@ int unet_set_tuning(const char* key, int value) {
   return 0;
 }
 
+int unet_tile_gather(const float* image, int c, int h, int w, int tile_in, int tile_out, int top, int left, int nx,
+                     int first, int stride, int ntiles, float* tiles, unet_stream_t st) {
+  if (!image || !tiles) return -EINVAL;
+  OPCK(launch_tile_gather(image, c, h, w, tile_in, tile_out, top, left, nx, first, stride, ntiles, tiles,
+                          reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_tile_scatter(const float* tile_logits, int k, int tile_out, int nx, int first, int stride, int ntiles, int h,
+                      int w, float* logits, uint8_t* mask, unet_stream_t st) {
+  if (!tile_logits) return -EINVAL;
+  OPCK(launch_tile_scatter(tile_logits, k, tile_out, nx, first, stride, ntiles, h, w, logits, mask,
+                           reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
 size_t unet_elastic_ws_bytes(int n, int h, int w) { return n > 0 && h > 0 && w > 0 ? elastic_ws_bytes(n, h, w) : 0; }
 
 int unet_elastic_deform(const uint8_t* image, const uint16_t* labels, int n, int h, int w, const double* noise,

@@ -132,6 +132,12 @@ bool bf16_tile_splits(int tile);
 // lo (optional): lo[i] = bf16(in[i] - out[i]), the residual plane of split operands
 hipError_t launch_f2bf(const float* in, uint16_t* out, size_t n, hipStream_t s, uint16_t* lo = nullptr);
 
+// overlap-tile gather / scatter (tiling.hip)
+hipError_t launch_tile_gather(const float* img, int c, int h, int w, int ti, int to, int top, int left, int nx,
+                              int first, int stride, int ntiles, float* tiles, hipStream_t s);
+hipError_t launch_tile_scatter(const float* lt, int k, int to, int nx, int first, int stride, int ntiles, int h,
+                               int w, float* full, uint8_t* mask, hipStream_t s);
+
 // elastic-deformation input pipeline (elastic.hip)
 size_t elastic_ws_bytes(int n, int h, int w);
 hipError_t launch_elastic(const uint8_t* img, const uint16_t* lab, int n, int h, int w, const double* noise,

@@ -11,12 +11,16 @@ tiles then tile the image exactly with no overlap, so stitching is a copy.
 Tiles are farmed over GPUs with no collective: ``TileFarm`` runs one model
 replica per device (one host thread each, HIP calls release the GIL) and deals
 tiles round-robin; ``rank_share`` gives the tiles of one rank when each GPU is
-driven by its own process.  Each tile batch is an eval-mode forward
-(scripts/predict.py:70-82: BatchNorm with running statistics).
+driven by its own process.  On the device, ``unet_tile_gather`` reads each tile
+batch straight from the unpadded image (mirror folded into the index),
+each batch is an eval-mode forward (scripts/predict.py:70-82: BatchNorm with
+running statistics), and ``unet_tile_scatter`` writes the tile logits -- or the
+uint8 mask directly -- into the full image.
 """
 from __future__ import annotations
 
 import copy
+import functools
 import threading
 
 import torch
@@ -58,21 +62,26 @@ class TileGeometry:
         return len(self.origins)
 
 
+def mirror_index(n_out, start, n):
+    """Indices of a whole-sample-symmetric extension (np.pad 'reflect',
+    repeated for pads beyond the image; a length-1 axis repeats its sample):
+    position start + i of the infinite mirrored axis, i < n_out."""
+    i = torch.arange(start, start + n_out)
+    if n == 1:
+        return torch.zeros_like(i)
+    p = 2 * n - 2
+    i = torch.remainder(i, p)
+    return torch.where(i < n, i, p - i)
+
+
 def mirror_pad(img, pads):
-    """Reflect padding of an (..., H, W) tensor; pads larger than the image are
-    reflected repeatedly (np.pad(mode='reflect') semantics)."""
+    """Mirror padding of an (..., H, W) tensor on the host (the geometry
+    reference of unet_tile_gather, which folds the same indices on the GPU)."""
     top, bottom, left, right = pads
-    out = img
-    while top or bottom or left or right:
-        H, W = out.shape[-2:]
-        t, b = min(top, H - 1), min(bottom, H - 1)
-        l, r = min(left, W - 1), min(right, W - 1)
-        shp = out.shape
-        o4 = out.reshape(-1, 1, H, W)
-        o4 = F.pad(o4, (l, r, t, b), mode="reflect")
-        out = o4.reshape(*shp[:-2], H + t + b, W + l + r)
-        top, bottom, left, right = top - t, bottom - b, left - l, right - r
-    return out
+    H, W = img.shape[-2:]
+    iy = mirror_index(H + top + bottom, -top, H).to(img.device)
+    ix = mirror_index(W + left + right, -left, W).to(img.device)
+    return img.index_select(-2, iy).index_select(-1, ix)
 
 
 def extract_tiles(padded, geo, indices):
@@ -84,20 +93,6 @@ def extract_tiles(padded, geo, indices):
 def rank_share(geo, rank, world):
     """Tile indices processed by `rank` (round-robin deal, no collective)."""
     return list(range(rank, len(geo), world))
-
-
-@torch.no_grad()
-def predict_tiles(model, padded, geo, indices, batch=4):
-    """Eval forwards of the listed tiles; returns {index: logits (K, t, t)}."""
-    out = {}
-    dev = next(model.parameters()).device
-    for s in range(0, len(indices), batch):
-        idx = indices[s:s + batch]
-        x = extract_tiles(padded, geo, idx).to(dev, torch.float32).contiguous()
-        logits = model(x)
-        for i, lg in zip(idx, logits):
-            out[i] = lg
-    return out
 
 
 def stitch(results, geo, n_classes):
@@ -113,7 +108,10 @@ def stitch(results, geo, n_classes):
 class TileFarm:
     """Overlap-tile inference of large images farmed over several GPUs of one
     process (one replica + one host thread per device, tiles dealt round-robin,
-    no collectives)."""
+    no collectives).  On each device the tiles are gathered from the unpadded
+    image with the mirror padding folded into the index (unet_tile_gather) and
+    the tile logits are scattered into the device's full-image logits / mask
+    (unet_tile_scatter): no padded copy, no per-tile host traffic."""
 
     def __init__(self, model, devices=None, tile_in=512, batch=4):
         if devices is None:
@@ -126,27 +124,49 @@ class TileFarm:
             r = copy.deepcopy(model).to(d).eval()
             self.replicas.append(r)
 
-    def predict(self, image):
+    @torch.no_grad()
+    def _run_device(self, k, image, geo, want_logits, want_mask):
+        from . import _lib
+        lib = _lib.load()
+        dev, model = self.devices[k], self.replicas[k]
+        world = len(self.devices)
+        C, H, W = image.shape
+        img = image.to(dev, torch.float32).contiguous()
+        K = self.n_classes
+        full = torch.zeros((K, H, W), dtype=torch.float32, device=dev) if want_logits else None
+        mask = torch.zeros((H, W), dtype=torch.uint8, device=dev) if want_mask else None
+        mine = rank_share(geo, k, world)
+        ti, to, top, left = geo.tile_in, geo.tile_out, geo.pads[0], geo.pads[2]
+        tiles = torch.empty((self.batch, C, ti, ti), dtype=torch.float32, device=dev)
+        for s in range(0, len(mine), self.batch):
+            nb = min(self.batch, len(mine) - s)
+            st = _lib.stream_of(dev)
+            _lib.check(lib.unet_tile_gather(img.data_ptr(), C, H, W, ti, to, top, left, geo.nx, mine[s], world, nb,
+                                            tiles.data_ptr(), st), "unet_tile_gather")
+            logits = model(tiles[:nb]).contiguous()
+            _lib.check(lib.unet_tile_scatter(logits.data_ptr(), K, to, geo.nx, mine[s], world, nb, H, W,
+                                             full.data_ptr() if full is not None else None,
+                                             mask.data_ptr() if mask is not None else None, st), "unet_tile_scatter")
+        return full, mask
+
+    def predict(self, image, return_mask=False):
         """image: (C, H, W) or (H, W) float tensor (already normalised the way
         the model was trained, e.g. predict.py's Normalize(0.5, 0.5)).
-        Returns (K, H, W) logits on the host."""
+        Returns (K, H, W) logits on the host, or with return_mask=True the
+        (H, W) uint8 mask (255 * (l1 > l0), scripts/predict.py:85-92)."""
         if image.dim() == 2:
             image = image[None]
         C, H, W = image.shape
         geo = TileGeometry(H, W, self.tile_in)
-        padded = mirror_pad(image.float(), geo.pads)
-        results, errors = {}, []
-        lock = threading.Lock()
+        if return_mask and self.n_classes != 2:
+            raise ValueError("the mask needs 2 classes")
+        outs, errors = [None] * len(self.devices), []
 
         def work(k):
             try:
-                dev = self.devices[k]
-                with torch.cuda.device(dev):
-                    local = predict_tiles(self.replicas[k], padded.to(dev), geo,
-                                          rank_share(geo, k, len(self.devices)), self.batch)
-                    torch.cuda.synchronize(dev)
-                with lock:
-                    results.update(local)
+                with torch.cuda.device(self.devices[k]):
+                    outs[k] = self._run_device(k, image, geo, not return_mask, return_mask)
+                    torch.cuda.synchronize(self.devices[k])
             except Exception as e:  # surfaced below
                 errors.append(e)
 
@@ -157,7 +177,10 @@ class TileFarm:
             th.join()
         if errors:
             raise errors[0]
-        return stitch(results, geo, self.n_classes)
+        # every pixel belongs to exactly one device's tiles; the others hold 0 there
+        if return_mask:
+            return functools.reduce(torch.maximum, [m.cpu() for _, m in outs])
+        return functools.reduce(torch.add, [f.cpu() for f, _ in outs])
 
 
 def mask_from_logits(logits):
