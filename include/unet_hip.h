@@ -180,6 +180,17 @@ int unet_tile_gather(const float* image, int c, int h, int w, int tile_in, int t
 int unet_tile_scatter(const float* tile_logits, int k, int tile_out, int nx, int first, int stride, int ntiles,
                       int h, int w, float* logits, uint8_t* mask, unet_stream_t stream);
 
+/* Loss weight maps (scripts/preprocess_data.py:17-77 with
+ * w0, sigma as its :14-15 = 10, 5): per sample of labels (n, h, w) uint16,
+ * weights = fp32(wc) + w0 * exp(-(d1 + d2)^2 / (2 (sigma^2 + 1e-8))) where wc =
+ * 1 / (class count / h w) of labels > 0 and d1 = d2 = 0 (the reference's
+ * min(edt(obj), edt(!obj)) is identically 0).  weights (n, h, w) fp32 (what
+ * utils/dataset.py:111 feeds the loss), weights64 (may be NULL) the fp64 map
+ * the reference saves.  ws >= unet_weight_map_ws_bytes(n), 8-byte aligned. */
+size_t unet_weight_map_ws_bytes(int n);
+int unet_weight_map(const uint16_t* labels, int n, int h, int w, double w0, double sigma, float* weights,
+                    double* weights64, void* ws, unet_stream_t stream);
+
 /* Tuning hooks, process-global:
  *  "autotune"      1 (default, or env UNET_AUTOTUNE) = the plan times the
  *                  applicable GEMM variants (tile shape, split-K, wgrad pixel

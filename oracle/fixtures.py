@@ -54,3 +54,17 @@ def elastic_synthetic_case():
     lab = g.integers(0, 301, (61, 77)).astype(np.uint16)
     lab[g.random((61, 77)) < 0.4] = 0
     return img, lab
+
+
+def weightmap_synthetic_cases():
+    """Label maps of the synthetic weight-map fixtures
+    (tests/golden/make_golden_weightmap.py): ragged multi-object, one object,
+    empty, all foreground."""
+    g = np.random.default_rng(77)
+    multi = g.integers(0, 9, (45, 71)).astype(np.uint16)
+    multi[g.random((45, 71)) < 0.5] = 0
+    one = np.zeros((30, 30), np.uint16)
+    one[5:12, 8:20] = 3
+    empty = np.zeros((17, 23), np.uint16)
+    full = np.full((9, 11), 5, np.uint16)
+    return {"multi": multi, "one": one, "empty": empty, "full": full}

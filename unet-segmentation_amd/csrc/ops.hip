@@ -371,6 +371,15 @@ int unet_tile_scatter(const float* tile_logits, int k, int tile_out, int nx, int
   return 0;
 }
 
+size_t unet_weight_map_ws_bytes(int n) { return n > 0 ? weight_map_ws_bytes(n) : 0; }
+
+int unet_weight_map(const uint16_t* labels, int n, int h, int w, double w0, double sigma, float* weights,
+                    double* weights64, void* ws, unet_stream_t st) {
+  if (!labels || !weights || !ws || (reinterpret_cast<uintptr_t>(ws) & 7)) return -EINVAL;
+  OPCK(launch_weight_map(labels, n, h, w, w0, sigma, weights, weights64, ws, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
 size_t unet_elastic_ws_bytes(int n, int h, int w) { return n > 0 && h > 0 && w > 0 ? elastic_ws_bytes(n, h, w) : 0; }
 
 int unet_elastic_deform(const uint8_t* image, const uint16_t* labels, int n, int h, int w, const double* noise,

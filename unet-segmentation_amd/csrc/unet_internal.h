@@ -138,6 +138,11 @@ hipError_t launch_tile_gather(const float* img, int c, int h, int w, int ti, int
 hipError_t launch_tile_scatter(const float* lt, int k, int to, int nx, int first, int stride, int ntiles, int h,
                                int w, float* full, uint8_t* mask, hipStream_t s);
 
+// loss weight maps (weightmap.hip)
+size_t weight_map_ws_bytes(int n);
+hipError_t launch_weight_map(const uint16_t* lab, int n, int h, int w, double w0, double sigma, float* out,
+                             double* out64, void* ws, hipStream_t s);
+
 // elastic-deformation input pipeline (elastic.hip)
 size_t elastic_ws_bytes(int n, int h, int w);
 hipError_t launch_elastic(const uint8_t* img, const uint16_t* lab, int n, int h, int w, const double* noise,

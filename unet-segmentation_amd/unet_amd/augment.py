@@ -82,3 +82,24 @@ class ElasticDeform:
                                                 x.data_ptr(), t.data_ptr(), img.data_ptr() if img is not None else None,
                                                 self._ws.data_ptr(), _lib.stream_of()), "unet_elastic_deform")
         return (x, t, img) if return_image else (x, t)
+
+
+def weight_maps(labels: torch.Tensor, w0: float = 10.0, sigma: float = 5.0, fp64: bool = False):
+    """scripts/preprocess_data.py:17-77 on the device for a batch of label maps
+    (N, H, W) (uint16 instance ids, or any integer type): the per-pixel loss
+    weights (N, H, W) fp32 utils/dataset.py:111 feeds the loss, and with
+    fp64=True also the fp64 map the reference saves as weight_map_*.npy."""
+    lib = _lib.load()
+    if labels.device.type != "cuda" or labels.dim() != 3:
+        raise ValueError("labels must be an (N, H, W) tensor on the HIP device")
+    if labels.dtype != torch.uint16:
+        labels = labels.to(torch.int32).to(torch.int16).view(torch.uint16)
+    labels = labels.contiguous()
+    n, h, w = labels.shape
+    out = torch.empty((n, h, w), dtype=torch.float32, device=labels.device)
+    out64 = torch.empty((n, h, w), dtype=torch.float64, device=labels.device) if fp64 else None
+    ws = torch.empty(lib.unet_weight_map_ws_bytes(n), dtype=torch.uint8, device=labels.device)
+    _lib.check(lib.unet_weight_map(labels.data_ptr(), n, h, w, ctypes.c_double(w0), ctypes.c_double(sigma),
+                                   out.data_ptr(), out64.data_ptr() if out64 is not None else None, ws.data_ptr(),
+                                   _lib.stream_of()), "unet_weight_map")
+    return (out, out64) if fp64 else out
