@@ -191,6 +191,22 @@ size_t unet_weight_map_ws_bytes(int n);
 int unet_weight_map(const uint16_t* labels, int n, int h, int w, double w0, double sigma, float* weights,
                     double* weights64, void* ws, unet_stream_t stream);
 
+/* Post-processing (utils/metrics.py):
+ * unet_instance_masks: get_instance_masks (:42-72) for n masks (h, w) uint8
+ *   (> 0 = foreground): 8-connected components numbered 1, 2, ... in raster
+ *   order of their first pixel (skimage.measure.label(connectivity=2)), those
+ *   with fewer than min_size pixels set to 0 without renumbering
+ *   (remove_small_objects), uint16 labels out.  n h w < 2^31.
+ * unet_rand_index: calculate_rand_index_and_error (:75-139) of two uint16
+ *   labelings (h, w): out[0] = Rand index, out[1] = Rand error (fp64, device);
+ *   up to 2^24 (gt label, pred label) pairs; synchronises the stream once. */
+size_t unet_instance_masks_ws_bytes(int n, int h, int w);
+int unet_instance_masks(const uint8_t* mask, int n, int h, int w, int min_size, uint16_t* labels, void* ws,
+                        unet_stream_t stream);
+size_t unet_rand_index_ws_bytes(int h, int w);
+int unet_rand_index(const uint16_t* gt, const uint16_t* pred, int h, int w, double* out, void* ws,
+                    unet_stream_t stream);
+
 /* Tuning hooks, process-global:
  *  "autotune"      1 (default, or env UNET_AUTOTUNE) = the plan times the
  *                  applicable GEMM variants (tile shape, split-K, wgrad pixel

@@ -371,6 +371,26 @@ int unet_tile_scatter(const float* tile_logits, int k, int tile_out, int nx, int
   return 0;
 }
 
+size_t unet_instance_masks_ws_bytes(int n, int h, int w) {
+  return n > 0 && h > 0 && w > 0 ? instance_masks_ws_bytes(n, h, w) : 0;
+}
+
+int unet_instance_masks(const uint8_t* mask, int n, int h, int w, int min_size, uint16_t* labels, void* ws,
+                        unet_stream_t st) {
+  if (!mask || !labels || !ws) return -EINVAL;
+  OPCK(launch_instance_masks(mask, n, h, w, min_size, labels, ws, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+size_t unet_rand_index_ws_bytes(int h, int w) { return h > 0 && w > 0 ? rand_index_ws_bytes(h, w) : 0; }
+
+int unet_rand_index(const uint16_t* gt, const uint16_t* pred, int h, int w, double* out, void* ws,
+                    unet_stream_t st) {
+  if (!gt || !pred || !out || !ws) return -EINVAL;
+  OPCK(launch_rand_index(gt, pred, h, w, out, ws, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
 size_t unet_weight_map_ws_bytes(int n) { return n > 0 ? weight_map_ws_bytes(n) : 0; }
 
 int unet_weight_map(const uint16_t* labels, int n, int h, int w, double w0, double sigma, float* weights,

@@ -1,0 +1,245 @@
+// Segmentation post-processing on the GPU, utils/metrics.py:
+//
+// * instance masks (get_instance_masks, :42-72): 8-connected components of
+//   mask > 0 by lock-free union-find -- every foreground pixel unions with its
+//   four raster-earlier neighbours (left, up-left, up, up-right) through
+//   atomicMin on the parent array, so each root is its component's smallest
+//   linear index = its first pixel in raster order.  Components are numbered
+//   by an exclusive scan of the root flags (the raster order of their first
+//   pixels, skimage.measure.label's numbering), sizes are counted with atomics
+//   at the roots, and components below min_size are zeroed without renumbering
+//   the rest (skimage.morphology.remove_small_objects); uint16 output.
+// * Rand index / error (calculate_rand_index_and_error, :75-139): the labels
+//   present in each map are compacted by a scan of presence flags, the
+//   contingency table is a dense histogram of (gt, pred) index pairs, and
+//   sum n(n-1)/2 over cells, rows and columns are exact 64-bit integers; the
+//   final fp64 arithmetic follows the reference's order (exact integers below
+//   2^53, so bit-identical).
+#include <hipcub/hipcub.hpp>
+
+#include <cstdint>
+
+#include "unet_internal.h"
+
+namespace unet {
+
+// ------------------------------- components ---------------------------------
+__device__ __forceinline__ int uf_find(const int* parent, int x) {
+  int p = parent[x];
+  while (p != x) {
+    x = p;
+    p = parent[x];
+  }
+  return x;
+}
+
+__device__ __forceinline__ void uf_union(int* parent, int a, int b) {
+  while (true) {
+    a = uf_find(parent, a);
+    b = uf_find(parent, b);
+    if (a == b) return;
+    if (a > b) {
+      const int t = a;
+      a = b;
+      b = t;
+    }
+    const int old = atomicMin(parent + b, a);
+    if (old == b) return;  // b was a root: now it points to a
+    b = old;
+  }
+}
+
+// parent[i] = i for foreground, -1 for background (per image, global index)
+__global__ void k_cc_init(const uint8_t* __restrict__ m, size_t total, int* __restrict__ parent) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i < total) parent[i] = m[i] ? (int)i : -1;
+}
+
+__global__ void k_cc_union(const uint8_t* __restrict__ m, int n, int h, int w, int* __restrict__ parent) {
+  const size_t hw = (size_t)h * w;
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= (size_t)n * hw || !m[i]) return;
+  const int p = (int)(i % hw);
+  const int y = p / w, x = p - (p / w) * w;
+  if (x > 0 && m[i - 1]) uf_union(parent, (int)i, (int)i - 1);
+  if (y > 0) {
+    if (x > 0 && m[i - w - 1]) uf_union(parent, (int)i, (int)(i - w - 1));
+    if (m[i - w]) uf_union(parent, (int)i, (int)(i - w));
+    if (x + 1 < w && m[i - w + 1]) uf_union(parent, (int)i, (int)(i - w + 1));
+  }
+}
+
+// flatten to roots; root flag and sizes
+__global__ void k_cc_flatten(size_t total, int* __restrict__ parent, int* __restrict__ is_root,
+                             unsigned* __restrict__ size) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  int r = -1;
+  if (parent[i] >= 0) {
+    r = uf_find(parent, (int)i);
+    atomicAdd(size + r, 1u);
+  }
+  is_root[i] = r == (int)i ? 1 : 0;
+  if (r >= 0) parent[i] = r;  // path compression: r is an ancestor, so concurrent finds stay correct
+}
+
+__global__ void k_cc_label(size_t total, size_t hw, const int* __restrict__ parent, const int* __restrict__ rank,
+                           const unsigned* __restrict__ size, int min_size, uint16_t* __restrict__ out) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= total) return;
+  if (parent[i] < 0) {
+    out[i] = 0;
+    return;
+  }
+  const int r = uf_find(parent, (int)i);
+  const size_t first = (i / hw) * hw;  // numbering restarts per image
+  const int id = rank[r] - rank[first] + 1;  // exclusive scan of root flags
+  out[i] = (int)size[r] < min_size ? 0 : (uint16_t)id;
+}
+
+size_t instance_masks_ws_bytes(int n, int h, int w) {
+  const size_t total = (size_t)n * h * w;
+  size_t scan = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int*)nullptr, (int*)nullptr, (int)total);
+  return 4 * (total * 4 + 256) + scan + 256;
+}
+
+static char* carve(char*& p, size_t bytes) {
+  char* r = p;
+  p += (bytes + 255) / 256 * 256;
+  return r;
+}
+
+hipError_t launch_instance_masks(const uint8_t* mask, int n, int h, int w, int min_size, uint16_t* out, void* ws,
+                                 hipStream_t s) {
+  const size_t total = (size_t)n * h * w;
+  if (n < 1 || h < 1 || w < 1 || total >= (1u << 31)) return hipErrorInvalidValue;
+  char* p = reinterpret_cast<char*>(ws);
+  int* parent = reinterpret_cast<int*>(carve(p, total * 4));
+  int* is_root = reinterpret_cast<int*>(carve(p, total * 4));
+  int* rank = reinterpret_cast<int*>(carve(p, total * 4));
+  unsigned* size = reinterpret_cast<unsigned*>(carve(p, total * 4));
+  size_t scan = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, is_root, rank, (int)total, s);
+  void* tmp = carve(p, scan);
+  const unsigned g = (unsigned)((total + 255) / 256);
+  hipError_t e = hipMemsetAsync(size, 0, total * 4, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_cc_init, dim3(g), dim3(256), 0, s, mask, total, parent);
+  hipLaunchKernelGGL(k_cc_union, dim3(g), dim3(256), 0, s, mask, n, h, w, parent);
+  hipLaunchKernelGGL(k_cc_flatten, dim3(g), dim3(256), 0, s, total, parent, is_root, size);
+  e = hipcub::DeviceScan::ExclusiveSum(tmp, scan, is_root, rank, (int)total, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(k_cc_label, dim3(g), dim3(256), 0, s, total, (size_t)h * w, parent, rank, size, min_size, out);
+  return hipGetLastError();
+}
+
+// -------------------------------- Rand index ---------------------------------
+constexpr int kLabels = 65536;
+constexpr long long kMaxCells = 1ll << 24;  // contingency table cap (64 MiB of counts)
+
+__global__ void k_ri_mark(const uint16_t* __restrict__ g, const uint16_t* __restrict__ p, size_t n,
+                          int* __restrict__ pg, int* __restrict__ pp) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  pg[g[i]] = 1;
+  pp[p[i]] = 1;
+}
+
+__global__ void k_ri_hist(const uint16_t* __restrict__ g, const uint16_t* __restrict__ p, size_t n,
+                          const int* __restrict__ ig, const int* __restrict__ ip, const int* __restrict__ npred,
+                          unsigned* __restrict__ table, unsigned* __restrict__ rows, unsigned* __restrict__ cols) {
+  const size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const int a = ig[g[i]], b = ip[p[i]];
+  atomicAdd(table + (size_t)a * (*npred) + b, 1u);
+  atomicAdd(rows + a, 1u);
+  atomicAdd(cols + b, 1u);
+}
+
+// sums of c (c - 1) / 2 over the table (acc[0]), rows (acc[1]), columns (acc[2])
+__global__ void k_ri_pairs(const unsigned* __restrict__ table, size_t cells, size_t span,
+                           const unsigned* __restrict__ rows, const unsigned* __restrict__ cols,
+                           unsigned long long* __restrict__ acc) {
+  unsigned long long s[3] = {0, 0, 0};
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < span; i += (size_t)gridDim.x * blockDim.x) {
+    if (i < cells) {
+      const unsigned long long c = table[i];
+      s[0] += c * (c - (c > 0)) / 2;
+    }
+    if (i < (size_t)kLabels) {
+      const unsigned long long r = rows[i], q = cols[i];
+      s[1] += r * (r - (r > 0)) / 2;
+      s[2] += q * (q - (q > 0)) / 2;
+    }
+  }
+  for (int k = 0; k < 3; ++k) {
+    unsigned long long v = s[k];
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+    if ((threadIdx.x & 63) == 0) atomicAdd(acc + k, v);
+  }
+}
+
+__global__ void k_ri_final(const unsigned long long* __restrict__ acc, size_t n, double* __restrict__ out) {
+  const double total = (double)n * (double)(n - 1) / 2.0;
+  const double a = (double)acc[0], same_gt = (double)acc[1], same_pred = (double)acc[2];
+  const double b = total - same_gt - same_pred + a;
+  const double ri = (a + b) / total;
+  out[0] = ri;
+  out[1] = 1.0 - ri;
+}
+
+size_t rand_index_ws_bytes(int h, int w) {
+  size_t scan = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int*)nullptr, (int*)nullptr, kLabels + 1);
+  (void)h;
+  (void)w;
+  return 4 * ((size_t)(kLabels + 1) * 4 + 256) + 2 * ((size_t)kLabels * 4 + 256) + (size_t)kMaxCells * 4 + 256 +
+         scan + 512;
+}
+
+hipError_t launch_rand_index(const uint16_t* g, const uint16_t* p, int h, int w, double* out, void* ws,
+                             hipStream_t s) {
+  const size_t n = (size_t)h * w;
+  if (h < 1 || w < 1) return hipErrorInvalidValue;
+  char* c = reinterpret_cast<char*>(ws);
+  int* pg = reinterpret_cast<int*>(carve(c, (kLabels + 1) * 4));
+  int* pp = reinterpret_cast<int*>(carve(c, (kLabels + 1) * 4));
+  int* ig = reinterpret_cast<int*>(carve(c, (kLabels + 1) * 4));
+  int* ip = reinterpret_cast<int*>(carve(c, (kLabels + 1) * 4));
+  unsigned* rows = reinterpret_cast<unsigned*>(carve(c, kLabels * 4));
+  unsigned* cols = reinterpret_cast<unsigned*>(carve(c, kLabels * 4));
+  unsigned* table = reinterpret_cast<unsigned*>(carve(c, (size_t)kMaxCells * 4));
+  auto* acc = reinterpret_cast<unsigned long long*>(carve(c, 64));
+  size_t scan = 0;
+  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, pg, ig, kLabels + 1, s);
+  void* tmp = carve(c, scan);
+  hipError_t e;
+  for (void* z : {(void*)pg, (void*)pp, (void*)rows, (void*)cols}) {
+    e = hipMemsetAsync(z, 0, (z == rows || z == cols) ? kLabels * 4 : (kLabels + 1) * 4, s);
+    if (e != hipSuccess) return e;
+  }
+  if ((e = hipMemsetAsync(acc, 0, 64, s)) != hipSuccess) return e;
+  const unsigned gsz = (unsigned)((n + 255) / 256);
+  hipLaunchKernelGGL(k_ri_mark, dim3(gsz), dim3(256), 0, s, g, p, n, pg, pp);
+  // exclusive scans: ig[l] = compact index of label l; ig[kLabels] = label count
+  if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, scan, pg, ig, kLabels + 1, s)) != hipSuccess) return e;
+  if ((e = hipcub::DeviceScan::ExclusiveSum(tmp, scan, pp, ip, kLabels + 1, s)) != hipSuccess) return e;
+  int counts[2];
+  if ((e = hipMemcpyAsync(&counts[0], ig + kLabels, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipMemcpyAsync(&counts[1], ip + kLabels, 4, hipMemcpyDeviceToHost, s)) != hipSuccess) return e;
+  if ((e = hipStreamSynchronize(s)) != hipSuccess) return e;
+  const long long cells = (long long)counts[0] * counts[1];
+  if (cells > kMaxCells) return hipErrorInvalidValue;
+  if ((e = hipMemsetAsync(table, 0, (size_t)cells * 4, s)) != hipSuccess) return e;
+  hipLaunchKernelGGL(k_ri_hist, dim3(gsz), dim3(256), 0, s, g, p, n, ig, ip, ip + kLabels, table, rows, cols);
+  const size_t span = (size_t)(cells > kLabels ? cells : kLabels);
+  unsigned gr = (unsigned)((span + 255) / 256);
+  if (gr > 1024) gr = 1024;
+  // k_ri_pairs reads `cells` table entries and all kLabels row / column counters
+  hipLaunchKernelGGL(k_ri_pairs, dim3(gr), dim3(256), 0, s, table, (size_t)cells, span, rows, cols, acc);
+  hipLaunchKernelGGL(k_ri_final, dim3(1), dim3(1), 0, s, acc, n, out);
+  return hipGetLastError();
+}
+
+}  // namespace unet

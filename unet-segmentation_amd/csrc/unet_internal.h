@@ -138,6 +138,14 @@ hipError_t launch_tile_gather(const float* img, int c, int h, int w, int ti, int
 hipError_t launch_tile_scatter(const float* lt, int k, int to, int nx, int first, int stride, int ntiles, int h,
                                int w, float* full, uint8_t* mask, hipStream_t s);
 
+// post-processing (postproc.hip)
+size_t instance_masks_ws_bytes(int n, int h, int w);
+hipError_t launch_instance_masks(const uint8_t* mask, int n, int h, int w, int min_size, uint16_t* out, void* ws,
+                                 hipStream_t s);
+size_t rand_index_ws_bytes(int h, int w);
+hipError_t launch_rand_index(const uint16_t* g, const uint16_t* p, int h, int w, double* out, void* ws,
+                             hipStream_t s);
+
 // loss weight maps (weightmap.hip)
 size_t weight_map_ws_bytes(int n);
 hipError_t launch_weight_map(const uint16_t* lab, int n, int h, int w, double w0, double sigma, float* out,

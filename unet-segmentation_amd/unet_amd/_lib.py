@@ -42,6 +42,10 @@ SIGNATURES = {
     "unet_mask_from_logits": (_i, [_vp, _vp, _i, _i, _i, _vp]),
     "unet_tile_gather": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp]),
     "unet_tile_scatter": (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "unet_instance_masks_ws_bytes": (_sz, [_i, _i, _i]),
+    "unet_instance_masks": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp]),
+    "unet_rand_index_ws_bytes": (_sz, [_i, _i]),
+    "unet_rand_index": (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp]),
     "unet_weight_map_ws_bytes": (_sz, [_i]),
     "unet_weight_map": (_i, [_vp, _i, _i, _i, ctypes.c_double, ctypes.c_double, _vp, _vp, _vp, _vp]),
     "unet_elastic_ws_bytes": (_sz, [_i, _i, _i]),
