@@ -113,11 +113,30 @@ struct LinearRows {
     return m < M;
   }
 };
-template <int TW>
+// Tile pixel of GEMM row p (32 rows per MFMA fragment).  Row-major, except in
+// 16 x 16 tiles read from 80-B LDS rows: there fragment f holds tile rows f and
+// f + 8 (lanes 0-15 / 16-31), 144 halo pixels apart -- a multiple of 16 bank
+// quads, like the two halves of a 32-wide row -- instead of rows f, f + 1 (18
+// pixels apart), whose ds_read_b128 lane groups collide on two bank quads.
+template <int TH, int TW>
+__device__ __forceinline__ void halo_pix(int p, int& ty, int& tx) {
+  if constexpr (TH == 16 && TW == 16) {
+    const int f = p >> 5, l = p & 31;
+    ty = f + 8 * (l >> 4);
+    tx = l & 15;
+  } else {
+    ty = p / TW;
+    tx = p % TW;
+  }
+}
+
+template <int TW, int TH = 0>
 struct HaloRows {
   int n, y0, x0, Hg, Wg;
   __device__ __forceinline__ bool map(int row, int& m) const {
-    const int y = y0 + row / TW, x = x0 + row % TW;
+    int ty, tx;
+    halo_pix<TH, TW>(row, ty, tx);
+    const int y = y0 + ty, x = x0 + tx;
     m = (n * Hg + y) * Wg + x;
     return y < Hg && x < Wg;
   }

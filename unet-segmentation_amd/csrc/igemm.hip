@@ -566,7 +566,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_f32(const IgemmArg
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int p = (wm * TM + i) * 32 + li;
-    abase[i] = (p / TW) * HW2 + p % TW;
+    int ty, tx;
+    halo_pix<TH, TW>(p, ty, tx);
+    abase[i] = ty * HW2 + tx;
   }
   auto compute = [&] {
 #pragma unroll
@@ -611,7 +613,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_f32(const IgemmArg
       __syncthreads();
     }
   }
-  igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, hsm, HaloRows<TW>{n, y0, x0, Hg, Wg});
+  igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, hsm, HaloRows<TW, TH>{n, y0, x0, Hg, Wg});
 }
 
 // ---------------------------------------------------------------------------

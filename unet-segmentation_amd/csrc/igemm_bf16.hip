@@ -459,7 +459,9 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
     const int p = (wm * TM + i) * 32 + li;
-    abase[i] = (p / TW) * HW2 + p % TW;
+    int ty, tx;
+    halo_pix<TH, TW>(p, ty, tx);
+    abase[i] = ty * HW2 + tx;
   }
   auto compute = [&] {
 #pragma unroll
@@ -511,7 +513,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     }
   }
   igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, reinterpret_cast<float*>(smem),
-                                   HaloRows<TW>{n, y0, x0, Hg, Wg});
+                                   HaloRows<TW, TH>{n, y0, x0, Hg, Wg});
 }
 
 // ---------------------------------------------------------------------------
