@@ -369,3 +369,47 @@ def test_side_stream_weight_grads_match_serial():
     for name, g in ref.items():
         scale = max(np.abs(g).max(), 1e-30)
         assert np.abs(got[name] - g).max() <= 1e-5 * scale + 1e-12, name
+
+
+@pytest.mark.parametrize("c,k", [(2, 3), (4, 4), (3, 2)])
+def test_channel_and_class_counts_vs_oracle(c, k):
+    """n_channels 2-4 (the first conv's direct kernel) and n_classes 3-4 (head,
+    weighted CE over K classes) -- the reference's constructor arguments
+    (models/unet_model.py:66) beyond the 1 -> 2 of scripts/train.py."""
+    from unet_amd import WeightedCrossEntropyLoss
+    seed = 60 + 10 * c + k
+    params = O.hash_init(c, k, seed=seed, bn_random=True)
+    x, _, wmap = F.make_inputs(seed, 2, c, 188)
+    ho = O.output_size(188)
+    tgt = np.minimum((O.hash_uniform(seed, 1002, 2 * ho * ho) * k).astype(np.int64), k - 1).reshape(2, ho, ho)
+    net = O.UNetOracle(params)
+    rl, cache, _ = net.forward(x)
+    rloss, rdl = O.weighted_ce(rl, tgt, wmap)
+    rg = net.backward(rdl, cache)
+    m = make_model(params, c, k)
+    m.train()
+    logits = m(torch.from_numpy(x).cuda())
+    loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+    loss.backward()
+    lg = logits.detach().double().cpu().numpy()
+    assert lg.shape == (2, k, ho, ho)
+    assert np.abs(lg - rl).max() <= 1e-3
+    assert abs(loss.item() - rloss) <= 1e-4 * abs(rloss)
+    check_grads(grads_of(m), rg)
+
+
+def test_single_class_loss_and_grads_are_zero():
+    """n_classes = 1: CrossEntropy over one class is identically 0 (logsumexp of
+    one logit is the logit), so every gradient is exactly 0."""
+    from unet_amd import WeightedCrossEntropyLoss
+    params = O.hash_init(1, 1, seed=71, bn_random=True)
+    x, _, wmap = F.make_inputs(71, 2, 1, 188)
+    tgt = np.zeros((2, O.output_size(188), O.output_size(188)), np.int64)
+    m = make_model(params, 1, 1)
+    m.train()
+    loss = WeightedCrossEntropyLoss()(m(torch.from_numpy(x).cuda()), torch.from_numpy(tgt).cuda(),
+                                      torch.from_numpy(wmap).cuda())
+    loss.backward()
+    assert loss.item() == 0.0
+    for name, p in m.named_parameters():
+        assert float(p.grad.abs().max()) == 0.0, name
