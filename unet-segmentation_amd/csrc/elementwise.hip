@@ -702,7 +702,8 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
   if (c != 64) return hipErrorInvalidValue;
   const long long pixels = (long long)n * h * w;
   dim3 grid(grid_cap(pixels, 16 * 8, 2048));
-  hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
+  hipError_t me = hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
+  if (me != hipSuccess) return me;
   switch (k) {
     case 1: hipLaunchKernelGGL(k_head_bwd<1>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
     case 2: hipLaunchKernelGGL(k_head_bwd<2>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
@@ -770,7 +771,8 @@ hipError_t launch_wce(const float* logits, const int64_t* t, const float* wm, in
                       hipStream_t s) {
   const long long total = (long long)n * h * w;
   dim3 grid(grid_cap(total, 256 * 4, 2048));
-  hipMemsetAsync(acc, 0, sizeof(double), s);
+  hipError_t me = hipMemsetAsync(acc, 0, sizeof(double), s);
+  if (me != hipSuccess) return me;
   switch (k) {
     case 1: hipLaunchKernelGGL(k_wce<1>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
     case 2: hipLaunchKernelGGL(k_wce<2>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
@@ -1007,7 +1009,8 @@ __global__ void k_iou(const uint8_t* __restrict__ a, const uint8_t* __restrict__
   }
 }
 hipError_t launch_iou(const uint8_t* a, const uint8_t* b, size_t n, unsigned long long* out, hipStream_t s) {
-  hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), s);
+  hipError_t me = hipMemsetAsync(out, 0, 2 * sizeof(unsigned long long), s);
+  if (me != hipSuccess) return me;
   hipLaunchKernelGGL(k_iou, dim3(grid_cap((long long)n, 256, 1024)), dim3(256), 0, s, a, b, n, out);
   return hipGetLastError();
 }

@@ -145,19 +145,29 @@ struct Timer {
   unet_plan* p;
   hipStream_t s;
   hipEvent_t a{}, b{};
+  bool ok = false;
   int cls;
   double fl, by;
   Timer(unet_plan* p_, hipStream_t s_, int c, double f, double by_) : p(p_), s(s_), cls(c), fl(f), by(by_) {
+    // timing is best effort (bench / tools only): a failed event leaves the
+    // interval out of the report instead of failing the plan call
     if (p->timing) {
-      hipEventCreate(&a);
-      hipEventCreate(&b);
-      hipEventRecord(a, s);
+      ok = hipEventCreate(&a) == hipSuccess;
+      if (ok && hipEventCreate(&b) != hipSuccess) {
+        (void)hipEventDestroy(a);
+        ok = false;
+      }
+      if (ok) ok = hipEventRecord(a, s) == hipSuccess;
     }
   }
   ~Timer() {
-    if (p->timing) {
-      hipEventRecord(b, s);
-      p->evs.push_back({a, b, cls, fl, by});
+    if (p->timing && ok) {
+      if (hipEventRecord(b, s) == hipSuccess) {
+        p->evs.push_back({a, b, cls, fl, by});
+      } else {
+        (void)hipEventDestroy(a);
+        (void)hipEventDestroy(b);
+      }
     }
   }
 };
@@ -934,8 +944,8 @@ void unet_plan_destroy(unet_plan* p) {
     (void)hipStreamDestroy(p->side);
   }
   for (auto& e : p->evs) {
-    hipEventDestroy(e.a);
-    hipEventDestroy(e.b);
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
   }
   delete p;
 }
@@ -1015,16 +1025,20 @@ int unet_plan_set_timing(unet_plan* p, int enable) {
 int unet_plan_timing(const unet_plan* pc, double* ms, double* fl, double* by, int* cnt) {
   auto* p = const_cast<unet_plan*>(pc);
   if (!p) return -EINVAL;
+  int rc = 0;
   for (auto& e : p->evs) {
-    hipEventSynchronize(e.b);
     float t = 0;
-    hipEventElapsedTime(&t, e.a, e.b);
-    p->t_ms[e.cls] += t;
-    p->t_fl[e.cls] += e.flops;
-    p->t_by[e.cls] += e.bytes;
-    p->t_n[e.cls] += 1;
-    hipEventDestroy(e.a);
-    hipEventDestroy(e.b);
+    if (hipEventSynchronize(e.b) != hipSuccess || hipEventElapsedTime(&t, e.a, e.b) != hipSuccess) {
+      set_err("unet_plan_timing: event query failed");
+      rc = -EIO;
+    } else {
+      p->t_ms[e.cls] += t;
+      p->t_fl[e.cls] += e.flops;
+      p->t_by[e.cls] += e.bytes;
+      p->t_n[e.cls] += 1;
+    }
+    (void)hipEventDestroy(e.a);
+    (void)hipEventDestroy(e.b);
   }
   p->evs.clear();
   for (int i = 0; i < UNET_KC_COUNT; ++i) {
@@ -1035,7 +1049,7 @@ int unet_plan_timing(const unet_plan* pc, double* ms, double* fl, double* by, in
     p->t_ms[i] = p->t_fl[i] = p->t_by[i] = 0;
     p->t_n[i] = 0;
   }
-  return 0;
+  return rc;
 }
 
 }  // extern "C"
