@@ -221,6 +221,13 @@ def main():
                                          "profiles/pmc_traffic.json)",
                          "flops_per_step": conv_fl, "launches_per_step": launches,
                          "avg_launch_ms": round(conv_ms / max(launches, 1), 4)},
+            # SURVEY.md §8d target: >= 50 % MFMA on the 1024-channel bottleneck set
+            "bottleneck": {"layers": "down4.c0, down4.c1, up1.convT, up1.c0 (fwd + dgrad + wgrad)",
+                           "ms": round(tim["bottleneck"][0], 3),
+                           "tflops": round(tim["bottleneck"][1] / (tim["bottleneck"][0] * 1e-3) / 1e12, 2)
+                           if tim["bottleneck"][0] > 0 else None,
+                           "frac": round(tim["bottleneck"][1] / (tim["bottleneck"][0] * 1e-3) / 1e12 / peak, 4)
+                           if tim["bottleneck"][0] > 0 else None},
             "stage1": {"bound": "hbm", "ms": round(st[0], 3),
                        "achieved_gbs": round(st[2] / (st[0] * 1e-3) / 1e9, 1) if st[0] > 0 else None,
                        "peak_gbs": HBM_PEAK_GBS, "traffic": pmc.get("stage1")},

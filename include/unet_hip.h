@@ -111,7 +111,9 @@ enum {
   UNET_KC_CONV_FWD = 0, UNET_KC_CONV_DGRAD = 1, UNET_KC_CONV_WGRAD = 2,
   UNET_KC_STAGE1 = 3,   /* inc.c0 fwd + its BN/ReLU passes (memory-bound) */
   UNET_KC_ELEMWISE = 4, /* BN / pool / head / repack passes */
-  UNET_KC_COUNT = 5
+  UNET_KC_BOTTLENECK = 5, /* overlaps 0-2: the GEMMs of down4.c0, down4.c1,
+                             up1.convT, up1.c0 (SURVEY.md §8d's bottleneck set) */
+  UNET_KC_COUNT = 6
 };
 int unet_plan_set_timing(unet_plan* p, int enable);
 int unet_plan_timing(const unet_plan* p, double* ms, double* flops, double* bytes, int* launches);

@@ -141,6 +141,10 @@ struct Ctx {
     }                                                           \
   } while (0)
 
+// the 1024-channel bottleneck set of SURVEY.md §8d: down4.c0, down4.c1, up1.c0
+// (and up1.convT, ConvT index 0)
+inline bool bottleneck_conv(int l) { return l == 8 || l == 9 || l == 10; }
+
 struct Timer {
   unet_plan* p;
   hipStream_t s;
@@ -148,10 +152,11 @@ struct Timer {
   bool ok = false;
   int cls;
   double fl, by;
-  Timer(unet_plan* p_, hipStream_t s_, int c, double f, double by_) : p(p_), s(s_), cls(c), fl(f), by(by_) {
+  Timer(unet_plan* p_, hipStream_t s_, int c, double f, double by_, bool on = true)
+      : p(p_), s(s_), cls(c), fl(f), by(by_) {
     // timing is best effort (bench / tools only): a failed event leaves the
     // interval out of the report instead of failing the plan call
-    if (p->timing) {
+    if (p->timing && on) {
       ok = hipEventCreate(&a) == hipSuccess;
       if (ok && hipEventCreate(&b) != hipSuccess) {
         (void)hipEventDestroy(a);
@@ -490,6 +495,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       a.e.shuffle_co = T.co;
       a.e.d[0] = Dst{c.f(T.u), 2 * T.h, 2 * T.w, T.co, 0, 0, p->prec == UNET_PREC_BF16};
       Timer t(p, s, UNET_KC_CONV_FWD, 2.0 * a.M * a.N * a.K, 0);
+      Timer tb(p, s, UNET_KC_BOTTLENECK, 2.0 * a.M * a.N * a.K, 0, k == 0);
       CK(run_igemm(c, a));
     }
     IgemmArgs a;
@@ -503,6 +509,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
     a.e.stats = train ? c.d(L.stats) : nullptr;
     {
       Timer t(p, s, UNET_KC_CONV_FWD, conv_flops(L, n), 0);
+      Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
       CK(run_igemm(c, a));
     }
     if (int r = finalize(l)) return r;
@@ -609,6 +616,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       w.P = n * L.ho * L.wo;
       w.out = c.f(L.dwp);
       Timer t(p, sw, UNET_KC_CONV_WGRAD, conv_flops(L, n), 0);
+      Timer tb(p, sw, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
       CK(run_wgrad(cw, w));
     }
     CK(launch_permute_last2(c.f(L.dwp), L.co, 9, L.ci, P<float>(grd, L.gw), sw));
@@ -637,6 +645,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       a.e.bn_invstd = c.f(Q.invstd);
       a.e.bstats = c.d(Q.bstats);
       Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+      Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
       CK(run_igemm(c, a));
     } else if (l <= 8) {  // -> gradient of the pooled tensor, then pool backward
       const int k = l / 2 - 1;
@@ -644,6 +653,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       a.e.d[0] = Dst{c.f(pl.dp), pl.h / 2, pl.w / 2, pl.c, 0, 0};
       {
         Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+        Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
         CK(run_igemm(c, a));
       }
       Conv& Q = p->L[l - 1];  // encoder output feeding this pool (and a skip)
@@ -662,6 +672,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       a.e.colsum1 = c.d(T.colsum);
       {
         Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+        Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
         CK(run_igemm(c, a));
       }
       CK(launch_colsum(c.d(T.colsum), kStatGroups, T.co, P<float>(grd, T.gw + 1), s));
@@ -698,6 +709,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
         w.P = n * T.h * T.w;
         w.out = c.f(T.dwp);
         Timer t(p, sw, UNET_KC_CONV_WGRAD, 2.0 * w.P * (double)w.Mo * w.No, 0);
+        Timer tb(p, sw, UNET_KC_BOTTLENECK, 2.0 * w.P * (double)w.Mo * w.No, 0, k == 0);
         CK(run_wgrad(cw, w));
       }
       CK(launch_permute_last2(c.f(T.dwp), T.ci, 4, T.co, P<float>(grd, T.gw), sw));
@@ -730,6 +742,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       b.e.bn_invstd = c.f(Q.invstd);
       b.e.bstats = c.d(Q.bstats);
       Timer t(p, s, UNET_KC_CONV_DGRAD, 2.0 * b.M * (double)b.N * b.K, 0);
+      Timer tb(p, s, UNET_KC_BOTTLENECK, 2.0 * b.M * (double)b.N * b.K, 0, k == 0);
       CK(run_igemm(c, b));
     }
   }

@@ -100,7 +100,8 @@ __global__ void k_cc_label(size_t total, size_t hw, const int* __restrict__ pare
 size_t instance_masks_ws_bytes(int n, int h, int w) {
   const size_t total = (size_t)n * h * w;
   size_t scan = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int*)nullptr, (int*)nullptr, (int)total);
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int*)nullptr, (int*)nullptr, (int)total) != hipSuccess)
+    return 0;  // the launch then fails on the missing workspace
   return 4 * (total * 4 + 256) + scan + 256;
 }
 
@@ -120,10 +121,11 @@ hipError_t launch_instance_masks(const uint8_t* mask, int n, int h, int w, int m
   int* rank = reinterpret_cast<int*>(carve(p, total * 4));
   unsigned* size = reinterpret_cast<unsigned*>(carve(p, total * 4));
   size_t scan = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, is_root, rank, (int)total, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan, is_root, rank, (int)total, s);
+  if (e != hipSuccess) return e;
   void* tmp = carve(p, scan);
   const unsigned g = (unsigned)((total + 255) / 256);
-  hipError_t e = hipMemsetAsync(size, 0, total * 4, s);
+  e = hipMemsetAsync(size, 0, total * 4, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_cc_init, dim3(g), dim3(256), 0, s, mask, total, parent);
   hipLaunchKernelGGL(k_cc_union, dim3(g), dim3(256), 0, s, mask, n, h, w, parent);
@@ -191,7 +193,8 @@ __global__ void k_ri_final(const unsigned long long* __restrict__ acc, size_t n,
 
 size_t rand_index_ws_bytes(int h, int w) {
   size_t scan = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int*)nullptr, (int*)nullptr, kLabels + 1);
+  if (hipcub::DeviceScan::ExclusiveSum(nullptr, scan, (const int*)nullptr, (int*)nullptr, kLabels + 1) != hipSuccess)
+    return 0;  // the launch then fails on the missing workspace
   (void)h;
   (void)w;
   return 4 * ((size_t)(kLabels + 1) * 4 + 256) + 2 * ((size_t)kLabels * 4 + 256) + (size_t)kMaxCells * 4 + 256 +
@@ -212,9 +215,9 @@ hipError_t launch_rand_index(const uint16_t* g, const uint16_t* p, int h, int w,
   unsigned* table = reinterpret_cast<unsigned*>(carve(c, (size_t)kMaxCells * 4));
   auto* acc = reinterpret_cast<unsigned long long*>(carve(c, 64));
   size_t scan = 0;
-  hipcub::DeviceScan::ExclusiveSum(nullptr, scan, pg, ig, kLabels + 1, s);
+  hipError_t e = hipcub::DeviceScan::ExclusiveSum(nullptr, scan, pg, ig, kLabels + 1, s);
+  if (e != hipSuccess) return e;
   void* tmp = carve(c, scan);
-  hipError_t e;
   for (void* z : {(void*)pg, (void*)pp, (void*)rows, (void*)cols}) {
     e = hipMemsetAsync(z, 0, (z == rows || z == cols) ? kLabels * 4 : (kLabels + 1) * 4, s);
     if (e != hipSuccess) return e;

@@ -60,11 +60,11 @@ class Plan:
 
     def timing(self):
         """{class: (ms, flops, bytes, launches)} accumulated since the last call."""
-        n = 5
+        n = 6
         ms = (ctypes.c_double * n)()
         fl = (ctypes.c_double * n)()
         by = (ctypes.c_double * n)()
         cnt = (ctypes.c_int * n)()
         _lib.check(self.lib.unet_plan_timing(self.handle, ms, fl, by, cnt), "unet_plan_timing")
-        names = ["conv_fwd", "conv_dgrad", "conv_wgrad", "stage1", "elementwise"]
+        names = ["conv_fwd", "conv_dgrad", "conv_wgrad", "stage1", "elementwise", "bottleneck"]
         return {names[i]: (ms[i], fl[i], by[i], cnt[i]) for i in range(n)}
