@@ -103,8 +103,8 @@ def pmc_traffic(args):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--batch", type=int, default=8, help="images per GPU")
     ap.add_argument("--size", type=int, default=512)
     ap.add_argument("--channels", type=int, default=1, help="input channels (configs[4]: 3)")
@@ -220,7 +220,11 @@ def main():
                          "traffic_unit": "HBM bytes/launch (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, "
                                          "profiles/pmc_traffic.json)",
                          "flops_per_step": conv_fl, "launches_per_step": launches,
-                         "avg_launch_ms": round(conv_ms / max(launches, 1), 4)},
+                         "avg_launch_ms": round(conv_ms / max(launches, 1), 4),
+                         "timing": "HIP events on the plan's stream over one extra step after the timed steps, "
+                                   "weight-gradient side stream serialised; in the timed steps wgrad overlaps dgrad "
+                                   "on a second stream (per-dispatch times then overlap: "
+                                   "profiles/r01_trace_check*.txt)"},
             # SURVEY.md §8d target: >= 50 % MFMA on the 1024-channel bottleneck set
             "bottleneck": {"layers": "down4.c0, down4.c1, up1.convT, up1.c0 (fwd + dgrad + wgrad)",
                            "ms": round(tim["bottleneck"][0], 3),
