@@ -336,31 +336,33 @@ template <int H16, int Y16>  // H16: dYpad stored bf16; Y16: y stored bf16
 __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restrict__ yr,
                             const float* __restrict__ coef, int n, int h, int w, int C,
                             float* __restrict__ dyp, int pad) {
+  // grid: x over one padded row's (pixel, 4-channel group) pairs, y over padded
+  // rows; one division per row instead of per element
   const int C4 = C / 4;
-  const int hp = h + 2 * pad, wp = w + 2 * pad;
-  const long long total = (long long)n * hp * wp * C4;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(i % C4);
-    long long p = i / C4;
-    const int xp = (int)(p % wp);
-    p /= wp;
-    const int yp = (int)(p % hp);
-    const int nn = (int)(p / hp);
-    const int yy = yp - pad, xx = xp - pad;
+  const int hp = h + 2 * pad, wp = w + 2 * pad, rowlen = wp * C4;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= rowlen) return;
+  const int xp = j / C4, c4 = j - xp * C4, xx = xp - pad;
+  float4 k0, k1, k2, mu;
+  const bool colin = xx >= 0 && xx < w;
+  if (colin) {
+    k0 = ld4(coef + c4 * 4); k1 = ld4(coef + C + c4 * 4); k2 = ld4(coef + 2 * C + c4 * 4);
+    mu = ld4(coef + 3 * C + c4 * 4);
+  }
+  for (int r = blockIdx.y; r < n * hp; r += gridDim.y) {
+    const int nn = r / hp, yy = r - nn * hp - pad;
     float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (yy >= 0 && yy < h && xx >= 0 && xx < w) {
+    if (colin && yy >= 0 && yy < h) {
       const size_t src = (((size_t)nn * h + yy) * w + xx) * C + c4 * 4;
       const float4 d = ld4(dz + src);
       const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + src))
                             : ld4(yr + src);
-      const float4 k0 = ld4(coef + c4 * 4), k1 = ld4(coef + C + c4 * 4), k2 = ld4(coef + 2 * C + c4 * 4),
-                   mu = ld4(coef + 3 * C + c4 * 4);
       out.x = fmaf(k0.x, d.x, fmaf(k1.x, yv.x - mu.x, k2.x));
       out.y = fmaf(k0.y, d.y, fmaf(k1.y, yv.y - mu.y, k2.y));
       out.z = fmaf(k0.z, d.z, fmaf(k1.z, yv.z - mu.z, k2.z));
       out.w = fmaf(k0.w, d.w, fmaf(k1.w, yv.w - mu.w, k2.w));
     }
+    const size_t i = (size_t)r * rowlen + j;
     if (H16)
       reinterpret_cast<uint2*>(dyp)[i] = make_uint2(bf16pack(out.x, out.y), bf16pack(out.z, out.w));
     else
@@ -391,8 +393,11 @@ hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const 
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h, int w, int c,
                             float* dypad, int pad, hipStream_t s, int out_h16, int y_h16) {
   if (c % 4) return hipErrorInvalidValue;
-  const long long work = (long long)n * (h + 2 * pad) * (w + 2 * pad) * (c / 4);
-  const dim3 grid(grid_cap(work, 256, 8192));
+  const long long rowlen = (long long)(w + 2 * pad) * (c / 4), rows = (long long)n * (h + 2 * pad);
+  if (rows >= (1LL << 31) || rowlen >= (1LL << 31)) return hipErrorInvalidValue;
+  const int gx = (int)((rowlen + 255) / 256);
+  // ~4 rows per block keeps the row loop short while filling the chip
+  const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max<long long>(1, 32768 / gx))));
   switch (out_h16 * 2 + y_h16) {
     case 0: hipLaunchKernelGGL((k_bnb_apply<0, 0>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad); break;
     case 1: hipLaunchKernelGGL((k_bnb_apply<0, 1>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad); break;
@@ -480,51 +485,57 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
   const int C4 = C / 4;            // channel groups; C4 divides 256 (C <= 1024, power of 2)
   const int tid = threadIdx.x;
   const int cg = tid % C4;
-  const int ppb = 256 / C4;        // pixels per block iteration
+  const int ppb = 256 / C4;        // pixels of one row per block
   const int ho = h / 2, wo = w / 2;
-  const long long pixels = (long long)n * h * w;
   float sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
   const int c = cg * 4;
   float4 sc = make_float4(0, 0, 0, 0), sf = sc, mu = sc, is = sc;
   if (scale) { sc = ld4(scale + c); sf = ld4(shift + c); mu = ld4(mean + c); is = ld4(invstd + c); }
-  for (long long p = (long long)blockIdx.x * ppb + tid / C4; p < pixels; p += (long long)gridDim.x * ppb) {
-    const int xx = (int)(p % w);
-    const long long t = p / w;
-    const int yy = (int)(t % h);
-    const int nn = (int)(t / h);
-    float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int yo = yy >> 1, xo = xx >> 1;
-    if (yo < ho && xo < wo) {
-      const size_t pi = (((size_t)nn * ho + yo) * wo + xo) * C + c;
-      const uchar4 a = *reinterpret_cast<const uchar4*>(arg + pi);
-      const float4 g = ld4(dpool + pi);
-      const int k = (yy & 1) * 2 + (xx & 1);
-      d.x = (a.x == k) ? g.x : 0.f;
-      d.y = (a.y == k) ? g.y : 0.f;
-      d.z = (a.z == k) ? g.z : 0.f;
-      d.w = (a.w == k) ? g.w : 0.f;
+  // grid: x over ppb-pixel segments of a row, y over rows (n*h); the row index
+  // is the only division
+  const int xx = blockIdx.x * ppb + tid / C4;
+  if (xx < w) {
+    const int xo = xx >> 1;
+    const bool in_skip_x = dskip && xx >= sox && xx < sox + sw;
+    for (int r = blockIdx.y; r < n * h; r += gridDim.y) {
+      const int nn = r / h, yy = r - nn * h;
+      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+      const int yo = yy >> 1;
+      if (yo < ho && xo < wo) {
+        const size_t pi = (((size_t)nn * ho + yo) * wo + xo) * C + c;
+        const uchar4 a = *reinterpret_cast<const uchar4*>(arg + pi);
+        const float4 g = ld4(dpool + pi);
+        const int k = (yy & 1) * 2 + (xx & 1);
+        d.x = (a.x == k) ? g.x : 0.f;
+        d.y = (a.y == k) ? g.y : 0.f;
+        d.z = (a.z == k) ? g.z : 0.f;
+        d.w = (a.w == k) ? g.w : 0.f;
+      }
+      if (in_skip_x && yy >= soy && yy < soy + sh) {
+        const float4 g = ld4(dskip + (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c);
+        d.x += g.x; d.y += g.y; d.z += g.z; d.w += g.w;
+      }
+      const size_t oi = ((size_t)r * w + xx) * C + c;
+      if (scale) {
+        const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
+                              : ld4(yr + oi);
+        d.x = (fmaf(yv.x, sc.x, sf.x) > 0.f) ? d.x : 0.f;
+        d.y = (fmaf(yv.y, sc.y, sf.y) > 0.f) ? d.y : 0.f;
+        d.z = (fmaf(yv.z, sc.z, sf.z) > 0.f) ? d.z : 0.f;
+        d.w = (fmaf(yv.w, sc.w, sf.w) > 0.f) ? d.w : 0.f;
+        sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
+        sb[0] += d.x * (yv.x - mu.x) * is.x;
+        sb[1] += d.y * (yv.y - mu.y) * is.y;
+        sb[2] += d.z * (yv.z - mu.z) * is.z;
+        sb[3] += d.w * (yv.w - mu.w) * is.w;
+      }
+      st4(dz + oi, d);
     }
-    if (dskip && yy >= soy && yy < soy + sh && xx >= sox && xx < sox + sw) {
-      const float4 g = ld4(dskip + (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c);
-      d.x += g.x; d.y += g.y; d.z += g.z; d.w += g.w;
-    }
-    const size_t oi = (size_t)p * C + c;
-    if (scale) {
-      const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
-                            : ld4(yr + oi);
-      d.x = (fmaf(yv.x, sc.x, sf.x) > 0.f) ? d.x : 0.f;
-      d.y = (fmaf(yv.y, sc.y, sf.y) > 0.f) ? d.y : 0.f;
-      d.z = (fmaf(yv.z, sc.z, sf.z) > 0.f) ? d.z : 0.f;
-      d.w = (fmaf(yv.w, sc.w, sf.w) > 0.f) ? d.w : 0.f;
-      sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
-      sb[0] += d.x * (yv.x - mu.x) * is.x;
-      sb[1] += d.y * (yv.y - mu.y) * is.y;
-      sb[2] += d.z * (yv.z - mu.z) * is.z;
-      sb[3] += d.w * (yv.w - mu.w) * is.w;
-    }
-    st4(dz + oi, d);
   }
-  if (bstats) reduce_pairs_to_global(sa, sb, C4, C, bstats + (size_t)(blockIdx.x % kStatGroups) * C * 2);
+  // every thread of the block takes part in the reduction (out-of-row lanes add zeros)
+  if (bstats)
+    reduce_pairs_to_global(sa, sb, C4, C,
+                           bstats + (size_t)((blockIdx.y * gridDim.x + blockIdx.x) % kStatGroups) * C * 2);
 }
 
 hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, const float* dskip, int soy, int sox,
@@ -532,9 +543,12 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
                                     const float* mean, const float* invstd, int n, int h, int w, int c, float* dz,
                                     double* bstats, hipStream_t s, int y_h16) {
   if (c % 4 || (256 % (c / 4)) != 0) return hipErrorInvalidValue;
-  const long long pixels = (long long)n * h * w;
+  const long long rows = (long long)n * h;
+  if (rows * w >= (1LL << 31)) return hipErrorInvalidValue;
   const int ppb = 256 / (c / 4);
-  const dim3 grid(grid_cap(pixels, ppb * 4, 4096));
+  const int gx = (w + ppb - 1) / ppb;
+  // ~4096 blocks in all (the fp64 BN-statistics atomics scale with the block count)
+  const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max(1, 4096 / gx))));
   if (y_h16)
     hipLaunchKernelGGL(k_maxpool_bwd_fused<1>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
                        shift, mean, invstd, n, h, w, c, dz, bstats);
