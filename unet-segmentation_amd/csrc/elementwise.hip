@@ -491,45 +491,62 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
   const int c = cg * 4;
   float4 sc = make_float4(0, 0, 0, 0), sf = sc, mu = sc, is = sc;
   if (scale) { sc = ld4(scale + c); sf = ld4(shift + c); mu = ld4(mean + c); is = ld4(invstd + c); }
-  // grid: x over ppb-pixel segments of a row, y over rows (n*h); the row index
-  // is the only division
+  // grid: x over ppb-pixel segments of a row, y over row pairs (the two input
+  // rows of one pooled row; an odd last row is alone): the pooled gradient and
+  // argmax are read once for both rows, and both rows' loads are in flight
+  // together.  The row-pair index is the only division.
   const int xx = blockIdx.x * ppb + tid / C4;
+  const int hq = (h + 1) / 2;
   if (xx < w) {
     const int xo = xx >> 1;
     const bool in_skip_x = dskip && xx >= sox && xx < sox + sw;
-    for (int r = blockIdx.y; r < n * h; r += gridDim.y) {
-      const int nn = r / h, yy = r - nn * h;
-      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
-      const int yo = yy >> 1;
+    for (int q = blockIdx.y; q < n * hq; q += gridDim.y) {
+      const int nn = q / hq, yo = q - nn * hq;
+      uchar4 a = make_uchar4(255, 255, 255, 255);
+      float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
       if (yo < ho && xo < wo) {
         const size_t pi = (((size_t)nn * ho + yo) * wo + xo) * C + c;
-        const uchar4 a = *reinterpret_cast<const uchar4*>(arg + pi);
-        const float4 g = ld4(dpool + pi);
-        const int k = (yy & 1) * 2 + (xx & 1);
-        d.x = (a.x == k) ? g.x : 0.f;
-        d.y = (a.y == k) ? g.y : 0.f;
-        d.z = (a.z == k) ? g.z : 0.f;
-        d.w = (a.w == k) ? g.w : 0.f;
+        a = *reinterpret_cast<const uchar4*>(arg + pi);
+        g = ld4(dpool + pi);
       }
-      if (in_skip_x && yy >= soy && yy < soy + sh) {
-        const float4 g = ld4(dskip + (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c);
-        d.x += g.x; d.y += g.y; d.z += g.z; d.w += g.w;
+      float4 d[2], yv[2];
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int yy = 2 * yo + k;
+        d[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+        yv[k] = d[k];
+        if (yy >= h) continue;
+        if (in_skip_x && yy >= soy && yy < soy + sh)
+          d[k] = ld4(dskip + (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c);
+        const size_t oi = (((size_t)nn * h + yy) * w + xx) * C + c;
+        if (scale)
+          yv[k] = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
+                      : ld4(yr + oi);
       }
-      const size_t oi = ((size_t)r * w + xx) * C + c;
-      if (scale) {
-        const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
-                              : ld4(yr + oi);
-        d.x = (fmaf(yv.x, sc.x, sf.x) > 0.f) ? d.x : 0.f;
-        d.y = (fmaf(yv.y, sc.y, sf.y) > 0.f) ? d.y : 0.f;
-        d.z = (fmaf(yv.z, sc.z, sf.z) > 0.f) ? d.z : 0.f;
-        d.w = (fmaf(yv.w, sc.w, sf.w) > 0.f) ? d.w : 0.f;
-        sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
-        sb[0] += d.x * (yv.x - mu.x) * is.x;
-        sb[1] += d.y * (yv.y - mu.y) * is.y;
-        sb[2] += d.z * (yv.z - mu.z) * is.z;
-        sb[3] += d.w * (yv.w - mu.w) * is.w;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int yy = 2 * yo + k;
+        if (yy >= h) continue;
+        const int sel = k * 2 + (xx & 1);  // window position of this pixel (argmax byte 255: not pooled)
+        float4 dd = d[k];
+        dd.x += (a.x == sel) ? g.x : 0.f;
+        dd.y += (a.y == sel) ? g.y : 0.f;
+        dd.z += (a.z == sel) ? g.z : 0.f;
+        dd.w += (a.w == sel) ? g.w : 0.f;
+        if (scale) {
+          const float4 y4 = yv[k];
+          dd.x = (fmaf(y4.x, sc.x, sf.x) > 0.f) ? dd.x : 0.f;
+          dd.y = (fmaf(y4.y, sc.y, sf.y) > 0.f) ? dd.y : 0.f;
+          dd.z = (fmaf(y4.z, sc.z, sf.z) > 0.f) ? dd.z : 0.f;
+          dd.w = (fmaf(y4.w, sc.w, sf.w) > 0.f) ? dd.w : 0.f;
+          sa[0] += dd.x; sa[1] += dd.y; sa[2] += dd.z; sa[3] += dd.w;
+          sb[0] += dd.x * (y4.x - mu.x) * is.x;
+          sb[1] += dd.y * (y4.y - mu.y) * is.y;
+          sb[2] += dd.z * (y4.z - mu.z) * is.z;
+          sb[3] += dd.w * (y4.w - mu.w) * is.w;
+        }
+        st4(dz + (((size_t)nn * h + yy) * w + xx) * C + c, dd);
       }
-      st4(dz + oi, d);
     }
   }
   // every thread of the block takes part in the reduction (out-of-row lanes add zeros)
@@ -543,8 +560,8 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
                                     const float* mean, const float* invstd, int n, int h, int w, int c, float* dz,
                                     double* bstats, hipStream_t s, int y_h16) {
   if (c % 4 || (256 % (c / 4)) != 0) return hipErrorInvalidValue;
-  const long long rows = (long long)n * h;
-  if (rows * w >= (1LL << 31)) return hipErrorInvalidValue;
+  const long long rows = (long long)n * ((h + 1) / 2);  // row pairs
+  if ((long long)n * h * w >= (1LL << 31)) return hipErrorInvalidValue;
   const int ppb = 256 / (c / 4);
   const int gx = (w + ppb - 1) / ppb;
   // ~4096 blocks in all (the fp64 BN-statistics atomics scale with the block count)
