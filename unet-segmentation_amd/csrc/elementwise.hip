@@ -564,8 +564,11 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
   if ((long long)n * h * w >= (1LL << 31)) return hipErrorInvalidValue;
   const int ppb = 256 / (c / 4);
   const int gx = (w + ppb - 1) / ppb;
-  // ~4096 blocks in all (the fp64 BN-statistics atomics scale with the block count)
-  const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max(1, 4096 / gx))));
+  // ~1024 blocks in all: every block ends in 2*C fp64 BN-statistics atomics, and
+  // those, not the HBM streams, set this kernel's time at larger grids (measured
+  // per step at 512^2 x 8: 256 blocks 1.14 ms, 512 0.73, 1024 0.54, 2048 0.71,
+  // 4096 0.80, 16384 1.28)
+  const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max(1, 1024 / gx))));
   if (y_h16)
     hipLaunchKernelGGL(k_maxpool_bwd_fused<1>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
                        shift, mean, invstd, n, h, w, c, dz, bstats);
@@ -732,7 +735,9 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
   (void)yraw;
   if (c != 64) return hipErrorInvalidValue;
   const long long pixels = (long long)n * h * w;
-  dim3 grid(grid_cap(pixels, 16 * 8, 2048));
+  // 512 blocks: the per-block fp64 atomics (BN statistics, dW, db) bound this
+  // kernel at larger grids (measured: 256 blocks 199 us, 512 146 us, 2048 236 us)
+  dim3 grid(grid_cap(pixels, 16 * 8, 512));
   hipError_t me = hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
   if (me != hipSuccess) return me;
   switch (k) {
