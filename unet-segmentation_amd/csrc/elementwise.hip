@@ -944,9 +944,32 @@ __global__ void k_permute_small_b(const float* __restrict__ in, long long AC, in
   }
 }
 
+// out[a][c][b] = in[a][b][c] with one block per a: the B x C slab is read and
+// written contiguously (coalesced both ways) through LDS, rows padded to C + 1
+// words so the transposed reads spread over the banks.  Used when one of B, C is
+// a tap count (<= 16) and the slab fits 64 KiB.
+__global__ __launch_bounds__(256) void k_permute_slab(const float* __restrict__ in, int B, int C,
+                                                      float* __restrict__ out) {
+  extern __shared__ float slab[];
+  const size_t base = (size_t)blockIdx.x * B * C;
+  const int BC = B * C;
+  for (int i = threadIdx.x; i < BC; i += 256) {
+    const int b = i / C, c = i - b * C;
+    slab[b * (C + 1) + c] = in[base + i];
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < BC; i += 256) {
+    const int c = i / B, b = i - c * B;
+    out[base + i] = slab[b * (C + 1) + c];
+  }
+}
+
 hipError_t launch_permute_last2(const float* in, int A, int B, int C, float* out, hipStream_t s) {
   if (A <= 0 || B <= 0 || C <= 0) return hipErrorInvalidValue;
-  if (C <= 16) {
+  const size_t slab_bytes = sizeof(float) * (size_t)B * (C + 1);
+  if ((B <= 16 || C <= 16) && slab_bytes <= 65536 && A <= 0x7fffffff) {
+    hipLaunchKernelGGL(k_permute_slab, dim3(A), dim3(256), slab_bytes, s, in, B, C, out);
+  } else if (C <= 16) {
     const long long ab = (long long)A * B;
     hipLaunchKernelGGL(k_permute_small_c, dim3(grid_cap(ab, 256, 8192)), dim3(256), 0, s, in, ab, B, C, out);
   } else if (B <= 16) {
