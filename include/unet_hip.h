@@ -75,9 +75,15 @@ enum { UNET_PREC_FP32 = 0, UNET_PREC_BF16 = 1, UNET_PREC_BF16X3 = 2 };
 unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int precision);
 int unet_plan_precision(const unet_plan* p);
 void unet_plan_destroy(unet_plan* p);
-/* Output spatial size and the workspace the caller must provide. */
+/* Output spatial size and the workspace the caller must provide.
+ * unet_plan_workspace_bytes: a forward followed by unet_plan_backward.
+ * unet_plan_forward_workspace_bytes: a forward that no backward follows (eval
+ * mode -- scripts/predict.py -- or a train-mode forward under torch.no_grad);
+ * a prefix of the full layout, about 1/3 of it (the gradient buffers are left
+ * out).  Running unet_plan_backward on such a workspace is undefined. */
 int unet_plan_out_hw(const unet_plan* p, int* out_h, int* out_w);
 size_t unet_plan_workspace_bytes(const unet_plan* p);
+size_t unet_plan_forward_workspace_bytes(const unet_plan* p);
 int unet_plan_num_params(const unet_plan* p);  /* 136 (state_dict entries) */
 int unet_plan_num_grads(const unet_plan* p);   /* 82 */
 
@@ -131,6 +137,9 @@ int unet_wce_fwd_bwd(const float* logits, const int64_t* targets, const float* w
                      unet_stream_t stream);
 /* dlogits *= g[0] (the upstream scalar gradient, device), in place. */
 int unet_scale_by_device_scalar(float* x, size_t n, const float* g, unet_stream_t stream);
+/* y = x * g[0] (y may alias x): the loss backward scales into a fresh tensor so
+ * the saved gradient survives a second backward (retain_graph=True). */
+int unet_scale_by_device_scalar_out(const float* x, float* y, size_t n, const float* g, unet_stream_t stream);
 
 /* SGD with momentum (torch.optim.SGD, dampening 0, no weight decay), flat,
  * on the gradient g*grad_scale (grad_scale = 1/world after a SUM all-reduce):
@@ -208,6 +217,42 @@ int unet_instance_masks(const uint8_t* mask, int n, int h, int w, int min_size, 
 size_t unet_rand_index_ws_bytes(int h, int w);
 int unet_rand_index(const uint16_t* gt, const uint16_t* pred, int h, int w, double* out, void* ws,
                     unet_stream_t stream);
+
+/* Cell tracking (scripts/track.py:103-275): a tracker
+ * consumes the instance labelings of a sequence frame by frame and keeps the
+ * lineage (CellTrack :27-36).  Per frame the GPU builds the overlap table of
+ * the previous and current objects in one pass (replacing calculate_mask_iou,
+ * :73-100, per object pair); the host side runs the reference's control flow:
+ * IoU cost matrix (1 - IoU, 1000 where no overlap), linear sum assignment,
+ * links with IoU >= iou_track, divisions (an unmatched parent overlapping 2..
+ * max_children unmatched objects with IoU >= iou_division), new tracks.
+ *   unet_tracker_create(h, w, 0.3, 0.1, 2) = the reference's constants
+ *     (:21-24).  NULL for bad sizes.
+ *   unet_tracker_add_frame: labels (h, w) uint16 on the device; frame = the
+ *     frame number (the reference parses it from mXXX.tif); synchronises the
+ *     stream; ws >= unet_tracker_ws_bytes(h, w) bytes, kept for the whole
+ *     sequence (it holds the previous frame).
+ *   unet_tracker_step_host: the same step from host data -- the current
+ *     objects' labels (ascending, > 0), areas, and the overlap counts
+ *     inter[i * n_curr + j] with the previous step's objects (NULL on the
+ *     first frame).  Host only (no device work).
+ *   unet_tracker_tracks: writes up to cap rows (label, start, end, parent) in
+ *     the res_track.txt order (start frame, then label; end >= start);
+ *     returns the track count.
+ * unet_linear_sum_assignment: scipy.optimize.linear_sum_assignment's
+ *   minimisation on a row-major nr x nc fp64 cost matrix (host pointers,
+ *   min(nr, nc) pairs sorted by row); -EINVAL for NaN / -inf / infeasible. */
+typedef struct unet_tracker unet_tracker;
+unet_tracker* unet_tracker_create(int h, int w, double iou_track, double iou_division, int max_children);
+void unet_tracker_destroy(unet_tracker* t);
+size_t unet_tracker_ws_bytes(int h, int w);
+int unet_tracker_add_frame(unet_tracker* t, const uint16_t* labels, int frame, void* ws, unet_stream_t stream);
+int unet_tracker_step_host(unet_tracker* t, int frame, int n_curr, const int32_t* host_labels,
+                           const int64_t* host_areas, const int64_t* host_inter);
+int unet_tracker_num_tracks(const unet_tracker* t);
+int unet_tracker_tracks(const unet_tracker* t, int32_t* host_out, int cap);
+int unet_linear_sum_assignment(long long nr, long long nc, const double* host_cost, int64_t* host_row_ind,
+                               int64_t* host_col_ind);
 
 /* Tuning hooks, process-global:
  *  "autotune"      1 (default, or env UNET_AUTOTUNE) = the plan times the

@@ -68,3 +68,18 @@ def weightmap_synthetic_cases():
     empty = np.zeros((17, 23), np.uint16)
     full = np.full((9, 11), 5, np.uint16)
     return {"multi": multi, "one": one, "empty": empty, "full": full}
+
+
+def plausible_running_stats(params, seed):
+    """Replace the BatchNorm running statistics of a hash-initialised parameter
+    set with plausible ones (mean ~ N(0, 0.2), var ~ 0.5 + U[0,1)), so that
+    eval-mode forwards (tile farm fixtures) are not degenerate.  Deterministic
+    (counter hash), shared by the fixture generator and the tests."""
+    out = dict(params)
+    for i, k in enumerate(sorted(params)):
+        n = int(np.prod(params[k].shape))
+        if k.endswith("running_mean"):
+            out[k] = (0.2 * O.hash_normal(seed, 5000 + i, n)).astype(np.float32).reshape(params[k].shape)
+        elif k.endswith("running_var"):
+            out[k] = (0.5 + O.hash_uniform(seed, 5000 + i, n)).astype(np.float32).reshape(params[k].shape)
+    return out

@@ -11,10 +11,13 @@ Restates utils/metrics.py:
   ``skimage.morphology.remove_small_objects(labels, min_size=15)``, which zeroes
   every component with fewer than ``min_size`` pixels WITHOUT renumbering the
   others, and a uint16 cast.  scikit-image is not installed in this image (the
-  reference module cannot be imported here), so the labelling is pinned to
-  ``scipy.ndimage.label`` with a 3x3 structure, which numbers components the
-  same way (tests/test_oracle_postproc.py); the small-object rule is skimage's
-  published one (``component_sizes < min_size`` are removed).
+  reference module cannot be imported here), so the labelling is checked
+  against ``scipy.ndimage.label`` with a 3x3 structure, which numbers components
+  the same way, and -- the pin -- against the reference's OWN outputs: its 84
+  committed ``01_RES/mask*.tif`` -> ``01_RES_INST/m*.tif`` pairs
+  (scripts/predict.py:92-112 with min_size=15; tests/golden/hela_postproc.npz)
+  are reproduced bit-exactly (tests/test_oracle_postproc.py); the small-object
+  rule is skimage's published one (``component_sizes < min_size`` are removed).
 * ``calculate_rand_index_and_error`` (:75-139): contingency table of the two
   labelings; a = sum n_ij (n_ij - 1) / 2, same_gt / same_pred the row / column
   analogues, b = total - same_gt - same_pred + a, RI = (a + b) / total with

@@ -1,0 +1,64 @@
+"""One rank of the data-parallel GPU test (tests/test_gpu_dp.py): the product
+DP path -- unet_amd.train.Trainer with a process group, its segmented
+backward, the bucketed asynchronous all-reduce and the 1/world SGD scale --
+on this rank's shard.  Ranks share the one GPU of the test box and talk over
+gloo (RCCL needs one GPU per rank; the all-reduce call pattern is the same).
+
+    python tests/dp_worker.py <out.npz> <overlap 0|1> <steps>
+    env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT
+"""
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path.insert(0, os.path.join(ROOT, "unet-segmentation_amd"))
+sys.path.insert(0, ROOT)
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from oracle import fixtures as F  # noqa: E402  (test inputs only)
+from oracle import unet_oracle as O  # noqa: E402
+
+SEED, BATCH, SIZE = 51, 2, 188
+
+
+def shard(rank):
+    return F.make_inputs(100 + rank, BATCH, 1, SIZE)
+
+
+def main():
+    out, overlap, steps = sys.argv[1], bool(int(sys.argv[2])), int(sys.argv[3])
+    rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo")
+    from unet_amd import UNet
+    from unet_amd.train import Trainer
+    params = O.hash_init(1, 2, seed=SEED, bn_random=True)
+    m = UNet(1, 2)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    m = m.cuda().train()
+    tr = Trainer(m, BATCH, SIZE, SIZE, lr=1e-4, momentum=0.99, process_group=dist.group.WORLD, overlap=overlap)
+    x, t, w = (torch.from_numpy(a).cuda() for a in shard(rank))
+    res = {}
+    for s in range(steps):
+        loss = tr.forward_loss(x, t, w)
+        tr.backward_and_reduce(x)
+        torch.cuda.synchronize()
+        res[f"grad{s}"] = tr.flat.grad.cpu().numpy().copy()     # SUM over ranks
+        res[f"loss{s}"] = np.array(loss.item())
+        tr.optimizer_step()
+    torch.cuda.synchronize()
+    res["params"] = tr.flat.flat.cpu().numpy().copy()
+    res["buffers_before_sync"] = np.concatenate([b.double().cpu().numpy().ravel() for b in m.buffers()])
+    tr.sync_buffers()
+    res["buffers"] = np.concatenate([b.double().cpu().numpy().ravel() for b in m.buffers()])
+    np.savez(out, **res)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

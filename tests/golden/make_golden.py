@@ -103,6 +103,132 @@ def whole_model_case(tag, n, h, n_channels=1, seed=1, steps=0):
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+def full_size_train_case(tag, n, h, n_channels=1, seed=5):
+    """Train-mode forward + WeightedCrossEntropyLoss + backward at a full image
+    size (configs[1]'s 512^2, batch 2): logits are large, so a strided sample,
+    the mask and its margin are kept, plus the usual gradient digests and the
+    updated running statistics (models/unet_model.py:105-146, utils/losses.py:49-57,
+    scripts/train.py:114-131)."""
+    params = O.hash_init(n_channels, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, n_channels, h)
+    m = ref_model(params, n_channels)
+    m.train()
+    logits = m(_t(x))
+    loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt), _t(wmap))
+    loss.backward()
+    lg = logits.detach().numpy()
+    out = {"x_seed": np.array(seed), "n": np.array(n), "h": np.array(h), "c": np.array(n_channels),
+           "loss": np.array(loss.item()),
+           "logits_sample": lg[:, :, ::7, ::5].copy(),
+           "mask": np.packbits(lg[:, 1] > lg[:, 0], axis=-1),
+           "sure": np.packbits(np.abs(lg[:, 1] - lg[:, 0]) > 1e-3, axis=-1)}
+    for name, p in m.named_parameters():
+        digest(name, p.grad.numpy(), out)
+    for name, b in m.named_buffers():
+        if "running" in name:
+            out[f"buf/{name}"] = b.detach().numpy().copy()
+    path = os.path.join(HERE, f"train_{tag}.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def hela_stitch_1024():
+    """configs[3]'s 1024^2 input: a 2x2 stitch of DIC-C2DH-HeLa 01 frames
+    t000-t003 (the reference's 1024^2 demo, images/phase5 5.png, is such a
+    stitch), Normalize(0.5, 0.5) as scripts/predict.py:50-54."""
+    from PIL import Image
+    root = os.path.join(REF, "data/raw/train/DIC-C2DH-HeLa/01")
+    fr = [np.array(Image.open(os.path.join(root, f"t{i:03d}.tif")).convert("L")) for i in range(4)]
+    img = np.block([[fr[0], fr[1]], [fr[2], fr[3]]]).astype(np.uint8)
+    return img
+
+
+def tile_farm_case(tile_in=512, seed=31):
+    """Overlap-tile inference of a 1024^2 image (configs[3]): mirror padding with
+    numpy's own np.pad(mode="reflect"), then the reference UNet in eval mode
+    (scripts/predict.py:70-82) on every 512^2 tile, outputs stitched.  Weights:
+    hash init with running statistics from F.plausible_running_stats."""
+    img = hela_stitch_1024()
+    xn = img.astype(np.float64) / 255.0 * 2.0 - 1.0
+    H, W = xn.shape
+    params = F.plausible_running_stats(O.hash_init(1, 2, seed=seed, bn_random=True), seed)
+    m = ref_model(params)
+    m.eval()
+    to = O.output_size(tile_in)
+    margin = (tile_in - to) // 2
+    ny, nx = -(-H // to), -(-W // to)
+    pads = ((margin, ny * to - H + (tile_in - to - margin)), (margin, nx * to - W + (tile_in - to - margin)))
+    padded = np.pad(xn, pads, mode="reflect")
+    full = np.zeros((2, ny * to, nx * to))
+    tiles = [(ty * to, tx * to) for ty in range(ny) for tx in range(nx)]
+    with torch.no_grad():
+        for b in range(0, len(tiles), 4):
+            chunk = tiles[b:b + 4]
+            xt = _t(np.stack([padded[None, y:y + tile_in, x:x + tile_in] for (y, x) in chunk]))
+            lg = m(xt).numpy()
+            for (y, x), l in zip(chunk, lg):
+                full[:, y:y + to, x:x + to] = l
+            print("tiles", b + len(chunk), "/", len(tiles), flush=True)
+    full = full[:, :H, :W]
+    out = {"image": img, "seed": np.array(seed), "tile_in": np.array(tile_in),
+           "logits_sample": full[:, ::7, ::5].astype(np.float64),
+           "mask": np.packbits(full[1] > full[0], axis=-1),
+           "sure": np.packbits(np.abs(full[1] - full[0]) > 1e-3, axis=-1)}
+    path = os.path.join(HERE, "farm_1024.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
+def hela_train_case(n_frames=3, seed=8, steps=2):
+    """configs[0] (C1): the scripts/train.py loop body on real DIC-C2DH-HeLa 01
+    frames with their 01_ST/SEG targets and the reference's committed
+    01_ST/WEIGHT_MAPS (utils/dataset.py:69-115 with augment=False: ToTensor,
+    mask > 0 as int64, weight map as float32; targets and weights center-cropped
+    to the output size, scripts/train.py:114-126), SGD(lr 1e-4, momentum 0.99).
+    The frames and masks are those of hela_real.npz; this fixture adds the
+    weight maps and the reference's results (fp64)."""
+    from PIL import Image
+    root = os.path.join(REF, "data/raw/train/DIC-C2DH-HeLa")
+    imgs, segs, wms = [], [], []
+    for i in range(n_frames):
+        imgs.append(np.array(Image.open(os.path.join(root, "01", f"t{i:03d}.tif")).convert("L")))
+        segs.append(np.array(Image.open(os.path.join(root, "01_ST", "SEG", f"man_seg{i:03d}.tif"))))
+        wms.append(np.load(os.path.join(root, "01_ST", "WEIGHT_MAPS", f"weight_map_{i:03d}.npy")))
+    x = np.stack(imgs).astype(np.float64)[:, None] / 255.0
+    tgt_full = (np.stack(segs) > 0).astype(np.int64)[:, None]
+    wm_full = np.stack(wms).astype(np.float32)[:, None]          # dataset.py:112 .float()
+    params = O.hash_init(1, 2, seed=seed)
+    m = ref_model(params)
+    m.train()
+    crit = WeightedCrossEntropyLoss()
+    opt = torch.optim.SGD(m.parameters(), lr=1e-4, momentum=0.99)
+    p0 = {k: v.detach().clone() for k, v in m.named_parameters()}
+    out = {"seed": np.array(seed), "weight_maps": wm_full[:, 0]}
+    losses = []
+    for step in range(steps):
+        opt.zero_grad()
+        logits = m(_t(x))
+        oh, ow = logits.shape[2:]
+        hs, ws = (512 - oh) // 2, (512 - ow) // 2
+        t = torch.from_numpy(tgt_full)[:, :, hs:hs + oh, ws:ws + ow].squeeze(1)
+        w = _t(wm_full)[:, :, hs:hs + oh, ws:ws + ow].squeeze(1)
+        loss = crit(logits, t, w)
+        loss.backward()
+        if step == 0:
+            lg = logits.detach().numpy()
+            out["logits_sample"] = lg[:, :, ::7, ::5].copy()
+            for name, p in m.named_parameters():
+                digest(name, p.grad.numpy(), out)
+        opt.step()
+        losses.append(loss.item())
+    for k, v in m.named_parameters():
+        out[f"dnorm/{k}"] = np.array(torch.linalg.norm(v.detach() - p0[k]).item())
+    out["losses"] = np.array(losses)
+    path = os.path.join(HERE, "hela_train.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes; losses", losses)
+
+
 def forward_only_case(tag, n, h, n_channels=1, seed=3):
     params = O.hash_init(n_channels, 2, seed=seed, bn_random=True)
     x, tgt, wmap = F.make_inputs(seed, n, n_channels, h)
@@ -231,7 +357,7 @@ def real_data_case(n_frames=3):
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["ops", "m188", "m204", "f512", "f572", "hela"]
+    which = sys.argv[1:] or ["ops", "m188", "m204", "f512", "f572", "hela", "t512", "farm", "hela_train"]
     if "ops" in which:
         op_cases()
     if "m188" in which:
@@ -244,3 +370,11 @@ if __name__ == "__main__":
         forward_only_case("n1_c3_572", 1, 572, n_channels=3, seed=4)
     if "hela" in which:
         real_data_case()
+    if "t512" in which:
+        full_size_train_case("n2_512", 2, 512, seed=5)
+    if "t512b8" in which:  # the bench configuration (configs[1]): batch 8 x 512^2
+        full_size_train_case("n8_512", 8, 512, seed=6)
+    if "farm" in which:
+        tile_farm_case()
+    if "hela_train" in which:
+        hela_train_case()

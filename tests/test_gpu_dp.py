@@ -1,0 +1,98 @@
+"""The product data-parallel path on the GPU: two ranks (tests/dp_worker.py,
+one process each, sharing the test box's GPU, gloo) run
+unet_amd.train.Trainer(process_group=WORLD) on their own shards -- segmented
+backward (plan.backward(s, s+1)), each segment's gradient bucket all-reduced
+asynchronously while the next computes, side-stream weight gradients from the
+second step on, fused SGD with the 1/world scale.  Checked against one process
+that computes each shard's gradient on the GPU without a group, averages them
+on the host and applies the same SGD(momentum 0.99) update (SURVEY.md §8e's
+"shard-wise" DP oracle with GPU shard gradients)."""
+import os
+import socket
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+from oracle import unet_oracle as O
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import dp_worker as W  # noqa: E402
+
+STEPS = 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def run_ranks(tmp_path, overlap, world=2):
+    port = _free_port()
+    procs, outs = [], []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        out = str(tmp_path / f"rank{r}.npz")
+        outs.append(out)
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, str(int(overlap)),
+                                       str(STEPS)], env=env))
+    rcs = []
+    for p in procs:
+        try:
+            rcs.append(p.wait(timeout=240))
+        except subprocess.TimeoutExpired:
+            for q in procs:
+                q.kill()
+            raise
+    assert rcs == [0] * world, rcs
+    return [np.load(o) for o in outs]
+
+
+def single_process_reference(world=2):
+    """Per-shard GPU gradients without a process group, averaged on the host."""
+    from unet_amd import UNet
+    from unet_amd.train import Trainer
+    params = O.hash_init(1, 2, seed=W.SEED, bn_random=True)
+    m = UNet(1, 2)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    m = m.cuda().train()
+    tr = Trainer(m, W.BATCH, W.SIZE, W.SIZE, lr=1e-4, momentum=0.99)
+    shards = [tuple(torch.from_numpy(a).cuda() for a in W.shard(r)) for r in range(world)]
+    sums = []
+    for _ in range(STEPS):
+        acc = torch.zeros_like(tr.flat.grad)
+        for x, t, w in shards:
+            tr.forward_loss(x, t, w)
+            tr.backward_and_reduce(x)
+            acc += tr.flat.grad
+        sums.append(acc.cpu().numpy())
+        tr.flat.grad.copy_(acc / world)
+        tr.optimizer_step()
+    torch.cuda.synchronize()
+    return sums, tr.flat.flat.cpu().numpy()
+
+
+@pytest.mark.parametrize("overlap", [True, False])
+def test_two_rank_trainer_matches_shard_average(tmp_path, overlap):
+    ranks = run_ranks(tmp_path, overlap)
+    sums, params = single_process_reference()
+    # identical all-reduced gradients and weights on every rank
+    for s in range(STEPS):
+        np.testing.assert_array_equal(ranks[0][f"grad{s}"], ranks[1][f"grad{s}"])
+    np.testing.assert_array_equal(ranks[0]["params"], ranks[1]["params"])
+    # = the host average of the shards' gradients (SUM, then 1/world in SGD)
+    for s in range(STEPS):
+        g, ref = ranks[0][f"grad{s}"], sums[s]
+        assert np.abs(g - ref).max() <= 1e-4 * np.abs(ref).max(), (s, np.abs(g - ref).max())
+    p = ranks[0]["params"]
+    assert np.abs(p - params).max() <= 1e-5 * np.abs(params).max()
+    # the shards differ, so the per-rank BN running statistics differ until
+    # sync_buffers broadcasts rank 0's (DDP buffer semantics)
+    assert not np.array_equal(ranks[0]["buffers_before_sync"], ranks[1]["buffers_before_sync"])
+    np.testing.assert_array_equal(ranks[1]["buffers"], ranks[0]["buffers_before_sync"])

@@ -424,3 +424,169 @@ def test_single_class_loss_and_grads_are_zero():
     assert loss.item() == 0.0
     for name, p in m.named_parameters():
         assert float(p.grad.abs().max()) == 0.0, name
+
+
+def _bits(packed, w):
+    return np.unpackbits(packed, axis=-1)[..., :w].astype(bool)
+
+
+def check_grad_digests(named_grads, z, rel=1e-2, vtol=2e-2):
+    """Gradients vs the reference's digests (norm + 32 sampled entries per
+    tensor); the 22 BN-cancelled biases are compared absolutely."""
+    for name, g in named_grads:
+        g = g.detach().double().cpu().numpy().ravel()
+        ref_norm = float(z[f"gnorm/{name}"])
+        if O.bn_cancelled(name):
+            wn = float(z[f"gnorm/{name.replace('.bias', '.weight')}"])
+            assert np.abs(g).max() <= 1e-3 * wn, name
+            continue
+        assert abs(np.linalg.norm(g) - ref_norm) <= rel * ref_norm, (name, np.linalg.norm(g), ref_norm)
+        idx, ref = z[f"gidx/{name}"], z[f"gval/{name}"]
+        assert np.all(np.abs(g[idx] - ref) <= vtol * np.abs(ref).max() + 1e-7), name
+
+
+def check_full_size_outputs(lg, loss, z, wout):
+    assert np.abs(lg[:, :, ::7, ::5] - z["logits_sample"]).max() <= 1e-3
+    assert abs(loss - float(z["loss"])) <= 1e-4 * abs(float(z["loss"]))
+    sure = _bits(z["sure"], wout)
+    np.testing.assert_array_equal((lg[:, 1] > lg[:, 0])[sure], _bits(z["mask"], wout)[sure])
+    return int((~sure).sum())
+
+
+def test_train_step_512_vs_reference_fixture():
+    """configs[1]'s image size through the whole train step (batch 2, fp32):
+    logits, loss, mask, every gradient and the BN running statistics against
+    the reference run in fp64 (tests/golden/train_n2_512.npz;
+    models/unet_model.py:105-146, utils/losses.py:49-57, scripts/train.py:114-131)."""
+    from unet_amd import WeightedCrossEntropyLoss
+    z = np.load(os.path.join(G, "train_n2_512.npz"), allow_pickle=False)
+    seed, n, h = int(z["x_seed"]), int(z["n"]), int(z["h"])
+    params = O.hash_init(1, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
+    m = make_model(params)
+    m.train()
+    logits = m(torch.from_numpy(x).cuda())
+    loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+    loss.backward()
+    lg = logits.detach().double().cpu().numpy()
+    low = check_full_size_outputs(lg, loss.item(), z, lg.shape[-1])
+    check_grad_digests([(k, p.grad) for k, p in m.named_parameters()], z)
+    sd = m.state_dict()
+    for k in z.files:
+        if k.startswith("buf/"):
+            np.testing.assert_allclose(sd[k[4:]].cpu().numpy(), z[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    print(f"512^2 train step: {low} low-margin pixels")
+
+
+def test_trainer_bench_plan_batch8_512_vs_reference_and_autograd():
+    """The bench workload itself (configs[1]: batch 8 x 512^2, fp32) through
+    unet_amd.train.Trainer with the autotuned 512^2 GEMM variants: one step's
+    logits / loss / mask / gradients / running stats against the reference run
+    (tests/golden/train_n8_512.npz), then the autograd drop-in on the same
+    batch against the Trainer's flat gradients."""
+    from unet_amd import WeightedCrossEntropyLoss
+    from unet_amd.train import Trainer
+    z = np.load(os.path.join(G, "train_n8_512.npz"), allow_pickle=False)
+    seed, n, h = int(z["x_seed"]), int(z["n"]), int(z["h"])
+    params = O.hash_init(1, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
+    xd, td, wd = (torch.from_numpy(a).cuda() for a in (x, tgt, wmap))
+    b = make_model(params)
+    tr = Trainer(b, n, h, h, lr=1e-4, momentum=0.99)
+    lb = tr.forward_loss(xd, td, wd)
+    tr.backward_and_reduce(xd)
+    torch.cuda.synchronize()
+    lg = tr.logits.double().cpu().numpy()
+    low = check_full_size_outputs(lg, lb.item(), z, lg.shape[-1])
+    names = [k for k, _ in b.named_parameters()]
+    check_grad_digests(list(zip(names, tr.flat.grad_views)), z)
+    sd = b.state_dict()
+    for k in z.files:
+        if k.startswith("buf/"):
+            np.testing.assert_allclose(sd[k[4:]].cpu().numpy(), z[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    # drop-in autograd path, same weights and batch (shares the tuned GEMM choices)
+    a = make_model(params)
+    a.train()
+    la = WeightedCrossEntropyLoss()(a(xd), td, wd)
+    la.backward()
+    assert abs(la.item() - lb.item()) <= 1e-5 * abs(lb.item())
+    for nme, gv in zip(names, tr.flat.grad_views):
+        if O.bn_cancelled(nme):
+            continue
+        ga = dict(a.named_parameters())[nme].grad
+        assert float((ga - gv).abs().max()) <= 1e-4 * float(ga.abs().max()), nme
+    print(f"batch-8 512^2 Trainer step: {low} low-margin pixels")
+
+
+def test_segmented_backward_matches_whole_backward():
+    """The data-parallel backward schedule (plan.backward(s, s+1) for the 9
+    segments, weight gradients on the side stream after the tuning pass,
+    head backward only in segment 0) gives the whole backward's gradients."""
+    from unet_amd import _lib
+    from unet_amd.plan import N_SEGMENTS
+    from unet_amd.train import Trainer
+    lib = _lib.load()
+    lib.unet_set_tuning(b"concurrent", 1)
+    params = O.hash_init(1, 2, seed=43, bn_random=True)
+    x, tgt, wmap = (torch.from_numpy(a).cuda() for a in F.make_inputs(43, 2, 1, 204))
+    m = make_model(params)
+    tr = Trainer(m, 2, 204, 204)
+    tr.forward_loss(x, tgt, wmap)
+    tr.backward_and_reduce(x)        # first (tuning, serial) backward
+    res = {}
+    for mode in ("segments", "whole"):
+        tr.forward_loss(x, tgt, wmap)
+        tr.flat.grad.fill_(float("nan"))  # every gradient must be written
+        if mode == "segments":
+            for s in range(N_SEGMENTS):
+                tr.plan.backward(tr.param_tab, tr.grad_tab, x, tr.dlogits, tr.ws, s, s + 1)
+        else:
+            tr.plan.backward(tr.param_tab, tr.grad_tab, x, tr.dlogits, tr.ws, 0, N_SEGMENTS)
+        torch.cuda.synchronize()
+        res[mode] = [g.double().cpu().numpy() for g in tr.flat.grad_views]
+    names = [k for k, _ in m.named_parameters()]
+    for nme, gs, gw in zip(names, res["segments"], res["whole"]):
+        assert np.isfinite(gs).all(), nme
+        assert np.abs(gs - gw).max() <= 1e-5 * max(np.abs(gw).max(), 1e-30) + 1e-12, nme
+
+
+def test_hela_train_step_real_data():
+    """configs[0] (C1) plumbing on the GPU: real DIC-C2DH-HeLa 01 frames with
+    their man_seg targets and the reference's committed weight maps, batch 3,
+    ToTensor inputs, targets/weights center-cropped as strided views exactly as
+    scripts/train.py:114-126 does, two SGD(0.99) steps -- against the
+    reference's fp64 run (tests/golden/hela_train.npz)."""
+    from unet_amd import UNet, WeightedCrossEntropyLoss
+    zr = np.load(os.path.join(G, "hela_real.npz"), allow_pickle=False)
+    z = np.load(os.path.join(G, "hela_train.npz"), allow_pickle=False)
+    params = O.hash_init(1, 2, seed=int(z["seed"]))
+    m = make_model(params)
+    m.train()
+    x = torch.from_numpy(zr["images"].astype(np.float32)[:, None] / 255.0).cuda()
+    t_full = torch.from_numpy((zr["segs"] > 0).astype(np.int64)[:, None]).cuda()
+    w_full = torch.from_numpy(z["weight_maps"][:, None]).cuda()
+    crit = WeightedCrossEntropyLoss()
+    opt = torch.optim.SGD(m.parameters(), lr=1e-4, momentum=0.99)
+    p0 = {k: v.detach().clone() for k, v in m.named_parameters()}
+    losses = []
+    for step in range(len(z["losses"])):
+        opt.zero_grad()
+        out = m(x)
+        oh, ow = out.shape[2:]
+        hs, ws = (512 - oh) // 2, (512 - ow) // 2
+        t = t_full[:, :, hs:hs + oh, ws:ws + ow].squeeze(1)     # non-contiguous views
+        w = w_full[:, :, hs:hs + oh, ws:ws + ow].squeeze(1)
+        loss = crit(out, t, w)
+        loss.backward()
+        if step == 0:
+            assert np.abs(out.detach().double().cpu().numpy()[:, :, ::7, ::5] - z["logits_sample"]).max() <= 1e-3
+            check_grad_digests([(k, p.grad) for k, p in m.named_parameters()], z)
+        opt.step()
+        losses.append(loss.item())
+    np.testing.assert_allclose(losses, z["losses"], rtol=1e-4)
+    for k, v in m.named_parameters():
+        if O.bn_cancelled(k):
+            continue
+        d = float(torch.linalg.norm(v.detach() - p0[k]))
+        r = float(z[f"dnorm/{k}"])
+        assert abs(d - r) <= 1e-2 * r, (k, d, r)

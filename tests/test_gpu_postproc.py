@@ -63,3 +63,18 @@ def test_rand_index_vs_oracle(pp, seed):
     b = g.integers(0, 5, (61, 47)).astype(np.uint16)
     assert pp.rand_index(torch.from_numpy(a).cuda(), torch.from_numpy(b).cuda()) == P.rand_index(a, b)
     assert pp.rand_index(torch.from_numpy(a).cuda(), torch.from_numpy(a).cuda()) == (1.0, 0.0)
+
+
+def test_instance_masks_vs_reference_committed_outputs(pp):
+    """get_instance_masks(min_size=15) (scripts/predict.py:92-112,
+    utils/metrics.py:42-72) on the reference's own 84 predicted masks
+    (01_RES/mask*.tif) must give its committed instance labelings
+    (01_RES_INST/m*.tif) bit-exactly, numbering included
+    (tests/golden/hela_postproc.npz)."""
+    z = np.load(os.path.join(G, "hela_postproc.npz"), allow_pickle=False)
+    t, h, w = (int(v) for v in z["mask_shape"])
+    masks = (np.unpackbits(z["mask_bits"], axis=-1)[..., :w] * 255).astype(np.uint8)
+    got = pp.instance_masks(torch.from_numpy(masks).cuda(), min_size=int(z["min_size"])).cpu().numpy()
+    assert got.shape == (t, h, w)
+    bad = [i for i in range(t) if not np.array_equal(got[i], z["labels"][i])]
+    assert not bad, f"frames differing from the reference: {bad}"

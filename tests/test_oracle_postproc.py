@@ -58,3 +58,15 @@ def test_rand_index_known_answers():
     # pairs: (0,1) same/same, (2,3) same/diff, others diff/diff except (1,2) diff/same
     assert P.rand_index(g, np.array([[5, 5, 5, 6]]))[0] == pytest.approx(3 / 6)
     assert P.rand_index(np.array([[3]]), np.array([[4]])) == (1.0, 0.0)
+
+
+def test_oracle_instance_masks_vs_reference_committed_outputs():
+    """The CC oracle reproduces the reference's committed 01_RES_INST labelings
+    from its 01_RES masks (84 frames) -- pins the restatement to the
+    reference's own outputs, not only to scipy.ndimage.label."""
+    import os
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "hela_postproc.npz"), allow_pickle=False)
+    t, h, w = (int(v) for v in z["mask_shape"])
+    masks = (np.unpackbits(z["mask_bits"], axis=-1)[..., :w] * 255).astype(np.uint8)
+    for i in range(t):
+        np.testing.assert_array_equal(P.get_instance_masks(masks[i], int(z["min_size"])), z["labels"][i])

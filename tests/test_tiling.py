@@ -125,3 +125,40 @@ def test_tile_gather_scatter_kernels(c, h, w, tile, world, rank):
     mk = mask.cpu().numpy()
     np.testing.assert_array_equal(mk[covered], ((ref[1] > ref[0]) * 255).astype(np.uint8)[covered])
     assert (mk[~covered] == 3).all()
+
+
+@pytest.mark.gpu
+def test_tile_farm_1024_vs_reference_fixture():
+    """configs[3] at its size: a 1024^2 image (2x2 stitch of DIC-C2DH-HeLa 01
+    frames, Normalize(0.5, 0.5)), 512^2 tiles, 16 tiles dealt round-robin over
+    two replicas (devices [0, 0]), batch 8 per forward, mask straight from the
+    tile scatter -- against the reference UNet run per tile on numpy's own
+    mirror padding (tests/golden/farm_1024.npz): mask bit-exact on every pixel
+    whose reference margin exceeds 1e-3, logits within 1e-3."""
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    import os
+    from oracle import fixtures as F
+    from unet_amd import UNet
+    from unet_amd.plan import Plan
+    from unet_amd.tiling import TileFarm, TileGeometry
+    z = np.load(os.path.join(os.path.dirname(__file__), "golden", "farm_1024.npz"), allow_pickle=False)
+    params = F.plausible_running_stats(O.hash_init(1, 2, seed=int(z["seed"]), bn_random=True), int(z["seed"]))
+    m = UNet(1, 2)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    img = torch.from_numpy(z["image"].astype(np.float32) / 255.0 * 2.0 - 1.0)
+    H, W = img.shape
+    g = TileGeometry(H, W, int(z["tile_in"]))
+    assert (len(g), g.tile_out, g.margin) == (16, 324, 94)
+    farm = TileFarm(m, devices=[0, 0], tile_in=int(z["tile_in"]), batch=8)
+    mask = farm.predict(img, return_mask=True).numpy()
+    logits = farm.predict(img).numpy()
+    sure = np.unpackbits(z["sure"], axis=-1)[..., :W].astype(bool)
+    ref_mask = np.unpackbits(z["mask"], axis=-1)[..., :W].astype(bool)
+    np.testing.assert_array_equal(mask[sure] > 0, ref_mask[sure])
+    assert set(np.unique(mask)) <= {0, 255}
+    assert np.abs(logits[:, ::7, ::5] - z["logits_sample"]).max() <= 1e-3
+    # eval forwards run in the forward-only workspace prefix (no gradient buffers)
+    p = Plan(8, 1, 512, 512, 2)
+    assert p.forward_workspace_bytes < 0.5 * p.workspace_bytes
+    print(f"1024^2 farm: {int((~sure).sum())} low-margin pixels of {sure.size}")

@@ -862,12 +862,13 @@ hipError_t launch_sgd(float* p, const float* g, float* buf, size_t n, float lr, 
   return hipGetLastError();
 }
 
-__global__ void k_scale_dev(float* x, size_t n, const float* g) {
+__global__ void k_scale_dev(const float* x, float* y, size_t n, const float* g) {
   const float s = *g;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) x[i] *= s;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    y[i] = x[i] * s;
 }
-hipError_t launch_scale_by_dev(float* x, size_t n, const float* g, hipStream_t s) {
-  hipLaunchKernelGGL(k_scale_dev, dim3(grid_cap((long long)n, 256, 4096)), dim3(256), 0, s, x, n, g);
+hipError_t launch_scale_by_dev(const float* x, float* y, size_t n, const float* g, hipStream_t s) {
+  hipLaunchKernelGGL(k_scale_dev, dim3(grid_cap((long long)n, 256, 4096)), dim3(256), 0, s, x, y, n, g);
   return hipGetLastError();
 }
 

@@ -324,7 +324,12 @@ int unet_wce_fwd_bwd(const float* logits, const int64_t* t, const float* wm, int
 }
 
 int unet_scale_by_device_scalar(float* x, size_t n, const float* g, unet_stream_t st) {
-  OPCK(launch_scale_by_dev(x, n, g, reinterpret_cast<hipStream_t>(st)));
+  OPCK(launch_scale_by_dev(x, x, n, g, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_scale_by_device_scalar_out(const float* x, float* y, size_t n, const float* g, unet_stream_t st) {
+  OPCK(launch_scale_by_dev(x, y, n, g, reinterpret_cast<hipStream_t>(st)));
   return 0;
 }
 

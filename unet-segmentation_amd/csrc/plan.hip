@@ -102,6 +102,7 @@ struct unet_plan {
   Buf slab;          // split-K partial tiles (igemm sites the tuner splits)
   Buf tune_scratch;  // atomic targets of the autotuner's trial launches
   size_t ws_bytes = 0;
+  size_t fwd_ws_bytes = 0;  // prefix of the workspace a forward uses (no backward buffers)
   // timing
   bool timing = false;
   struct Ev {
@@ -916,6 +917,7 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     if (prec != UNET_PREC_FP32)  // hi plane (+ lo plane for split operands)
       p->pack16 = al.take(p->pack_region.bytes / 2 * (prec == UNET_PREC_BF16X3 ? 2 : 1));
   }
+  // everything a forward touches (train or eval) ...
   for (int l = 0; l < 18; ++l) {
     Conv& L = p->L[l];
     const long long pix = (long long)n * L.ho * L.wo;
@@ -925,23 +927,36 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     L.scale = al.take(fsz(L.co));
     L.shift = al.take(fsz(L.co));
     L.coef = al.take(fsz(4LL * L.co));
-    L.dz = al.take(fsz(pix * L.co));
-    L.dyp = al.take(fsz((long long)n * (L.ho + 4) * (L.wo + 4) * L.co));
   }
   for (int k = 0; k < 4; ++k) {
     ConvT& T = p->T[k];
-    const long long opix = (long long)n * 4 * T.h * T.w;
-    T.u = al.take(fsz(opix * T.co));
-    T.du = al.take(fsz(opix * T.co));
-    Skip& sk = p->S[k];
-    sk.d = al.take(fsz((long long)n * sk.th * sk.tw * sk.c));
+    T.u = al.take(fsz((long long)n * 4 * T.h * T.w * T.co));
   }
   for (int k = 0; k < 4; ++k) {
     Pool& pl = p->P[k];
     const long long pp = (long long)n * (pl.h / 2) * (pl.w / 2) * pl.c;
     pl.p = al.take(fsz(pp));
     pl.arg = al.take((size_t)pp);
-    pl.dp = al.take(fsz(pp));
+  }
+  p->fwd_ws_bytes = al.top;
+  // ... then the gradient buffers only a backward writes (about 2/3 of a
+  // train workspace): a forward that no backward follows -- eval, predict.py,
+  // the tile farm, no_grad validation -- needs only the prefix
+  for (int l = 0; l < 18; ++l) {
+    Conv& L = p->L[l];
+    const long long pix = (long long)n * L.ho * L.wo;
+    L.dz = al.take(fsz(pix * L.co));
+    L.dyp = al.take(fsz((long long)n * (L.ho + 4) * (L.wo + 4) * L.co));
+  }
+  for (int k = 0; k < 4; ++k) {
+    ConvT& T = p->T[k];
+    T.du = al.take(fsz((long long)n * 4 * T.h * T.w * T.co));
+    Skip& sk = p->S[k];
+    sk.d = al.take(fsz((long long)n * sk.th * sk.tw * sk.c));
+  }
+  for (int k = 0; k < 4; ++k) {
+    Pool& pl = p->P[k];
+    pl.dp = al.take(fsz((long long)n * (pl.h / 2) * (pl.w / 2) * pl.c));
   }
   p->ws_bytes = al.top;
   return p;
@@ -970,6 +985,7 @@ int unet_plan_out_hw(const unet_plan* p, int* oh, int* ow) {
   return 0;
 }
 size_t unet_plan_workspace_bytes(const unet_plan* p) { return p ? p->ws_bytes : 0; }
+size_t unet_plan_forward_workspace_bytes(const unet_plan* p) { return p ? p->fwd_ws_bytes : 0; }
 int unet_plan_num_params(const unet_plan*) { return 136; }
 int unet_plan_num_grads(const unet_plan*) { return 82; }
 int unet_plan_num_segments(const unet_plan*) { return 9; }

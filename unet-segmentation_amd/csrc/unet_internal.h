@@ -209,7 +209,7 @@ hipError_t launch_wce(const float* logits, const int64_t* t, const float* wm, in
                       float grad_scale, double* acc, hipStream_t s);
 hipError_t launch_sgd(float* p, const float* g, float* buf, size_t n, float lr, float mom,
                       float gscale, int first, hipStream_t s);
-hipError_t launch_scale_by_dev(float* x, size_t n, const float* g, hipStream_t s);
+hipError_t launch_scale_by_dev(const float* x, float* y, size_t n, const float* g, hipStream_t s);
 // weight repacks
 hipError_t launch_pack_conv(const float* w_oihw, int co, int ci, int kh, int kw, float* wf,
                             float* wd, hipStream_t s);

@@ -27,6 +27,7 @@ SIGNATURES = {
     "unet_plan_destroy": (None, [_vp]),
     "unet_plan_out_hw": (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "unet_plan_workspace_bytes": (_sz, [_vp]),
+    "unet_plan_forward_workspace_bytes": (_sz, [_vp]),
     "unet_plan_num_params": (_i, [_vp]),
     "unet_plan_num_grads": (_i, [_vp]),
     "unet_plan_forward": (_i, [_vp, _vp, _vp, _vp, _vp, _i, _vp]),
@@ -37,6 +38,7 @@ SIGNATURES = {
     "unet_plan_timing": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "unet_wce_fwd_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp]),
     "unet_scale_by_device_scalar": (_i, [_vp, _sz, _vp, _vp]),
+    "unet_scale_by_device_scalar_out": (_i, [_vp, _vp, _sz, _vp, _vp]),
     "unet_sgd_momentum": (_i, [_vp, _vp, _vp, _sz, _f, _f, _f, _i, _vp]),
     "unet_iou_counts": (_i, [_vp, _vp, _sz, _vp, _vp]),
     "unet_mask_from_logits": (_i, [_vp, _vp, _i, _i, _i, _vp]),
@@ -62,6 +64,14 @@ SIGNATURES = {
     "unet_bn_train_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "unet_bn_train_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "unet_bn_ws_bytes": (_sz, [_i]),
+    "unet_tracker_create": (_vp, [_i, _i, ctypes.c_double, ctypes.c_double, _i]),
+    "unet_tracker_destroy": (None, [_vp]),
+    "unet_tracker_ws_bytes": (_sz, [_i, _i]),
+    "unet_tracker_add_frame": (_i, [_vp, _vp, _i, _vp, _vp]),
+    "unet_tracker_step_host": (_i, [_vp, _i, _i, _vp, _vp, _vp]),
+    "unet_tracker_num_tracks": (_i, [_vp]),
+    "unet_tracker_tracks": (_i, [_vp, _vp, _i]),
+    "unet_linear_sum_assignment": (_i, [ctypes.c_longlong, ctypes.c_longlong, _vp, _vp, _vp]),
     "unet_set_tuning": (_i, [ctypes.c_char_p, _i]),
     "unet_tuning_report": (_sz, [ctypes.c_char_p, _sz]),
     "unet_tuning_reset": (_i, []),

@@ -107,8 +107,10 @@ class _Runner:
     def __setstate__(self, state):
         self.__init__()
 
-    def plan(self, n, c, h, w, k, precision="fp32"):
-        key = (n, c, h, w, k, precision)
+    def plan(self, n, c, h, w, k, precision="fp32", device=0):
+        # the device is part of the key: a plan's side stream and events belong
+        # to the device that was current when it first ran a concurrent backward
+        key = (n, c, h, w, k, precision, device)
         with self.lock:
             p = self.plans.get(key)
             if p is None:
@@ -129,19 +131,27 @@ def _check_tensor(t, name):
 class _UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, module, train, precision, *params):
-        plan = module._runner.plan(x.shape[0], x.shape[1], x.shape[2], x.shape[3], module.n_classes, precision)
+        plan = module._runner.plan(x.shape[0], x.shape[1], x.shape[2], x.shape[3], module.n_classes, precision,
+                                   x.device.index)
         state = module._state_tensors()
         for name, t in state:
             if t.is_floating_point():
                 _check_tensor(t, name)
             elif not t.is_cuda:
                 raise RuntimeError(f"{name} must be on a HIP device")
-        ws = torch.empty(plan.workspace_bytes, dtype=torch.uint8, device=x.device)
+            if t.device != x.device:
+                raise RuntimeError(f"{name} is on {t.device}, the input on {x.device}")
+        # the backward's gradient buffers are only allocated when a backward can
+        # follow (train mode with autograd recording); eval / no_grad forwards
+        # (predict.py, validation, the tile farm) take the forward-only prefix
+        need_bwd = bool(train) and any(ctx.needs_input_grad)
+        ws = torch.empty(plan.workspace_bytes if need_bwd else plan.forward_workspace_bytes, dtype=torch.uint8,
+                         device=x.device)
         logits = torch.empty((x.shape[0], module.n_classes, plan.out_h, plan.out_w), dtype=torch.float32,
                              device=x.device)
         tab = _lib.ptr_array([t for _, t in state])
         plan.forward(tab, x, logits, ws, train)
-        ctx.plan, ctx.ws, ctx.tab, ctx.train = plan, ws, tab, train
+        ctx.plan, ctx.ws, ctx.tab, ctx.train, ctx.need_bwd = plan, ws, tab, train, need_bwd
         ctx.params = params
         ctx.save_for_backward(x)
         return logits
@@ -151,6 +161,9 @@ class _UNetFunction(torch.autograd.Function):
         if not ctx.train:
             raise RuntimeError("backward through an eval-mode UNet forward is not supported by the MI355X "
                                "plan (train.py only differentiates train-mode forwards)")
+        if not ctx.need_bwd or ctx.ws is None:
+            raise RuntimeError("the MI355X UNet backward needs the workspace of a forward that recorded autograd "
+                               "(and it runs once per forward: use retain_graph=False)")
         (x,) = ctx.saved_tensors
         dlogits = dlogits.contiguous()
         grads = [torch.empty_like(p) for p in ctx.params]
@@ -218,18 +231,34 @@ class UNet(nn.Module):
         return "fp32"
 
 
+def _check_loss_operands(logits, targets, weights):
+    """The checks torch's CrossEntropyLoss / the reference's elementwise product
+    make before touching memory (utils/losses.py:49-57): targets int64 and the
+    weight map floating point, both (N, H, W) of the logits and on their device.
+    Labels outside [0, K) are treated as ignore_index (contribute 0) instead of
+    raising as torch does for values other than -100: validating them would
+    need a device synchronisation per step."""
+    n, k, h, w = logits.shape
+    if targets.dtype != torch.int64:
+        raise RuntimeError(f"targets must be int64 class indices, got {targets.dtype}")
+    if not weights.is_floating_point():
+        raise RuntimeError(f"weight_maps must be floating point, got {weights.dtype}")
+    for name, t in (("targets", targets), ("weight_maps", weights)):
+        if t.device != logits.device:
+            raise RuntimeError(f"{name} is on {t.device}, the logits on {logits.device}")
+    if tuple(targets.shape) != (n, h, w) or tuple(weights.shape) != (n, h, w):
+        raise ValueError(f"targets/weight_maps must be (N,H,W)=({n},{h},{w}); got {tuple(targets.shape)}, "
+                         f"{tuple(weights.shape)}")
+
+
 class _WCEFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, targets, weights):
         _check_tensor(logits, "inputs")
-        if targets.dtype != torch.int64 or not targets.is_cuda:
-            raise RuntimeError("targets must be an int64 HIP tensor")
+        _check_loss_operands(logits, targets, weights)
         if weights.dtype != torch.float32:
             weights = weights.float()
         n, k, h, w = logits.shape
-        if targets.shape != (n, h, w) or weights.shape != (n, h, w):
-            raise ValueError(f"targets/weight_maps must be (N,H,W)=({n},{h},{w}); got {tuple(targets.shape)}, "
-                             f"{tuple(weights.shape)}")
         lib = _lib.load()
         loss = torch.empty((), dtype=torch.float32, device=logits.device)
         dl = torch.empty_like(logits)
@@ -247,9 +276,11 @@ class _WCEFunction(torch.autograd.Function):
         (dl,) = ctx.saved_tensors
         g = g.to(torch.float32).contiguous()
         lib = _lib.load()
-        _lib.check(lib.unet_scale_by_device_scalar(dl.data_ptr(), dl.numel(), g.data_ptr(),
-                                                   _lib.stream_of(dl.device)), "unet_scale_by_device_scalar")
-        return dl, None, None
+        # scale into a fresh tensor: the saved one must survive a second backward
+        out = torch.empty_like(dl)
+        _lib.check(lib.unet_scale_by_device_scalar_out(dl.data_ptr(), out.data_ptr(), dl.numel(), g.data_ptr(),
+                                                       _lib.stream_of(dl.device)), "unet_scale_by_device_scalar_out")
+        return out, None, None
 
 
 class WeightedCrossEntropyLoss(nn.Module):

@@ -32,6 +32,8 @@ class Plan:
         self.n_classes = n_classes
         self.out_h, self.out_w = oh.value, ow.value
         self.workspace_bytes = int(self.lib.unet_plan_workspace_bytes(self.handle))
+        # a forward that no backward follows (eval, no_grad) needs only this prefix
+        self.forward_workspace_bytes = int(self.lib.unet_plan_forward_workspace_bytes(self.handle))
 
     def __del__(self):
         h = getattr(self, "handle", None)

@@ -94,7 +94,21 @@ class Trainer:
     def out_hw(self):
         return self.plan.out_h, self.plan.out_w
 
+    def _check_batch(self, x, targets, weights):
+        from .modules import _check_loss_operands
+        n, c, h, w = self.plan.shape
+        if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()):
+            raise RuntimeError("x must be a contiguous float32 HIP tensor")
+        if tuple(x.shape) != (n, c, h, w):
+            raise ValueError(f"x must be {(n, c, h, w)} (the Trainer's plan shape), got {tuple(x.shape)}")
+        if x.device != self.logits.device:
+            raise RuntimeError(f"x is on {x.device}, the model on {self.logits.device}")
+        _check_loss_operands(self.logits, targets, weights)
+        if weights.dtype != torch.float32:
+            raise RuntimeError(f"weight_maps must be float32 for the fused loss, got {weights.dtype}")
+
     def forward_loss(self, x, targets, weights):
+        self._check_batch(x, targets, weights)
         self.plan.forward(self.param_tab, x, self.logits, self.ws, True)
         n, k, h, w = self.logits.shape
         ts = (ctypes.c_int64 * 3)(*targets.stride())
@@ -127,8 +141,6 @@ class Trainer:
 
     def step(self, x, targets, weights):
         """One train.py step; returns the (device) loss without synchronising."""
-        if not (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous()):
-            raise RuntimeError("x must be a contiguous float32 HIP tensor")
         loss = self.forward_loss(x, targets, weights)
         self.backward_and_reduce(x)
         self.optimizer_step()
