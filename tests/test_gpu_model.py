@@ -584,9 +584,14 @@ def test_hela_train_step_real_data():
         opt.step()
         losses.append(loss.item())
     np.testing.assert_allclose(losses, z["losses"], rtol=1e-4)
+    # update norms: the BN weights' gradients nearly cancel at the default init
+    # (gamma 1, beta 0), so the reference's own fp32 run already deviates from
+    # its fp64 run by up to 25 % on some of them (dnorm32/, recorded with the
+    # fixture); tolerance max(1 %, 2 x that floor) per tensor
     for k, v in m.named_parameters():
         if O.bn_cancelled(k):
             continue
         d = float(torch.linalg.norm(v.detach() - p0[k]))
         r = float(z[f"dnorm/{k}"])
-        assert abs(d - r) <= 1e-2 * r, (k, d, r)
+        floor = abs(float(z[f"dnorm32/{k}"]) - r)
+        assert abs(d - r) <= max(1e-2 * r, 2 * floor), (k, d, r, floor)
