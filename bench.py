@@ -1,8 +1,10 @@
 """Benchmark: U-Net training images/s at 512x512x1, batch 8 per GPU, fp32
 (BASELINE.json configs[1]; weak scaling over 1/2/4/8 MI355X with an RCCL
-gradient all-reduce over xGMI).  ``--dtype bf16`` runs the convolution GEMMs on
-bf16 operands with fp32 accumulation (configs[2] per GPU; with ``--channels 3
---size 572`` the configs[4] stress shape); the default stays configs[1].
+gradient all-reduce over xGMI).  The same invocation also times the bf16-operand
+GEMM plan (configs[2] per GPU: global batch 8 x N) and reports it as the
+``bf16`` sub-object; ``--dtype`` picks the precision of the headline ``value``
+(default fp32 = configs[1]); ``--channels 3 --size 572`` is the configs[4]
+stress shape.
 
 A step = forward + WeightedCrossEntropyLoss + backward + all-reduce (N>1) +
 SGD(momentum 0.99) over one synthetic batch resident in HBM, exactly the body
@@ -11,7 +13,19 @@ of scripts/train.py:108-131 (no per-step .item()).
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.
+Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
+* roofline: the implicit-GEMM conv family (63 GEMM launch sites per step) at
+  the MFMA peak of the precision, HIP-event timed on the plan's stream in an
+  extra untimed step; traffic from the committed rocprofv3 PMC passes of this
+  command (profiles/pmc_traffic*.json, per GEMM launch site);
+* bottleneck / stage1: SURVEY.md §8d's two targets (MFMA on the 1024-channel
+  set, HBM on the fused stage-1 kernels);
+* iou: eval-mode masks of the real DIC-C2DH-HeLa frames of
+  tests/golden/hela_real.npz against 01_ST/SEG, next to the reference's IoU on
+  the same frames and weights (a checker leg, run after the timing);
+* cpu_baseline: the reference train step restated on torch CPU
+  (oracle/torch_cpu_ref.py; the reference .py does not travel to the GPU box)
+  at batch 8 and batch 1 on this host's cores.
 """
 from __future__ import annotations
 
@@ -34,6 +48,7 @@ BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 (no sp
 HBM_PEAK_GBS = 8000.0
 GEMM_DESC = {"fp32": "fp32", "bf16": "bf16-operand/fp32-acc",
              "bf16x3": "fp32-accurate bf16x3 split-operand (3 bf16 MFMA products, fp32 acc)"}
+PEAK = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "bf16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1)}
 
 
 def init_weights(m):
@@ -59,84 +74,93 @@ def synthetic_batch(n, size, out, device, seed, channels=1):
     return x.contiguous(), t.contiguous(), w.contiguous()
 
 
-def cpu_baseline(seconds_hint=20.0):
-    """The CPU restatement of the reference train step (oracle/, a port: the
-    reference .py does not travel), 512x512x1 batch 1, fp32, timed on this host."""
-    import numpy as np
-    from oracle import unet_oracle as O
-    from oracle import fixtures as F
+def cpu_model():
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                return ln.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def cpu_baseline():
+    """The reference train step (scripts/train.py:114-131 semantics) restated on
+    torch CPU -- the same oneDNN / native kernels the reference runs on -- at
+    512x512x1, batch 8 (the metric's batch) and batch 1 (configs[0]), timed on
+    this host.  Bounded: one untimed warm-up step at batch 1, then ~10 s per
+    batch size.  Measurement infrastructure (oracle/torch_cpu_ref.py)."""
+    from oracle import torch_cpu_ref as R
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    params = O.hash_init(1, 2, seed=0)
-    x, t, w = F.make_inputs(0, 1, 1, 512)
-    p = {k: np.asarray(v, np.float32) for k, v in params.items()}
-    bufs = {}
-    steps, t0 = 0, time.time()
-    while True:
-        net = O.UNetOracle(p, dtype=np.float32)
-        logits, cache, nb = net.forward(x)
-        loss, dl = O.weighted_ce(logits, t, w)
-        grads = net.backward(dl.astype(np.float32), cache)
-        for k, g in grads.items():
-            p[k], bufs[k] = O.sgd_momentum_step(p[k], g.astype(np.float32), bufs.get(k))
-        p.update(nb)
-        steps += 1
-        if time.time() - t0 > seconds_hint or steps >= 3:
-            break
-    dt = time.time() - t0
-    return {"value": round(steps / dt, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{steps} train step(s) (fwd+WCE+bwd+SGD) of one 512x512x1 image, NumPy/OpenBLAS fp32 "
-                      f"restatement in oracle/, {dt:.1f} s"}
+    torch.set_num_threads(threads)
+    R.train_steps_per_second(1, seconds=0.0, max_steps=1)
+    v1, s1, e1 = R.train_steps_per_second(1, seconds=6.0, max_steps=3)
+    v8, s8, e8 = R.train_steps_per_second(8, seconds=8.0, max_steps=2)
+    return {"value": round(v8, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "batch1_value": round(v1, 4),
+            "sample": f"torch {torch.__version__} CPU restatement of the reference train step (fwd + weighted CE + "
+                      f"bwd + SGD(0.99), fp32, 512x512x1): batch 8 x {s8} step(s) in {e8:.1f} s; batch 1 x {s1} "
+                      f"step(s) in {e1:.1f} s, after one warm-up step"}
 
 
-def pmc_traffic(args):
-    """HBM bytes per launch per kernel family, from the committed PMC passes of
-    this same command (tools/pmc_report.py --json); counters cannot be read in
-    the timed run itself (separate rocprofv3 --pmc passes)."""
-    name = "pmc_traffic.json" if args.dtype == "fp32" else f"pmc_traffic_{args.dtype}.json"
-    path = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles", name)
+def pmc_traffic(args, dtype):
+    """HBM bytes per GEMM launch site and per stage-1 step from the committed PMC
+    passes of this command (tools/pmc_report.py --json); counters cannot be read
+    in the timed run itself (separate rocprofv3 --pmc passes)."""
+    name = "pmc_traffic.json" if dtype == "fp32" else f"pmc_traffic_{dtype}.json"
+    path = os.path.join(ROOT, "profiles", name)
     if args.size != 512 or args.batch != 8 or args.channels != 1 or not os.path.exists(path):
         return {}
-    fams = json.load(open(path))["families"]
-    return {k: int(v["bytes_per_launch"]) for k, v in fams.items()}
+    return json.load(open(path))
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=50)
-    ap.add_argument("--warmup", type=int, default=10)
-    ap.add_argument("--batch", type=int, default=8, help="images per GPU")
-    ap.add_argument("--size", type=int, default=512)
-    ap.add_argument("--channels", type=int, default=1, help="input channels (configs[4]: 3)")
-    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "bf16x3"],
-                    help="GEMM arithmetic: fp32 MFMA; bf16 = bf16-in / fp32-acc MFMA; bf16x3 = fp32-accurate "
-                         "split operands (hi*hi + hi*lo + lo*hi on the bf16 MFMA)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--no-overlap", action="store_true")
-    ap.add_argument("--tuning-report", default=None, help="write the GEMM autotuner's choices to this file")
-    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
-                    help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (ranks may share a GPU; rehearsal only)")
-    args = ap.parse_args()
+def hela_iou(device, precision):
+    """Checker leg (after the timing): eval-mode masks of the real HeLa frames of
+    tests/golden/hela_real.npz (weights: the fixture's hash init + running
+    statistics) vs 01_ST/SEG, next to the reference's IoUs on the same frames."""
+    import numpy as np
+    from oracle import unet_oracle as O
+    from unet_amd import UNet, _lib
+    path = os.path.join(ROOT, "tests", "golden", "hela_real.npz")
+    if not os.path.exists(path):
+        return None
+    z = np.load(path, allow_pickle=False)
+    params = O.hash_init(1, 2, seed=int(z["seed"]), bn_random=True)
+    for k in z.files:
+        if k.startswith("buf/"):
+            params[k[4:]] = z[k].astype(np.float32)
+    m = UNet(1, 2)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    m = m.to(device).eval()
+    m.precision = precision
+    x = torch.from_numpy((z["images"].astype(np.float32)[:, None] / 255.0) * 2.0 - 1.0).to(device)
+    with torch.no_grad():
+        logits = m(x)
+    lib = _lib.load()
+    n, _, oh, ow = logits.shape
+    mask = torch.empty((n, oh, ow), dtype=torch.uint8, device=device)
+    _lib.check(lib.unet_mask_from_logits(logits.data_ptr(), mask.data_ptr(), n, oh, ow, _lib.stream_of(device)),
+               "unet_mask_from_logits")
+    oy = (z["segs"].shape[1] - oh) // 2
+    gt = torch.from_numpy((z["segs"][:, oy:oy + oh, oy:oy + ow] > 0).astype(np.uint8) * 255).to(device)
+    ious = []
+    for i in range(n):
+        cnt = torch.zeros(2, dtype=torch.int64, device=device)
+        _lib.check(lib.unet_iou_counts(mask[i].data_ptr(), gt[i].contiguous().data_ptr(), oh * ow, cnt.data_ptr(),
+                                       _lib.stream_of(device)), "unet_iou_counts")
+        c = cnt.cpu().numpy()
+        ious.append(float(c[0] / c[1]) if c[1] else 1.0)
+    ref = [float(v) for v in z["ious"]]
+    return {"iou": round(float(np.mean(ious)), 6), "iou_ref": round(float(np.mean(ref)), 6),
+            "max_abs_diff": float(max(abs(a - b) for a, b in zip(ious, ref))), "frames": n,
+            "data": "DIC-C2DH-HeLa 01 t000-t002 vs 01_ST/SEG, eval mode, Normalize(0.5, 0.5) (predict.py:50-92); "
+                    "iou_ref = the reference UNet on the same frames and weights (tests/golden/hela_real.npz)"}
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    # one GPU per rank; "--dist-backend gloo" lets several ranks share a device
-    # (a rehearsal of the DP path on a 1-GPU box, not a measurement)
-    local_dev = local if args.dist_backend == "nccl" else local % torch.cuda.device_count()
-    torch.cuda.set_device(local_dev)
-    device = torch.device("cuda", local_dev)
-    pg = None
-    if world > 1:
-        if args.dist_backend == "nccl":
-            dist.init_process_group("nccl", device_id=device)
-        else:
-            dist.init_process_group(args.dist_backend)
-        pg = dist.group.WORLD
 
+def run_precision(args, dtype, device, pg, world, rank):
+    """Time args.steps train steps of one GEMM precision; returns its summary."""
     from unet_amd import UNet
     from unet_amd.train import Trainer
-
     torch.manual_seed(0)
     model = UNet(n_channels=args.channels, n_classes=2)
     model.apply(init_weights)
@@ -145,7 +169,7 @@ def main():
         for t in model.state_dict().values():
             dist.broadcast(t, 0)
     trainer = Trainer(model, args.batch, args.size, args.size, lr=1e-4, momentum=0.99, process_group=pg,
-                      overlap=not args.no_overlap, precision=args.dtype)
+                      overlap=not args.no_overlap, precision=dtype)
     oh, ow = trainer.out_hw
     x, t, w = synthetic_batch(args.batch, args.size, oh, device, seed=1234 + rank, channels=args.channels)
 
@@ -176,72 +200,138 @@ def main():
     torch.cuda.synchronize()
     trainer.plan.set_timing(False)
     tim = trainer.plan.timing()
+    del trainer, model, x, t, w
+    torch.cuda.empty_cache()
+
+    peak = PEAK[dtype]
+    conv = [tim[k] for k in ("conv_fwd", "conv_dgrad", "conv_wgrad")]
+    conv_ms = sum(c[0] for c in conv)
+    conv_fl = sum(c[1] for c in conv)
+    launches = sum(c[3] for c in conv)
+    achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    pmc = pmc_traffic(args, dtype)
+    fam = pmc.get("families", {})
+    st, bn = tim["stage1"], tim["bottleneck"]
+    kernels = {k: {"ms": round(v[0], 3), "launches": v[3],
+                   "tflops": round(v[1] / (v[0] * 1e-3) / 1e12, 2) if v[0] > 0 and v[1] else None,
+                   "gbs": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 and v[2] else None}
+               for k, v in tim.items()}
+    imgs = world * args.batch * args.steps
+    return {
+        "value": round(imgs / elapsed, 3),
+        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "dtype": dtype,
+        "roofline": {"bound": "mfma", "kernel": f"implicit-GEMM conv family (fwd/dgrad igemm + wgrad, {dtype} operands)",
+                     "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                     "frac": round(achieved / peak, 4),
+                     "traffic": fam.get("conv", {}).get("bytes_per_launch"),
+                     "traffic_unit": "HBM bytes per GEMM launch site (rocprofv3 --pmc 2*FETCH_SIZE + WRITE_SIZE of "
+                                     "this command's conv family incl. split-K epilogues, summed over one step / "
+                                     f"{launches}; profiles/pmc_traffic{'' if dtype == 'fp32' else '_' + dtype}.json)",
+                     "flops_per_step": conv_fl, "launches_per_step": launches,
+                     "avg_launch_ms": round(conv_ms / max(launches, 1), 4),
+                     "timing": "HIP events on the plan's stream over one extra step after the timed steps, "
+                               "weight-gradient side stream serialised; in the timed steps wgrad overlaps dgrad "
+                               "on a second stream (per-dispatch times then overlap: profiles/*trace_check*.txt)"},
+        # SURVEY.md §8d target: >= 50 % MFMA on the 1024-channel bottleneck set
+        "bottleneck": {"layers": "down4.c0, down4.c1, up1.convT, up1.c0 (fwd + dgrad + wgrad)",
+                       "ms": round(bn[0], 3),
+                       "tflops": round(bn[1] / (bn[0] * 1e-3) / 1e12, 2) if bn[0] > 0 else None,
+                       "frac": round(bn[1] / (bn[0] * 1e-3) / 1e12 / peak, 4) if bn[0] > 0 else None},
+        # SURVEY.md §8d target: >= 40 % HBM on stage 1 (inc.c0 + BN0 stats fwd;
+        # BN0 backward fused into inc.c0's weight gradient)
+        "stage1": {"bound": "hbm", "ms": round(st[0], 3), "launches": st[3],
+                   "kernels": "k_conv_first_fwd (read x, write y0, BN0 stats) + k_bnb_finalize(BN0) + "
+                              "k_conv_first_wgrad<FUSED> (read dz0, y0, x) + k_reduce_slabs",
+                   "algorithmic_bytes": st[2],
+                   "achieved_gbs": round(st[2] / (st[0] * 1e-3) / 1e9, 1) if st[0] > 0 else None,
+                   "peak_gbs": HBM_PEAK_GBS,
+                   "frac": round(st[2] / (st[0] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4) if st[0] > 0 else None,
+                   "traffic": fam.get("stage1", {}).get("bytes_per_step")},
+        "kernels": kernels,
+        "final_loss": round(final_loss, 5),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=10)
+    ap.add_argument("--batch", type=int, default=8, help="images per GPU")
+    ap.add_argument("--size", type=int, default=512)
+    ap.add_argument("--channels", type=int, default=1, help="input channels (configs[4]: 3)")
+    ap.add_argument("--dtype", default="fp32", choices=["fp32", "bf16", "bf16x3"],
+                    help="GEMM arithmetic of the headline value: fp32 MFMA; bf16 = bf16-in / fp32-acc MFMA; "
+                         "bf16x3 = fp32-accurate split operands (hi*hi + hi*lo + lo*hi on the bf16 MFMA)")
+    ap.add_argument("--extra-dtypes", default="bf16",
+                    help="comma-separated precisions also timed in this invocation and reported as sub-objects "
+                         "('' = none; profiling runs use '')")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-iou", action="store_true")
+    ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--tuning-report", default=None, help="write the GEMM autotuner's choices to this file")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (ranks may share a GPU; rehearsal only)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one GPU per rank; "--dist-backend gloo" lets several ranks share a device
+    # (a rehearsal of the DP path on a 1-GPU box, not a measurement)
+    local_dev = local if args.dist_backend == "nccl" else local % torch.cuda.device_count()
+    torch.cuda.set_device(local_dev)
+    device = torch.device("cuda", local_dev)
+    pg = None
+    if world > 1:
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=device)
+        else:
+            dist.init_process_group(args.dist_backend)
+        pg = dist.group.WORLD
+
+    main_res = run_precision(args, args.dtype, device, pg, world, rank)
+    extras = {}
+    for d in [d for d in args.extra_dtypes.split(",") if d and d != args.dtype]:
+        extras[d] = run_precision(args, d, device, pg, world, rank)
 
     if rank == 0:
-        pmc = pmc_traffic(args)
-        imgs = world * args.batch * args.steps
-        value = imgs / elapsed
-        conv = [tim[k] for k in ("conv_fwd", "conv_dgrad", "conv_wgrad")]
-        conv_ms = sum(c[0] for c in conv)
-        conv_fl = sum(c[1] for c in conv)
-        achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
-        # bf16x3: fp32 GEMM flops at three bf16 MFMA products each
-        peak = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS,
-                "bf16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1)}[args.dtype]
-        launches = sum(c[3] for c in conv)
-        st = tim["stage1"]
-        kernels = {k: {"ms": round(v[0], 3), "launches": v[3],
-                       "tflops": round(v[1] / (v[0] * 1e-3) / 1e12, 2) if v[0] > 0 and v[1] else None,
-                       "gbs": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 and v[2] else None}
-                   for k, v in tim.items()}
+        comm = f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-reduce" if world > 1 else ""
         out = {
             "metric": METRIC,
-            "value": round(value, 3),
+            "value": main_res["value"],
             "unit": "images/s",
             "n_gpus": world,
             "steps": args.steps,
             "warmup": args.warmup,
-            "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "ms_per_step": main_res["ms_per_step"],
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": args.dtype,
-            "data": "synthetic: x~U[0,1) (N,1,512,512), Bernoulli(0.4) targets, 10+1/freq(class) weight maps; "
-                    "kaiming fan_out init (scripts/train.py:54-61)",
+            "data": f"synthetic: x~U[0,1) (N,{args.channels},{args.size},{args.size}), Bernoulli(0.4) targets, "
+                    "10+1/freq(class) weight maps; kaiming fan_out init (scripts/train.py:54-61)",
             "config": {"workload": f"U-Net train step {args.size}x{args.size}x{args.channels}, batch {args.batch}/GPU, "
-                                   f"{GEMM_DESC[args.dtype]} GEMMs: "
-                                   "fwd + weighted CE + bwd + SGD(0.99)" + ((f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-reduce" if world > 1 else "")),
+                                   f"{GEMM_DESC[args.dtype]} GEMMs: fwd + weighted CE + bwd + SGD(0.99){comm}",
                        "global_batch": world * args.batch, "image": args.size,
                        "parallelism": f"dp{world}"},
-            "roofline": {"bound": "mfma", "kernel": "implicit-GEMM conv family (fwd/dgrad igemm + wgrad, "
-                                                    f"{args.dtype} operands)",
-                         "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
-                         "frac": round(achieved / peak, 4), "traffic": pmc.get("conv"),
-                         "traffic_unit": "HBM bytes/launch (rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE, "
-                                         "profiles/pmc_traffic.json)",
-                         "flops_per_step": conv_fl, "launches_per_step": launches,
-                         "avg_launch_ms": round(conv_ms / max(launches, 1), 4),
-                         "timing": "HIP events on the plan's stream over one extra step after the timed steps, "
-                                   "weight-gradient side stream serialised; in the timed steps wgrad overlaps dgrad "
-                                   "on a second stream (per-dispatch times then overlap: "
-                                   "profiles/r01_trace_check*.txt)"},
-            # SURVEY.md §8d target: >= 50 % MFMA on the 1024-channel bottleneck set
-            "bottleneck": {"layers": "down4.c0, down4.c1, up1.convT, up1.c0 (fwd + dgrad + wgrad)",
-                           "ms": round(tim["bottleneck"][0], 3),
-                           "tflops": round(tim["bottleneck"][1] / (tim["bottleneck"][0] * 1e-3) / 1e12, 2)
-                           if tim["bottleneck"][0] > 0 else None,
-                           "frac": round(tim["bottleneck"][1] / (tim["bottleneck"][0] * 1e-3) / 1e12 / peak, 4)
-                           if tim["bottleneck"][0] > 0 else None},
-            "stage1": {"bound": "hbm", "ms": round(st[0], 3),
-                       "achieved_gbs": round(st[2] / (st[0] * 1e-3) / 1e9, 1) if st[0] > 0 else None,
-                       "peak_gbs": HBM_PEAK_GBS, "traffic": pmc.get("stage1")},
-            "kernels": kernels,
-            "final_loss": round(final_loss, 5),
         }
+        for k in ("roofline", "bottleneck", "stage1", "kernels", "final_loss"):
+            out[k] = main_res[k]
+        for d, r in extras.items():
+            out[d] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
+                      "config": f"same workload, {GEMM_DESC[d]} GEMMs (global batch {world * args.batch}"
+                                f"{'; configs[2] at N=8' if d == 'bf16' else ''})",
+                      **{k: r[k] for k in ("roofline", "bottleneck", "stage1", "kernels", "final_loss")}}
         if args.tuning_report:
             from unet_amd import _lib as _ulib
             with open(args.tuning_report, "w") as f:
                 f.write(_ulib.tuning_report())
+        if not args.no_iou and args.channels == 1:
+            out["iou"] = hela_iou(device, args.dtype)
+            if "bf16" in extras and out["iou"] is not None:
+                out["bf16"]["iou"] = hela_iou(device, "bf16")
         if world == 1 and not args.no_cpu_baseline and args.channels == 1:
             out["cpu_baseline"] = cpu_baseline()
         print(json.dumps(out))

@@ -105,28 +105,41 @@ def whole_model_case(tag, n, h, n_channels=1, seed=1, steps=0):
 
 def full_size_train_case(tag, n, h, n_channels=1, seed=5):
     """Train-mode forward + WeightedCrossEntropyLoss + backward at a full image
-    size (configs[1]'s 512^2, batch 2): logits are large, so a strided sample,
-    the mask and its margin are kept, plus the usual gradient digests and the
-    updated running statistics (models/unet_model.py:105-146, utils/losses.py:49-57,
-    scripts/train.py:114-131)."""
+    size (configs[1]'s 512^2, batch 2 and 8): logits are large, so a strided
+    sample, the mask and its margin are kept, plus the usual gradient digests and
+    the updated running statistics (models/unet_model.py:105-146,
+    utils/losses.py:49-57, scripts/train.py:114-131).  The same step is run a
+    second time in fp32 (the reference's own arithmetic on torch CPU): its
+    gradient digests (g32norm/, g32val/) give the per-tensor fp32 noise floor
+    the GPU tolerances are set against."""
     params = O.hash_init(n_channels, 2, seed=seed, bn_random=True)
     x, tgt, wmap = F.make_inputs(seed, n, n_channels, h)
-    m = ref_model(params, n_channels)
-    m.train()
-    logits = m(_t(x))
-    loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt), _t(wmap))
-    loss.backward()
-    lg = logits.detach().numpy()
-    out = {"x_seed": np.array(seed), "n": np.array(n), "h": np.array(h), "c": np.array(n_channels),
-           "loss": np.array(loss.item()),
-           "logits_sample": lg[:, :, ::7, ::5].copy(),
-           "mask": np.packbits(lg[:, 1] > lg[:, 0], axis=-1),
-           "sure": np.packbits(np.abs(lg[:, 1] - lg[:, 0]) > 1e-3, axis=-1)}
-    for name, p in m.named_parameters():
-        digest(name, p.grad.numpy(), out)
-    for name, b in m.named_buffers():
-        if "running" in name:
-            out[f"buf/{name}"] = b.detach().numpy().copy()
+    out = {"x_seed": np.array(seed), "n": np.array(n), "h": np.array(h), "c": np.array(n_channels)}
+    for dt in (torch.float64, torch.float32):
+        m = ref_model(params, n_channels).to(dt)
+        m.train()
+        xt = torch.from_numpy(x).to(dt)
+        logits = m(xt)
+        loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt), torch.from_numpy(wmap).to(dt))
+        loss.backward()
+        if dt == torch.float32:
+            for name, p in m.named_parameters():
+                g = p.grad.double().numpy().ravel()
+                out[f"g32norm/{name}"] = np.array(np.linalg.norm(g))
+                out[f"g32val/{name}"] = g[out[f"gidx/{name}"]]
+            out["loss32"] = np.array(loss.item())
+            continue
+        lg = logits.detach().numpy()
+        out.update({"loss": np.array(loss.item()),
+                    "logits_sample": lg[:, :, ::7, ::5].copy(),
+                    "mask": np.packbits(lg[:, 1] > lg[:, 0], axis=-1),
+                    "sure": np.packbits(np.abs(lg[:, 1] - lg[:, 0]) > 1e-3, axis=-1)})
+        for name, p in m.named_parameters():
+            digest(name, p.grad.numpy(), out)
+        for name, b in m.named_buffers():
+            if "running" in name:
+                out[f"buf/{name}"] = b.detach().numpy().copy()
+        del m, logits, loss
     path = os.path.join(HERE, f"train_{tag}.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")

@@ -431,8 +431,13 @@ def _bits(packed, w):
 
 
 def check_grad_digests(named_grads, z, rel=1e-2, vtol=2e-2):
-    """Gradients vs the reference's digests (norm + 32 sampled entries per
-    tensor); the 22 BN-cancelled biases are compared absolutely."""
+    """Gradients vs the reference's fp64 digests (norm + 32 sampled entries per
+    tensor): norm within max(rel, 2 x the reference's own fp32 deviation) and
+    samples within max(vtol x max|sample|, 3 x that deviation per entry) when
+    the fixture records its fp32 run (g32norm/, g32val/) -- BatchNorm makes
+    some deep-layer gradients sensitive to fp32 rounding (measured up to a few
+    % on sampled entries).  The 22 BN-cancelled biases are compared absolutely."""
+    worst = 0.0
     for name, g in named_grads:
         g = g.detach().double().cpu().numpy().ravel()
         ref_norm = float(z[f"gnorm/{name}"])
@@ -440,9 +445,16 @@ def check_grad_digests(named_grads, z, rel=1e-2, vtol=2e-2):
             wn = float(z[f"gnorm/{name.replace('.bias', '.weight')}"])
             assert np.abs(g).max() <= 1e-3 * wn, name
             continue
-        assert abs(np.linalg.norm(g) - ref_norm) <= rel * ref_norm, (name, np.linalg.norm(g), ref_norm)
         idx, ref = z[f"gidx/{name}"], z[f"gval/{name}"]
-        assert np.all(np.abs(g[idx] - ref) <= vtol * np.abs(ref).max() + 1e-7), name
+        nfl = abs(float(z[f"g32norm/{name}"]) - ref_norm) if f"g32norm/{name}" in z.files else 0.0
+        vfl = np.abs(z[f"g32val/{name}"] - ref) if f"g32val/{name}" in z.files else 0.0
+        ntol = max(rel * ref_norm, 2 * nfl)
+        vt = np.maximum(vtol * np.abs(ref).max(), 3 * vfl) + 1e-7
+        assert abs(np.linalg.norm(g) - ref_norm) <= ntol, (name, np.linalg.norm(g), ref_norm, nfl)
+        assert np.all(np.abs(g[idx] - ref) <= vt), (name, np.abs(g[idx] - ref).max(), vt.max())
+        worst = max(worst, abs(np.linalg.norm(g) - ref_norm) / ntol, float((np.abs(g[idx] - ref) / vt).max()))
+    print(f"worst gradient error / tolerance: {worst:.2f}")
+    return worst
 
 
 def check_full_size_outputs(lg, loss, z, wout):

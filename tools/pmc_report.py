@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc passes of bench.py per kernel family.
 
     python tools/pmc_report.py gpurun_out/pmc1 gpurun_out/pmc2 gpurun_out/pmc3 gpurun_out/pmc4
-    python tools/pmc_report.py --json profiles/pmc_traffic.json gpurun_out/pmc3 gpurun_out/pmc4
+    python tools/pmc_report.py --json profiles/pmc_traffic.json 63 gpurun_out/pmc3 gpurun_out/pmc4
 
 Per kernel name (summed over the dispatches of the last profiled step):
 effective clock = GRBM_GUI_ACTIVE / 8 XCDs / time; MFMA busy = SQ_VALU_MFMA_BUSY_CYCLES
@@ -33,15 +33,21 @@ def last_step(d):
 
 
 def family(name):
-    if "conv_first" in name:
+    """Kernel family of a dispatch, matching bench.py's timing classes: the
+    implicit-GEMM conv family (every igemm / halo conv / wgrad kernel and the
+    split-K epilogue its launch site runs) and the stage-1 kernels (inc.c0
+    forward and its fused BN0-backward weight gradient + slab reduction)."""
+    if "conv_first" in name or "reduce_slabs" in name:
         return "stage1"
-    if "igemm" in name or "conv3_bf" in name or ("wgrad" in name and "first" not in name):
+    if "igemm" in name or "conv3" in name or "splitk_epi" in name or "wgrad" in name:
         return "conv"
     return "other"
 
 
-def traffic(paths):
-    """HBM bytes per launch per kernel family (2 x FETCH_SIZE + WRITE_SIZE, KiB units)."""
+def traffic(paths, sites):
+    """HBM bytes (2 x FETCH_SIZE + WRITE_SIZE, KiB units) of the last profiled
+    step per kernel family: per step, and for the conv family per GEMM launch
+    site (bench.py's roofline.launches_per_step)."""
     tot, launches = collections.Counter(), collections.Counter()
     for path in paths:
         d = load(path)
@@ -52,14 +58,18 @@ def traffic(paths):
                 launches[f] += 1
             if "WRITE_SIZE" in d[i]:
                 tot[f] += d[i]["WRITE_SIZE"] * 1024
-    return {f: {"bytes_per_launch": tot[f] / launches[f], "launches": launches[f]} for f in launches}
+    out = {f: {"bytes_per_step": tot[f], "dispatches": launches[f]} for f in launches}
+    if "conv" in out:
+        out["conv"]["bytes_per_launch"] = tot["conv"] / sites
+        out["conv"]["launch_sites"] = sites
+    return out
 
 
 def main():
-    if sys.argv[1] == "--json":
-        out, paths = sys.argv[2], sys.argv[3:]
+    if sys.argv[1] == "--json":  # --json out.json SITES pmc_dir...
+        out, sites, paths = sys.argv[2], int(sys.argv[3]), sys.argv[4:]
         json.dump({"source": " ".join(paths), "correction": "2*FETCH_SIZE + WRITE_SIZE (gfx950)",
-                   "families": traffic(paths)}, open(out, "w"), indent=1)
+                   "families": traffic(paths, sites)}, open(out, "w"), indent=1)
         return
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
     for path in sys.argv[1:]:

@@ -108,15 +108,30 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict_
 // 1 KiB of contiguous dY per load), 8 loads in flight per thread; the x strip
 // is staged in LDS.  Per-thread register sums, one fp32 atomic per weight per
 // workgroup at the end.
-template <int CI>
+// FUSED: dY is not read from a padded buffer but formed on the fly from the
+// BN0 backward -- dY = k0*dz + k1*(y - mean) + k2 with the per-channel
+// coefficients of k_bnb_finalize (coef[4][64]) -- from dz (dy.ptr, the
+// unpadded (ho, wo) grid) and the saved raw conv output y (Y16: bf16).  inc.c0
+// has no input gradient, so dY(0) is consumed only here and is never written
+// (SURVEY.md §8d's fused stage-1 backward: read dz, y, x once).
+template <int CI, int FUSED = 0, int Y16 = 0>
 __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restrict__ x, int nimg, int h, int w,
-                                                          Src dy, float* __restrict__ dw) {
+                                                          Src dy, float* __restrict__ dw,
+                                                          const float* __restrict__ yr = nullptr,
+                                                          const float* __restrict__ coef = nullptr) {
   constexpr int RB = 4, PX = 64, TW = PX + 2;
   const int ho = h - 2, wo = w - 2;
   const int nseg = (wo + PX - 1) / PX, nstrip = (ho + RB - 1) / RB;
   const long long items = (long long)nimg * nstrip * nseg;
   __shared__ float tile[CI][RB + 2][TW];
   const int tid = threadIdx.x, cg = tid & 15, slot = tid >> 4;  // 16 channel groups x 16 pixel slots
+  float4 k0, k1, k2, mu;
+  if (FUSED) {
+    k0 = ld4(coef + cg * 4);
+    k1 = ld4(coef + 64 + cg * 4);
+    k2 = ld4(coef + 128 + cg * 4);
+    mu = ld4(coef + 192 + cg * 4);
+  }
   float acc[4][CI * 9];
 #pragma unroll
   for (int c = 0; c < 4; ++c)
@@ -146,8 +161,17 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restric
         pc[j] = pix - pr[j] * PX;
         const bool ok = (r0 + pr[j] < ho) && (x0 + pc[j] < wo);
         const int yy = min(r0 + pr[j], ho - 1), xx = min(x0 + pc[j], wo - 1);
-        g[j] = *reinterpret_cast<const float4*>(
-            dy.ptr + ((size_t)(n * dy.H + yy + dy.oy) * dy.W + xx + dy.ox) * dy.C + cg * 4);
+        const size_t off = ((size_t)(n * dy.H + yy + dy.oy) * dy.W + xx + dy.ox) * dy.C + cg * 4;
+        g[j] = *reinterpret_cast<const float4*>(dy.ptr + off);
+        if (FUSED) {
+          const float4 d = g[j];
+          const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + off))
+                                : ld4(yr + off);
+          g[j].x = fmaf(k0.x, d.x, fmaf(k1.x, yv.x - mu.x, k2.x));
+          g[j].y = fmaf(k0.y, d.y, fmaf(k1.y, yv.y - mu.y, k2.y));
+          g[j].z = fmaf(k0.z, d.z, fmaf(k1.z, yv.z - mu.z, k2.z));
+          g[j].w = fmaf(k0.w, d.w, fmaf(k1.w, yv.w - mu.w, k2.w));
+        }
         if (!ok) g[j] = make_float4(0.f, 0.f, 0.f, 0.f);
       }
 #pragma unroll
@@ -227,6 +251,8 @@ hipError_t launch_conv_first_fwd(const float* x, int n, int ci, int h, int w, co
   return hipGetLastError();
 }
 
+hipError_t reduce_first_slabs(int ci, int grid, float* dw, const float* slabs, hipStream_t s);
+
 size_t conv_first_wgrad_ws_bytes(int ci) { return sizeof(float) * (size_t)kFirstWgradSlabs * ci * 9 * 64; }
 
 hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, const Src& dy, int co,
@@ -240,11 +266,45 @@ hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, 
     case 3: hipLaunchKernelGGL(k_conv_first_wgrad<3>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
     default: hipLaunchKernelGGL(k_conv_first_wgrad<4>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
   }
+  return reduce_first_slabs(ci, grid, dw, slabs, s);
+}
+
+hipError_t reduce_first_slabs(int ci, int grid, float* dw, const float* slabs, hipStream_t s) {
   const int nw = ci * 9 * 64;
   hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * nw, s);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(nw, 64), cdiv(grid, 64)), dim3(256), 0, s, slabs, grid, nw, dw);
   return hipGetLastError();
+}
+
+template <int FUSED, int Y16>
+static void first_wgrad_go(int grid, int ci, const float* x, int n, int h, int w, const Src& dy, float* slabs,
+                           const float* y, const float* coef, hipStream_t s) {
+  switch (ci) {
+    case 1: hipLaunchKernelGGL((k_conv_first_wgrad<1, FUSED, Y16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+    case 2: hipLaunchKernelGGL((k_conv_first_wgrad<2, FUSED, Y16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+    case 3: hipLaunchKernelGGL((k_conv_first_wgrad<3, FUSED, Y16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+    default: hipLaunchKernelGGL((k_conv_first_wgrad<4, FUSED, Y16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+  }
+}
+
+// inc.c0 weight gradient straight from the BN0 backward (dz, saved y, coef):
+// no padded dY(0) is written or read.
+hipError_t launch_conv_first_wgrad_bn(const float* x, int n, int ci, int h, int w, const float* dz, const float* y,
+                                      int y_h16, const float* coef, int co, float* dw, float* slabs, hipStream_t s) {
+  if (co != 64 || ci < 1 || ci > 4) return hipErrorInvalidValue;
+  const long long items = (long long)n * cdiv(h - 2, 4) * cdiv(w - 2, 64);
+  const int grid = (int)(items < kFirstWgradSlabs ? items : kFirstWgradSlabs);
+  Src d;
+  d.ptr = dz;
+  d.H = h - 2;
+  d.W = w - 2;
+  d.C = 64;
+  if (y_h16)
+    first_wgrad_go<1, 1>(grid, ci, x, n, h, w, d, slabs, y, coef, s);
+  else
+    first_wgrad_go<1, 0>(grid, ci, x, n, h, w, d, slabs, y, coef, s);
+  return reduce_first_slabs(ci, grid, dw, slabs, s);
 }
 
 // ---------------------------------------------------------------------------

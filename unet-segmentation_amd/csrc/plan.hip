@@ -471,7 +471,8 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
   {
     Conv& L = p->L[0];
     Timer t(p, s, UNET_KC_STAGE1, conv_flops(L, n),
-            4.0 * n * ((double)p->cin * p->h * p->w + (double)L.ho * L.wo * L.co));
+            4.0 * n * (double)p->cin * p->h * p->w +
+                (p->prec == UNET_PREC_BF16 ? 2.0 : 4.0) * n * (double)L.ho * L.wo * L.co);
     CK(launch_conv_first_fwd(x, n, p->cin, p->h, p->w, P<float>(prm, L.pw), P<float>(prm, L.pw + 1), L.co,
                              c.f(L.y), train ? c.d(L.stats) : nullptr, s, p->prec == UNET_PREC_BF16));
   }
@@ -576,6 +577,26 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     Conv& L = p->L[l];
     const double M = (double)n * L.ho * L.wo;
     const int dy16 = p->prec == UNET_PREC_BF16 && l > 0;
+    if (l == 0) {
+      // stage 1 backward: BN0 backward fused into inc.c0's weight
+      // gradient -- reads dz0, y0 and x once, dY(0) is never materialised
+      {
+        Timer t(p, s, UNET_KC_STAGE1, 0, 0);
+        CK(launch_bnb_finalize(c.d(L.bstats), L.co, M, P<float>(prm, L.pw + 2), c.f(L.mean), c.f(L.invstd),
+                               P<float>(grd, L.gw + 2), P<float>(grd, L.gw + 3), P<float>(grd, L.gw + 1),
+                               c.f(L.coef), s));
+      }
+      if (conc) {
+        CK(hipEventRecord(p->ev_dy[l], s));
+        CK(hipStreamWaitEvent(sw, p->ev_dy[l], 0));
+      }
+      Timer t(p, sw, UNET_KC_STAGE1, 2.0 * M * L.co * L.ci * 9,
+              4.0 * n * ((double)p->cin * p->h * p->w) +
+                  (p->prec == UNET_PREC_BF16 ? 6.0 : 8.0) * n * (double)L.ho * L.wo * L.co);
+      CK(launch_conv_first_wgrad_bn(x, n, p->cin, p->h, p->w, c.f(L.dz), c.f(L.y), p->prec == UNET_PREC_BF16,
+                                    c.f(L.coef), L.co, P<float>(grd, L.gw), c.f(p->first_slabs), sw));
+      continue;
+    }
     CK(launch_bnb_finalize(c.d(L.bstats), L.co, M, P<float>(prm, L.pw + 2), c.f(L.mean), c.f(L.invstd),
                            P<float>(grd, L.gw + 2), P<float>(grd, L.gw + 3), P<float>(grd, L.gw + 1), c.f(L.coef), s));
     {
@@ -596,12 +617,6 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     dy.C = L.co;
     dy.oy = dy.ox = 2;
     dy.h16 = dy16;
-    if (l == 0) {
-      Timer t(p, sw, UNET_KC_STAGE1, 2.0 * M * L.co * L.ci * 9,
-              4.0 * n * ((double)p->cin * p->h * p->w + (double)L.ho * L.wo * L.co));
-      CK(launch_conv_first_wgrad(x, n, p->cin, p->h, p->w, dy, L.co, P<float>(grd, L.gw), c.f(p->first_slabs), sw));
-      continue;
-    }
     // weight gradient
     {
       WgradArgs w;
@@ -946,7 +961,8 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     Conv& L = p->L[l];
     const long long pix = (long long)n * L.ho * L.wo;
     L.dz = al.take(fsz(pix * L.co));
-    L.dyp = al.take(fsz((long long)n * (L.ho + 4) * (L.wo + 4) * L.co));
+    if (l > 0)  // dY(0) is formed inside inc.c0's weight-gradient kernel
+      L.dyp = al.take(fsz((long long)n * (L.ho + 4) * (L.wo + 4) * L.co));
   }
   for (int k = 0; k < 4; ++k) {
     ConvT& T = p->T[k];

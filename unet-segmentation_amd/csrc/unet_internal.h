@@ -167,6 +167,10 @@ constexpr int kFirstWgradSlabs = 2048;
 size_t conv_first_wgrad_ws_bytes(int ci);
 hipError_t launch_conv_first_wgrad(const float* x_nchw, int n, int ci, int h, int w,
                                    const Src& dy, int co, float* dw_oihw, float* slabs, hipStream_t s);
+// inc.c0 weight gradient with the BN0 backward fused in (reads dz, y, x; coef =
+// k_bnb_finalize's [k0|k1|k2|mean] per channel)
+hipError_t launch_conv_first_wgrad_bn(const float* x, int n, int ci, int h, int w, const float* dz, const float* y,
+                                      int y_h16, const float* coef, int co, float* dw, float* slabs, hipStream_t s);
 
 // BN finalize (train): stats[G][C][2] -> mean, invstd, scale, shift; running update.
 hipError_t launch_bn_finalize(const double* stats, int c, double count, const float* gamma,
