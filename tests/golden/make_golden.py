@@ -110,8 +110,11 @@ def full_size_train_case(tag, n, h, n_channels=1, seed=5):
     the updated running statistics (models/unet_model.py:105-146,
     utils/losses.py:49-57, scripts/train.py:114-131).  The same step is run a
     second time in fp32 (the reference's own arithmetic on torch CPU): its
-    gradient digests (g32norm/, g32val/) give the per-tensor fp32 noise floor
-    the GPU tolerances are set against."""
+    gradient digests (g32norm/, g32val/) and those of the NumPy restatement run
+    in float32 (gnp32norm/, gnp32val/) give the per-tensor fp32 noise floor the
+    GPU tolerances are set against (two samples: oneDNN's CPU convolutions are
+    markedly more accurate than a plain fp32 GEMM on some deep-layer entries).
+    """
     params = O.hash_init(n_channels, 2, seed=seed, bn_random=True)
     x, tgt, wmap = F.make_inputs(seed, n, n_channels, h)
     out = {"x_seed": np.array(seed), "n": np.array(n), "h": np.array(h), "c": np.array(n_channels)}
@@ -140,6 +143,16 @@ def full_size_train_case(tag, n, h, n_channels=1, seed=5):
             if "running" in name:
                 out[f"buf/{name}"] = b.detach().numpy().copy()
         del m, logits, loss
+    # a second plain-fp32 sample with a different summation order: the build's
+    # NumPy restatement (oracle/unet_oracle.py) in float32 (gnp32norm/, gnp32val/)
+    net = O.UNetOracle(params, dtype=np.float32)
+    lg, cache, _ = net.forward(x)
+    _, dl = O.weighted_ce(lg, tgt, wmap)
+    g = net.backward(dl.astype(np.float32), cache)
+    for name in g:
+        v = np.asarray(g[name], np.float64).ravel()
+        out[f"gnp32norm/{name}"] = np.array(np.linalg.norm(v))
+        out[f"gnp32val/{name}"] = v[out[f"gidx/{name}"]]
     path = os.path.join(HERE, f"train_{tag}.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")

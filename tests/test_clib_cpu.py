@@ -123,3 +123,16 @@ def test_state_dict_roundtrip_with_reference_layout():
     sd = m.state_dict()
     for k, v in params.items():
         np.testing.assert_array_equal(sd[k].numpy(), np.asarray(v))
+
+
+def test_host_sanitizer_selftest():
+    """The library's host logic under AddressSanitizer + UBSan
+    (csrc/Makefile `sanitize`, built by __graft_entry__.build())."""
+    import subprocess
+    exe = os.path.join(os.path.dirname(__file__), "..", "build", "asan", "host_selftest")
+    if not os.path.exists(exe):
+        pytest.skip("host_selftest not built (make -C unet-segmentation_amd/csrc sanitize)")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "all checks passed" in r.stdout

@@ -36,8 +36,11 @@ def run_ranks(tmp_path, overlap, world=2):
     port = _free_port()
     procs, outs = [], []
     for r in range(world):
+        # fixed GEMM variants (no autotuning) in every process: the comparison is
+        # then between identical kernels, not between timing-dependent tile
+        # choices whose different roundings small-sample BatchNorm amplifies
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port))
+                   MASTER_PORT=str(port), UNET_AUTOTUNE="0")
         out = str(tmp_path / f"rank{r}.npz")
         outs.append(out)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, str(int(overlap)),
@@ -56,6 +59,16 @@ def run_ranks(tmp_path, overlap, world=2):
 
 def single_process_reference(world=2):
     """Per-shard GPU gradients without a process group, averaged on the host."""
+    from unet_amd import UNet, _lib
+    from unet_amd.train import Trainer
+    _lib.load().unet_set_tuning(b"autotune", 0)
+    try:
+        return _single_process_reference(world)
+    finally:
+        _lib.load().unet_set_tuning(b"autotune", 1)
+
+
+def _single_process_reference(world):
     from unet_amd import UNet
     from unet_amd.train import Trainer
     params = O.hash_init(1, 2, seed=W.SEED, bn_random=True)
@@ -89,7 +102,7 @@ def test_two_rank_trainer_matches_shard_average(tmp_path, overlap):
     # = the host average of the shards' gradients (SUM, then 1/world in SGD)
     for s in range(STEPS):
         g, ref = ranks[0][f"grad{s}"], sums[s]
-        assert np.abs(g - ref).max() <= 1e-4 * np.abs(ref).max(), (s, np.abs(g - ref).max())
+        assert np.abs(g - ref).max() <= 1e-5 * np.abs(ref).max(), (s, np.abs(g - ref).max())
     p = ranks[0]["params"]
     assert np.abs(p - params).max() <= 1e-5 * np.abs(params).max()
     # the shards differ, so the per-rank BN running statistics differ until

@@ -432,11 +432,14 @@ def _bits(packed, w):
 
 def check_grad_digests(named_grads, z, rel=1e-2, vtol=2e-2):
     """Gradients vs the reference's fp64 digests (norm + 32 sampled entries per
-    tensor): norm within max(rel, 2 x the reference's own fp32 deviation) and
-    samples within max(vtol x max|sample|, 3 x that deviation per entry) when
-    the fixture records its fp32 run (g32norm/, g32val/) -- BatchNorm makes
-    some deep-layer gradients sensitive to fp32 rounding (measured up to a few
-    % on sampled entries).  The 22 BN-cancelled biases are compared absolutely."""
+    tensor).  When the fixture records plain-fp32 runs of the same step (the
+    reference on torch CPU: g32*, the NumPy restatement in float32: gnp32*),
+    their deviation from fp64 is the tensor's fp32 noise floor: norm within
+    max(rel, 2 x the larger norm deviation), samples within max(vtol x
+    max|sample|, 2 x the largest sample deviation of either run) -- BatchNorm
+    makes deep-layer entries sensitive to summation order (a plain fp32 run
+    lands up to ~9 % of max|sample| away on some tensors at 512^2).  The 22
+    BN-cancelled biases are compared absolutely."""
     worst = 0.0
     for name, g in named_grads:
         g = g.detach().double().cpu().numpy().ravel()
@@ -446,10 +449,12 @@ def check_grad_digests(named_grads, z, rel=1e-2, vtol=2e-2):
             assert np.abs(g).max() <= 1e-3 * wn, name
             continue
         idx, ref = z[f"gidx/{name}"], z[f"gval/{name}"]
-        nfl = abs(float(z[f"g32norm/{name}"]) - ref_norm) if f"g32norm/{name}" in z.files else 0.0
-        vfl = np.abs(z[f"g32val/{name}"] - ref) if f"g32val/{name}" in z.files else 0.0
+        nfl = max([abs(float(z[f"{p}norm/{name}"]) - ref_norm) for p in ("g32", "gnp32")
+                   if f"{p}norm/{name}" in z.files] + [0.0])
+        vfl = max([float(np.abs(z[f"{p}val/{name}"] - ref).max()) for p in ("g32", "gnp32")
+                   if f"{p}val/{name}" in z.files] + [0.0])
         ntol = max(rel * ref_norm, 2 * nfl)
-        vt = np.maximum(vtol * np.abs(ref).max(), 3 * vfl) + 1e-7
+        vt = max(vtol * np.abs(ref).max(), 2 * vfl) + 1e-7
         assert abs(np.linalg.norm(g) - ref_norm) <= ntol, (name, np.linalg.norm(g), ref_norm, nfl)
         assert np.all(np.abs(g[idx] - ref) <= vt), (name, np.abs(g[idx] - ref).max(), vt.max())
         worst = max(worst, abs(np.linalg.norm(g) - ref_norm) / ntol, float((np.abs(g[idx] - ref) / vt).max()))
