@@ -260,7 +260,8 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  split) the first time it meets a GEMM shape and caches the
  *                  fastest per shape; 0 = built-in heuristic only.
  *  "igemm_variant" heuristic override for A/B measurements (-1 = off, 1..9 =
- *                  forced tile shape; 21-26, 31-36 bf16 tiles); "wgrad_variant"
+ *                  forced tile shape; 21-26, 31-36, 41-44 bf16 tiles, 61-66
+ *                  bf16 halo tiles with LDS-DMA weights); "wgrad_variant"
  *                  (-1 = off, 1 = 64x64 tile, 2..9 = workgroups per CU for the
  *                  pixel split; bf16 GEMMs: 10-14, 20-21 = forced bf16 tile);
  *  "concurrent"    1 (default, or env UNET_CONCURRENT) = a plan's backward
@@ -271,7 +272,12 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  it (tests; 1-4, 6-9 register-staged, 11-14 LDS-DMA, 21-26
  *                  bf16 operands -- only in UNET_PREC_BF16 / _BF16X3 plans).
  *  "op_precision"  UNET_PREC_* of the per-op GEMM entry points below
- *                  (unet_conv3x3_*, unet_convT2_*); default fp32. */
+ *                  (unet_conv3x3_*, unet_convT2_*); default fp32.
+ *  "op_a16"        1 = with op_precision UNET_PREC_BF16, unet_conv3x3_fwd /
+ *                  _dgrad store their A operand bf16 first (x rounded before
+ *                  the BN+ReLU transform; padded dY bf16), as a bf16 plan
+ *                  does -- the configuration the 61-66 tiles (bf16-stored A
+ *                  only) run in; 0 (default) = fp32 A. */
 int unet_set_tuning(const char* key, int value);
 /* Text report of the tuned GEMM choices (one line per shape: key, heuristic
  * time, chosen variant and time).  Copies up to len-1 bytes + NUL into buf

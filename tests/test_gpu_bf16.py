@@ -140,6 +140,64 @@ def test_bf16_conv3x3_dgrad(op_bf16, n, h, w, ci, co, variant):
     assert rel_err(host(dx), ref) < 5e-5
 
 
+# k_conv3_dma (conv3_dma.hip): TH x 32 tiles, LDS-DMA weights, 2-stage ring;
+# bf16-stored A only, so the per-op entry points run with op_a16 = 1 (x stored
+# bf16 before its transform / padded dY bf16, as in a bf16 plan)
+DMA = [61, 62, 63, 64, 65, 66]
+
+
+@pytest.mark.parametrize("variant", DMA + [31, 33])
+@pytest.mark.parametrize("n,h,w,ci,co,tf", [(2, 14, 13, 64, 128, False), (2, 11, 17, 64, 64, True),
+                                              (1, 30, 41, 128, 256, True), (3, 9, 9, 256, 64, False),
+                                              (1, 40, 70, 64, 64, True)])
+def test_bf16_conv3x3_fwd_a16(op_bf16, n, h, w, ci, co, tf, variant):
+    lib = op_bf16
+    lib.unet_set_tuning(b"op_a16", 1)
+    try:
+        lib.unet_set_tuning(b"igemm_variant", variant)
+        rng = np.random.default_rng(12)
+        x = f32(rng.standard_normal((n, h, w, ci)))
+        wt = f32(rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci))
+        b = f32(rng.standard_normal(co))
+        sc = f32(rng.uniform(-0.5, 1.5, ci)) if tf else None
+        sh = f32(rng.standard_normal(ci) * 0.3) if tf else None
+        xq = f32(q(x))
+        xin = np.maximum(f32(xq * sc + sh), 0) if tf else xq
+        ref = O.conv_valid_fwd(q(xin), q(wt), b)
+        y = torch.empty((n, h - 2, w - 2, co), device="cuda")
+        ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
+        ck(lib.unet_conv3x3_fwd(dev(x).data_ptr(), n, h, w, ci, dev(wt).data_ptr(), dev(b).data_ptr(), co,
+                                dev(sc).data_ptr() if tf else None, dev(sh).data_ptr() if tf else None,
+                                y.data_ptr(), ws.data_ptr(), stream()))
+        torch.cuda.synchronize()
+        assert rel_err(host(y), ref) < 5e-5
+    finally:
+        lib.unet_set_tuning(b"op_a16", 0)
+
+
+@pytest.mark.parametrize("variant", DMA)
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 19, 40, 128, 64), (2, 8, 8, 64, 256),
+                                         (1, 36, 66, 64, 128)])
+def test_bf16_conv3x3_dgrad_a16(op_bf16, n, h, w, ci, co, variant):
+    lib = op_bf16
+    lib.unet_set_tuning(b"op_a16", 1)
+    try:
+        lib.unet_set_tuning(b"igemm_variant", variant)
+        rng = np.random.default_rng(13)
+        x = f32(rng.standard_normal((n, h, w, ci)))
+        wt = f32(rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci))
+        dy = f32(rng.standard_normal((n, h - 2, w - 2, co)))
+        ref, _, _ = O.conv_valid_bwd(x, q(wt), q(dy))
+        dx = torch.empty((n, h, w, ci), device="cuda")
+        ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
+        ck(lib.unet_conv3x3_dgrad(dev(dy).data_ptr(), n, h, w, ci, dev(wt).data_ptr(), co, dx.data_ptr(),
+                                  ws.data_ptr(), stream()))
+        torch.cuda.synchronize()
+        assert rel_err(host(dx), ref) < 5e-5
+    finally:
+        lib.unet_set_tuning(b"op_a16", 0)
+
+
 @pytest.mark.parametrize("variant", [-1, 10, 12, 20, 21])
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 40, 37, 128, 128), (2, 10, 9, 64, 128),
                                          (1, 7, 5, 64, 64), (2, 21, 44, 192, 128)])
@@ -277,7 +335,9 @@ def gemm_mode(request, lib):
 @pytest.mark.parametrize("gemm_mode", ["heuristic", "tile21", "tile22", "tile23", "tile24", "tile25", "tile26",
                                        "tile22+split3", "tile24+split8", "tile31", "tile32", "tile33", "tile34",
                                        "tile35", "tile36", "tile31+split2", "tile34+split3", "tile41", "tile42",
-                                       "tile43", "tile44", "tile41+split3"], indirect=True)
+                                       "tile43", "tile44", "tile41+split3", "tile61", "tile62", "tile63",
+                                       "tile64", "tile65", "tile66", "tile61+split3", "tile63+split2"],
+                         indirect=True)
 def test_bf16_gemm_variants_vs_bf16_oracle(gemm_mode):
     """Every bf16 tile (21-26 row gather, 31-36 halo-tiled 3x3 -- the convT GEMMs
     fall back to the built-in tile there) and split-K on every conv / convT /

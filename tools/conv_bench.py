@@ -30,6 +30,7 @@ SHAPES = [
     ("up4.c1", 8, 326, 326, 64, 64),
 ]
 VARIANTS = [-1, 21, 22, 23, 24, 31, 32, 33, 34, 35, 36, 41, 42, 43, 44]
+DMA_VARIANTS = [31, 33, 61, 62, 63, 64, 65, 66]
 
 
 def main():
@@ -38,17 +39,27 @@ def main():
     ap.add_argument("--dgrad", action="store_true")
     ap.add_argument("--wgrad", action="store_true", help="time the weight gradient over wgrad variants")
     ap.add_argument("--prec", type=int, default=1, help="0 = fp32, 1 = bf16 operands, 2 = bf16x3 split operands")
+    ap.add_argument("--a16", action="store_true", help="bf16-stored A as in a bf16 plan (op_a16; tiles 61-66)")
+    ap.add_argument("--variants", default=None, help="comma-separated variant ids")
+    ap.add_argument("--shapes", default=None, help="comma-separated shape names")
     args = ap.parse_args()
     lib = _lib.load()
     lib.unet_set_tuning(b"op_precision", args.prec)
+    lib.unet_set_tuning(b"op_a16", int(args.a16))
     variants = {0: [-1, 1, 2, 3, 4, 8, 11, 12, 13, 14, 51, 52, 53, 54], 1: VARIANTS,
                 2: [-1, 21, 22, 23, 24, 25, 26, 31, 33, 35]}[args.prec]
+    if args.a16:
+        variants = DMA_VARIANTS
+    if args.variants:
+        variants = [int(v) for v in args.variants.split(",")]
     knob = b"igemm_variant"
     if args.wgrad:  # -1 built-in; fp32 22/23 halo; bf16 / bf16x3 10-14 pixel-column, 20/21 halo
         knob = b"wgrad_variant"
         variants = [-1, 1, 22, 23] if args.prec == 0 else [-1, 10, 12, 13, 20, 21]
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for name, n, h, w, ci, co in SHAPES:
+        if args.shapes and name not in args.shapes.split(","):
+            continue
         g = torch.Generator(device="cuda").manual_seed(0)
         x = torch.randn((n, h, w, ci), device="cuda", generator=g)
         wt = torch.randn((co, ci, 3, 3), device="cuda", generator=g) / (3 * ci ** 0.5)
@@ -102,6 +113,7 @@ def main():
     lib.unet_set_tuning(b"igemm_variant", -1)
     lib.unet_set_tuning(b"wgrad_variant", -1)
     lib.unet_set_tuning(b"op_precision", 0)
+    lib.unet_set_tuning(b"op_a16", 0)
 
 
 if __name__ == "__main__":

@@ -112,6 +112,13 @@ struct LinearRows {
     m = m0 + row;
     return m < M;
   }
+  // fragment block fr (tile rows fr*32 ..): the row of accumulator register r
+  // of a lane in half h is mb + k_r (k_r = (r & 3) + 8 (r >> 2)), valid iff
+  // k_r < lim
+  __device__ __forceinline__ void block(int fr, int h, int& mb, int& lim) const {
+    mb = m0 + fr * 32 + 4 * h;
+    lim = M - mb;
+  }
 };
 // Tile pixel of GEMM row p (32 rows per MFMA fragment).  Row-major, except in
 // 16 x 16 tiles read from 80-B LDS rows: there fragment f holds tile rows f and
@@ -140,7 +147,67 @@ struct HaloRows {
     m = (n * Hg + y) * Wg + x;
     return y < Hg && x < Wg;
   }
+  // 32-wide tiles: fragment block fr is tile row fr (see LinearRows::block)
+  __device__ __forceinline__ void block(int fr, int h, int& mb, int& lim) const {
+    const int y = y0 + fr;
+    mb = (n * Hg + y) * Wg + x0 + 4 * h;
+    lim = y < Hg ? Wg - x0 - 4 * h : 0;
+  }
 };
+
+template <class R>
+struct fast_rows : std::false_type {};
+template <>
+struct fast_rows<LinearRows> : std::true_type {};
+template <int TH>
+struct fast_rows<HaloRows<32, TH>> : std::true_type {};
+
+// Column statistics of an epilogue (BN sums, BN-backward sums, concat column
+// sums): wave halves, then waves of a column block through LDS, then one fp64
+// atomic per column per workgroup into a spread group.
+template <int BN, int WM, int WN, int NT, int TN>
+__device__ __forceinline__ void igemm_finish_stats(const Epilogue& e, float (&s1)[TN], float (&s2)[TN],
+                                                   float (&t1)[TN], int n0, int wn, int N, int tid, float* red) {
+  const int lane = tid & 63, h = lane >> 5, li = lane & 31;
+  const int wm = (tid >> 6) / WN;
+  const bool want_stats = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
+  if (!want_stats) return;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    s1[j] += __shfl_xor(s1[j], 32);
+    s2[j] += __shfl_xor(s2[j], 32);
+    t1[j] += __shfl_xor(t1[j], 32);
+  }
+  if (h == 0) {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int lc = wn * TN * 32 + j * 32 + li;
+      red[(wm * 3 + 0) * BN + lc] = s1[j];
+      red[(wm * 3 + 1) * BN + lc] = s2[j];
+      red[(wm * 3 + 2) * BN + lc] = t1[j];
+    }
+  }
+  __syncthreads();
+  const int grp = blockIdx.x % kStatGroups;
+  const int nsplit = min(e.n_split, N);
+  for (int lc = tid; lc < BN; lc += NT) {
+    float a = 0.f, b = 0.f, c = 0.f;
+#pragma unroll
+    for (int w = 0; w < WM; ++w) { a += red[(w * 3 + 0) * BN + lc]; b += red[(w * 3 + 1) * BN + lc]; c += red[(w * 3 + 2) * BN + lc]; }
+    const int col = n0 + lc;
+    if (col < nsplit) {
+      double* st = e.yref ? e.bstats : e.stats;
+      if (st) {
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b);
+      }
+    } else if (e.colsum1) {
+      const int n2 = N - nsplit;
+      atomicAdd(e.colsum1 + (size_t)grp * n2 + (col - nsplit), (double)c);
+    }
+  }
+}
+
 
 // Split-K partial store or the full epilogue of an implicit-GEMM tile: bias,
 // destination mapping (linear / pixel shuffle / cropped), ReLU mask + BN-bwd
@@ -178,6 +245,63 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
   float s1[TN], s2[TN], t1[TN];
 #pragma unroll
   for (int j = 0; j < TN; ++j) { s1[j] = 0.f; s2[j] = 0.f; t1[j] = 0.f; }
+
+  // Fast path (the common case: every 3x3 conv forward / input gradient of the
+  // plan): destinations laid out on the gather grid itself, no pixel shuffle.
+  // Row bases come per fragment block, a register's element offset is the base
+  // plus a compile-time multiple of the (uniform) channel count: a handful of
+  // VALU per element instead of a per-element pixel decomposition -- the
+  // epilogue is a large share of the small-K (64 / 128-channel) GEMMs.
+  if constexpr (fast_rows<RowMap>::value) {
+    auto lin = [&](const Dst& d) { return d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg; };
+    if (!e.shuffle_co && lin(e.d[0]) && (e.n_split >= N || lin(e.d[1]))) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int col = n0 + wn * TN * 32 + j * 32 + li;
+        const float bias = e.bias ? e.bias[col] : 0.f;
+        const bool second = col >= e.n_split;  // uniform per 32-column block (n_split % 32 == 0)
+        float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
+        const int dC = second ? e.d[1].C : e.d[0].C;
+        const int dh16 = second ? e.d[1].h16 : e.d[0].h16;
+        const int dcol = second ? col - e.n_split : col;
+        const bool bwd_mask = (e.yref != nullptr) && !second;
+        float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
+        if (bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          int mb, lim;
+          rows.block(wm * TM + i, h, mb, lim);
+          const unsigned ib = (unsigned)mb * (unsigned)dC + (unsigned)dcol;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int k = (r & 3) + 8 * (r >> 2);
+            if (k >= lim) continue;
+            const unsigned idx = ib + (unsigned)(k * dC);
+            float v = acc[i][j][r] + bias;
+            if (e.stats && dh16) v = round_bf(v);
+            if (bwd_mask) {
+              const float yv = e.yref_h16 ? __uint_as_float((unsigned)reinterpret_cast<const uint16_t*>(e.yref)[idx] << 16)
+                                          : e.yref[idx];
+              v = (fmaf(yv, bsc, bsh) > 0.f) ? v : 0.f;
+              s1[j] += v;
+              s2[j] += v * ((yv - bmu) * bis);
+            } else if (e.stats) {
+              s1[j] += v;
+              s2[j] += v * v;
+            } else if (second && e.colsum1) {
+              t1[j] += v;
+            }
+            if (dh16)
+              reinterpret_cast<uint16_t*>(dptr)[idx] = bf16_of(v);
+            else
+              dptr[idx] = v;
+          }
+        }
+      }
+      igemm_finish_stats<BN, WM, WN, NT>(e, s1, s2, t1, n0, wn, N, tid, red);
+      return;
+    }
+  }
 
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -229,42 +353,7 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
       }
     }
   }
-  const bool want_stats = (e.stats != nullptr) || (e.yref != nullptr) || (e.colsum1 != nullptr);
-  if (!want_stats) return;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    s1[j] += __shfl_xor(s1[j], 32);
-    s2[j] += __shfl_xor(s2[j], 32);
-    t1[j] += __shfl_xor(t1[j], 32);
-  }
-  if (h == 0) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int lc = wn * TN * 32 + j * 32 + li;
-      red[(wm * 3 + 0) * BN + lc] = s1[j];
-      red[(wm * 3 + 1) * BN + lc] = s2[j];
-      red[(wm * 3 + 2) * BN + lc] = t1[j];
-    }
-  }
-  __syncthreads();
-  const int grp = blockIdx.x % kStatGroups;
-  const int nsplit = min(e.n_split, N);
-  for (int lc = tid; lc < BN; lc += NT) {
-    float a = 0.f, b = 0.f, c = 0.f;
-#pragma unroll
-    for (int w = 0; w < WM; ++w) { a += red[(w * 3 + 0) * BN + lc]; b += red[(w * 3 + 1) * BN + lc]; c += red[(w * 3 + 2) * BN + lc]; }
-    const int col = n0 + lc;
-    if (col < nsplit) {
-      double* st = e.yref ? e.bstats : e.stats;
-      if (st) {
-        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
-        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b);
-      }
-    } else if (e.colsum1) {
-      const int n2 = N - nsplit;
-      atomicAdd(e.colsum1 + (size_t)grp * n2 + (col - nsplit), (double)c);
-    }
-  }
+  igemm_finish_stats<BN, WM, WN, NT>(e, s1, s2, t1, n0, wn, N, tid, red);
 }
 
 }  // namespace unet

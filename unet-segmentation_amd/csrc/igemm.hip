@@ -1106,6 +1106,14 @@ static TileInfo tile_info(int id) {
     case 35: return {128, 64, 288, 2};
     case 36: return {256, 128, 288, 1};
     case 41: case 42: case 43: case 44: return {256, 64, 288, 1};  // persistent k_conv3p_bf
+    // bf16 halo-tiled 3x3 with LDS-DMA weights and a 2-stage ring (k_conv3_dma,
+    // conv3_dma.hip): bk = one channel chunk (16 or 32) x 9 taps
+    case 61: return {256, 128, 144, 1};
+    case 62: return {512, 128, 144, 1};
+    case 63: return {256, 64, 144, 2};
+    case 64: return {256, 64, 288, 1};
+    case 65: return {512, 64, 144, 1};
+    case 66: return {512, 64, 288, 1};
     // fp32 halo-tiled 3x3 (k_conv3_f32): bk = one 16-channel chunk x 9 taps
     case 51: return {256, 64, 144, 2};
     case 52: return {256, 64, 144, 2};
@@ -1116,7 +1124,8 @@ static TileInfo tile_info(int id) {
 }
 
 static bool is_halo_tile(int tile) { return (tile >= 31 && tile <= 36) || (tile >= 41 && tile <= 44); }
-static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_halo_tile(tile); }
+static bool is_dma_tile(int tile) { return tile >= 61 && tile <= 66; }
+static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile); }
 static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 
 // A tile applies when the shape divides and the packed B operand is in the
@@ -1128,6 +1137,13 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   if (is_halo_tile(tile))  // 3x3 stride-1 gathers only (conv fwd / dgrad), K = 9 x Cg
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
+  if (is_dma_tile(tile)) {  // bf16-stored A sources, no split operands
+    const int ch = tile_info(tile).bk / 9;
+    const bool two = a.a.c_split < a.a.Cg;
+    return a.bh != nullptr && a.bl == nullptr && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 &&
+           a.a.stride == 1 && a.K == 9 * a.a.Cg && a.a.Cg % ch == 0 && a.a.c_split % ch == 0 && a.a.Cg <= 1024 &&
+           a.a.s[0].h16 && (!two || a.a.s[1].h16);
+  }
   if (is_halo32_tile(tile))
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 16 == 0 && a.a.c_split % 16 == 0;
@@ -1137,9 +1153,11 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
 long long igemm_tile_count(const IgemmArgs& a, int tile) {
   const TileInfo t = tile_info(tile);
   if (t.bm == 0) return 0;
-  int th, tw, bn;
+  int th, tw, bn, ch;
   if (halo_tile_shape(tile, th, tw, bn))
     return (long long)a.a.nimg * ((a.a.Hg + th - 1) / th) * ((a.a.Wg + tw - 1) / tw) * (a.N / bn);
+  if (conv3_dma_tile_shape(tile, th, bn, ch))
+    return (long long)a.a.nimg * ((a.a.Hg + th - 1) / th) * ((a.a.Wg + 31) / 32) * (a.N / bn);
   return (long long)((a.M + t.bm - 1) / t.bm) * (a.N / t.bn);
 }
 int igemm_tile_slots(int tile) { return tile_info(tile).slots; }
@@ -1210,6 +1228,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 21: case 22: case 23: case 24: case 25: case 26:
     case 31: case 32: case 33: case 34: case 35: case 36:
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
+    case 61: case 62: case 63: case 64: case 65: case 66: return go_conv3_dma_tile(a, s, tile);
     case 51: return go_halo32<8, 32, 64, 8, 1, 4>(a, s);
     case 52: return go_halo32<16, 16, 64, 8, 1, 4>(a, s);
     case 53: return go_halo32<8, 32, 64, 4, 1, 2>(a, s);

@@ -463,7 +463,40 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     halo_pix<TH, TW>(p, ty, tx);
     abase[i] = ty * HW2 + tx;
   }
+  // 18 (tap, 16-k) steps; the fragments of step t+1 are read while step t's
+  // MFMAs issue (register double buffer), so each wave keeps one step of LDS
+  // reads in flight instead of waiting on every read
+  auto compute_pipe = [&] {
+    bf16x8_t fa[2][TM], fb[2][TN];
+    auto load = [&](int step, int buf) {
+      const int tap = step >> 1, s = step & 1;
+      const int off = (tap / 3) * HW2 + tap % 3;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        fa[buf][i] = *reinterpret_cast<const bf16x8_t*>(As + (abase[i] + off) * LDR + 16 * s + 8 * h);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+        fb[buf][j] = *reinterpret_cast<const bf16x8_t*>(Bs + (tap * BN + wn * TN * 32 + j * 32 + li) * LDR + 16 * s + 8 * h);
+    };
+    load(0, 0);
+#pragma unroll
+    for (int step = 0; step < 18; ++step) {
+      if (step + 1 < 18) load(step + 1, (step + 1) & 1);
+      // keep the scheduler from sinking the next step's reads below this step's
+      // MFMAs (it otherwise re-serialises read -> wait -> MFMA)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[step & 1][i], fb[step & 1][j], acc[i][j], 0, 0, 0);
+    }
+  };
   auto compute = [&] {
+    if constexpr (!SPLIT) {
+      compute_pipe();
+      return;
+    }
 #pragma unroll
     for (int tap = 0; tap < 9; ++tap) {
       const int off = (tap / 3) * HW2 + tap % 3;

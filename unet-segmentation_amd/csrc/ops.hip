@@ -22,6 +22,12 @@ inline size_t al256(size_t b) { return (b + 255) / 256 * 256; }
 // unet_set_tuning("op_precision", UNET_PREC_*): GEMM arithmetic of the per-op
 // entry points (the plan has its own, unet_plan_create_ex)
 int g_op_prec = UNET_PREC_FP32;
+// unet_set_tuning("op_a16", 1): with op_precision UNET_PREC_BF16 the 3x3
+// conv entry points store their A operand in bf16 first, as a bf16 plan does
+// (raw conv outputs and padded dY are bf16 there): the conv forward rounds x to
+// bf16 before its BN+ReLU transform, the input gradient stores the padded dY
+// bf16.  Lets op-level tests and tools run the plan's exact GEMM configuration.
+int g_op_a16 = 0;
 
 // bf16 / split per-op GEMMs: round the packed fp32 B (n elements) into
 // `scratch` (4n bytes: hi plane, then the lo plane of split operands) and point
@@ -50,7 +56,8 @@ size_t unet_conv_ws_bytes(int n, int h, int w, int ci, int co) {
   const size_t wb = al256(sizeof(float) * 9 * (size_t)ci * co);
   const size_t pad = al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co);  // (h-2+4)
   const size_t misc = al256(sizeof(float) * 4 * co) + al256(sizeof(double) * kStatGroups * 2 * co);
-  return 2 * wb + pad + misc;
+  const size_t x16 = al256(sizeof(uint16_t) * (size_t)n * h * w * ci);  // op_a16: bf16 copy of x
+  return 2 * wb + pad + misc + x16;
 }
 
 int unet_conv3x3_fwd(const float* x, int n, int h, int w, int ci, const float* wt, const float* bias, int co,
@@ -67,6 +74,15 @@ int unet_conv3x3_fwd(const float* x, int n, int h, int w, int ci, const float* w
   x0.C = ci;
   x0.scale = xs;
   x0.shift = xb;
+  if (g_op_prec == UNET_PREC_BF16 && g_op_a16) {
+    const size_t wb = al256(sizeof(float) * 9 * (size_t)ci * co);
+    const size_t off = 2 * wb + al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co) +
+                       al256(sizeof(float) * 4 * co) + al256(sizeof(double) * kStatGroups * 2 * co);
+    uint16_t* x16 = reinterpret_cast<uint16_t*>(reinterpret_cast<char*>(ws) + off);
+    OPCK(launch_f2bf(x, x16, (size_t)n * h * w * ci, s));
+    x0.ptr = reinterpret_cast<const float*>(x16);
+    x0.h16 = 1;
+  }
   a.a.s[0] = a.a.s[1] = x0;
   a.a.Cg = a.a.c_split = ci;
   a.a.taps_h = a.a.taps_w = 3;
@@ -99,10 +115,12 @@ int unet_conv3x3_dgrad(const float* dy, int n, int h, int w, int ci, const float
   // zero-bordered copy of dy: dYpad = 1*dy + 0*(y-0) + 0
   OPCK(launch_fill(coef, co, 1.f, s));
   OPCK(launch_fill(coef + co, 3 * (size_t)co, 0.f, s));
-  OPCK(launch_bnb_apply(dy, dy, coef, n, h - 2, w - 2, co, dyp, 2, s));
+  const int dy16 = g_op_prec == UNET_PREC_BF16 && g_op_a16;
+  OPCK(launch_bnb_apply(dy, dy, coef, n, h - 2, w - 2, co, dyp, 2, s, dy16, 0));
   IgemmArgs a;
   Src d;
   d.ptr = dyp;
+  d.h16 = dy16;
   d.H = h + 2;
   d.W = w + 2;
   d.C = co;
@@ -353,6 +371,7 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "force_split") g_force_split = value;
   else if (k == "force_tile") g_force_tile = value;
   else if (k == "concurrent") g_concurrent = value;
+  else if (k == "op_a16") g_op_a16 = value != 0;
   else if (k == "op_precision") {
     if (value != UNET_PREC_FP32 && value != UNET_PREC_BF16 && value != UNET_PREC_BF16X3) return -EINVAL;
     g_op_prec = value;

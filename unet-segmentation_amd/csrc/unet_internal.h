@@ -107,6 +107,9 @@ struct GemmChoice {
   int tile = -1;
   int split = 1;
 };
+// bf16 halo conv with LDS-DMA weights (conv3_dma.hip), tile ids 61-66
+bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch);
+hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);
 int num_cus();
 hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s);  // heuristic
 hipError_t launch_igemm_v(const IgemmArgs& a, hipStream_t s, GemmChoice c);
