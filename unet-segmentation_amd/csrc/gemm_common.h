@@ -217,7 +217,9 @@ template <int BM, int BN, int WM, int WN, int NT, class RowMap = LinearRows>
 __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&acc)[BM / (WM * 32)][BN / (WN * 32)],
                                              int m0, int n0, int wm, int wn, int tid, float* red,
                                              RowMap rows = RowMap{0, 0}) {
-  if constexpr (std::is_same<RowMap, LinearRows>::value) rows = LinearRows{m0, args.M};
+  if constexpr (std::is_same<RowMap, LinearRows>::value) {
+    if (rows.M == 0) rows = LinearRows{m0, args.M};  // callers may pass a batched bound
+  }
   constexpr int TM = BM / (WM * 32), TN = BN / (WN * 32);
   const Gather& g = args.a;
   const int M = args.M;

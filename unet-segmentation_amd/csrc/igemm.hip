@@ -57,9 +57,11 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // batched dense GEMMs (Winograd points): rows of batch z are z*batch_rows ..
+  const int zb = args.batch > 1 ? (int)blockIdx.z : 0;
+  const int m0 = zb * args.batch_rows + blockIdx.x * BM, n0 = blockIdx.y * BN;
   const Gather& g = args.a;
-  const int M = args.M, K = args.K;
+  const int M = args.batch > 1 ? (zb + 1) * args.batch_rows : args.M, K = args.K;
   const int col4 = tid % C4, row0 = tid / C4;
 
   // Per staged A row: pixel base in each source grid (before the tap offset).
@@ -78,12 +80,13 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   }
   const float* bptr[BV];
 #pragma unroll
-  for (int q = 0; q < BV; ++q) bptr[q] = args.b + (size_t)(n0 + row0 + RPP * q) * K + col4 * 4;
+  for (int q = 0; q < BV; ++q)
+    bptr[q] = args.b + (size_t)zb * args.batch_b + (size_t)(n0 + row0 + RPP * q) * K + col4 * 4;
 
   // K range of this workgroup (split-K slices chunks over blockIdx.z)
   const int nk_all = K / BK;
   int kc0 = 0, kc1 = nk_all;
-  if (args.ksplit > 1) {
+  if (args.ksplit > 1 && args.batch <= 1) {
     const int per = (nk_all + args.ksplit - 1) / args.ksplit;
     kc0 = blockIdx.z * per;
     kc1 = min(nk_all, kc0 + per);
@@ -246,7 +249,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   }
 
   __shared__ float red[WM * 3 * BN];
-  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, red);
+  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, red, LinearRows{m0, M});
 }
 
 
@@ -1108,12 +1111,12 @@ static TileInfo tile_info(int id) {
     case 41: case 42: case 43: case 44: return {256, 64, 288, 1};  // persistent k_conv3p_bf
     // bf16 halo-tiled 3x3 with LDS-DMA weights and a 2-stage ring (k_conv3_dma,
     // conv3_dma.hip): bk = one channel chunk (16 or 32) x 9 taps
-    case 61: return {256, 128, 144, 1};
-    case 62: return {512, 128, 144, 1};
     case 63: return {256, 64, 144, 2};
-    case 64: return {256, 64, 288, 1};
     case 65: return {512, 64, 144, 1};
     case 66: return {512, 64, 288, 1};
+    case 67: return {256, 64, 144, 2};
+    // Winograd F(2x2, 3x3) (winograd.hip): no K split
+    case 70: return {256, 64, 9, 2};
     // fp32 halo-tiled 3x3 (k_conv3_f32): bk = one 16-channel chunk x 9 taps
     case 51: return {256, 64, 144, 2};
     case 52: return {256, 64, 144, 2};
@@ -1124,7 +1127,7 @@ static TileInfo tile_info(int id) {
 }
 
 static bool is_halo_tile(int tile) { return (tile >= 31 && tile <= 36) || (tile >= 41 && tile <= 44); }
-static bool is_dma_tile(int tile) { return tile >= 61 && tile <= 66; }
+static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 67); }
 static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile); }
 static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 
@@ -1137,6 +1140,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   if (is_halo_tile(tile))  // 3x3 stride-1 gathers only (conv fwd / dgrad), K = 9 x Cg
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
+  if (tile == 70) return wino_applies(a);
   if (is_dma_tile(tile)) {  // bf16-stored A sources, no split operands
     const int ch = tile_info(tile).bk / 9;
     const bool two = a.a.c_split < a.a.Cg;
@@ -1168,6 +1172,12 @@ size_t igemm_slab_bytes(const IgemmArgs& a, int ksplit) {
 template <int BM, int BN, int WM, int WN, int BK>
 static hipError_t go_igemm(const IgemmArgs& a, hipStream_t s) {
   if (a.N % BN != 0 || a.K % BK != 0 || a.a.Cg % BK != 0 || a.a.c_split % BK != 0) return hipErrorInvalidValue;
+  if (a.batch > 1) {
+    if (a.ksplit > 1 || a.batch_rows < 1) return hipErrorInvalidValue;
+    dim3 grid((a.batch_rows + BM - 1) / BM, a.N / BN, a.batch);
+    hipLaunchKernelGGL((k_igemm<BM, BN, WM, WN, BK>), grid, dim3(WM * WN * 64), 0, s, a);
+    return hipGetLastError();
+  }
   dim3 grid((a.M + BM - 1) / BM, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
   hipLaunchKernelGGL((k_igemm<BM, BN, WM, WN, BK>), grid, dim3(WM * WN * 64), 0, s, a);
   return hipGetLastError();
@@ -1228,7 +1238,8 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 21: case 22: case 23: case 24: case 25: case 26:
     case 31: case 32: case 33: case 34: case 35: case 36:
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
-    case 61: case 62: case 63: case 64: case 65: case 66: return go_conv3_dma_tile(a, s, tile);
+    case 63: case 65: case 66: case 67: return go_conv3_dma_tile(a, s, tile);
+    case 70: return launch_wino(a, s);
     case 51: return go_halo32<8, 32, 64, 8, 1, 4>(a, s);
     case 52: return go_halo32<16, 16, 64, 8, 1, 4>(a, s);
     case 53: return go_halo32<8, 32, 64, 4, 1, 2>(a, s);
@@ -1284,7 +1295,7 @@ hipError_t launch_igemm_v(const IgemmArgs& a0, hipStream_t s, GemmChoice c) {
   if (!igemm_args_ok(a0) || !igemm_tile_fits(a0, c.tile)) return hipErrorInvalidValue;
   IgemmArgs a = a0;
   const int nk = a.K / tile_info(c.tile).bk;
-  int ks = c.split < 1 ? 1 : (c.split > nk ? nk : c.split);
+  int ks = c.split < 1 || c.tile == 70 ? 1 : (c.split > nk ? nk : c.split);
   if (ks > 1) {  // no empty slice: ks = ceil(nk / ceil(nk / ks))
     const int per = (nk + ks - 1) / ks;
     ks = (nk + per - 1) / per;

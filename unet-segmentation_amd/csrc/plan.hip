@@ -100,6 +100,7 @@ struct unet_plan {
   hipEvent_t ev_dy[18] = {}, ev_du[4] = {}, ev_join = nullptr;
   int bwd_full = 0;  // completed whole backward passes (the first one tunes, serially)
   Buf slab;          // split-K partial tiles (igemm sites the tuner splits)
+  Buf wino;          // Winograd F(2x2, 3x3) scratch (fp32 plans; U, M, V of one GEMM)
   Buf tune_scratch;  // atomic targets of the autotuner's trial launches
   size_t ws_bytes = 0;
   size_t fwd_ws_bytes = 0;  // prefix of the workspace a forward uses (no backward buffers)
@@ -218,9 +219,10 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
-                36, 41, 42, 43, 44, 61, 62, 63, 64, 65, 66}) {  // fits() filters by precision and gather
+                36, 41, 42, 43, 44, 63, 65, 66, 67, 70}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t)) continue;
     v.push_back({t, 1});
+    if (t == 70) continue;  // Winograd: no K split
     const long long cnt = igemm_tile_count(a, t);
     const long long slots = (long long)igemm_tile_slots(t) * cus;
     if (cnt >= 4 * slots || a.N % 64 != 0) continue;  // enough workgroup rounds already
@@ -348,6 +350,10 @@ GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
 
 hipError_t run_igemm(const Ctx& c, IgemmArgs a) {
   a.slab = c.f(c.p->slab);
+  if (c.p->wino.bytes) {  // fp32 plans: the Winograd candidate's scratch
+    a.wino_ws = c.f(c.p->wino);
+    a.wino_ws_bytes = c.p->wino.bytes;
+  }
   if (c.p->prec != UNET_PREC_FP32) {  // B -> its bf16 copy (and lo plane) at the same element offset
     const char* b = reinterpret_cast<const char*>(a.b);
     const char* base = c.ws + c.p->pack_region.off;
@@ -914,6 +920,21 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     }
     p->slab = al.take(std::min(mx, kSlabBudget));
     p->tune_scratch = al.take(wmax);
+    if (prec == UNET_PREC_FP32) {
+      // Winograd candidates: the 3x3 GEMMs with >= 128 input and output
+      // channels (forward: Cg = ci, N = co over the output grid; input
+      // gradient: Cg = co, N = ci over the input grid)
+      size_t wmx = 0;
+      for (int l = 1; l < 18; ++l) {
+        const Conv& L = p->L[l];
+        if (std::min(L.ci, L.co) < 128) continue;
+        const long long tf = (long long)n * ((L.ho + 1) / 2) * ((L.wo + 1) / 2);
+        const long long td = (long long)n * ((L.hi + 1) / 2) * ((L.wi + 1) / 2);
+        wmx = std::max(wmx, wino_ws_bytes(tf, L.ci, L.co));
+        wmx = std::max(wmx, wino_ws_bytes(td, L.co, L.ci));
+      }
+      p->wino = al.take(wmx);
+    }
   }
   {
     const size_t pack_start = al.top;

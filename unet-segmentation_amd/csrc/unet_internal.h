@@ -83,6 +83,17 @@ struct IgemmArgs {
   // slab[z][M][N] and k_splitk_epi sums them and runs the epilogue
   int ksplit = 1;
   float* slab = nullptr;
+  // Winograd F(2x2, 3x3) path (tile 70, winograd.hip): scratch for U, M, V and
+  // the variant of its 16 per-point GEMMs
+  float* wino_ws = nullptr;
+  size_t wino_ws_bytes = 0;
+  // batched dense GEMMs (register-staged k_igemm tiles only, no split-K):
+  // blockIdx.z = b runs rows b*batch_rows .. (b+1)*batch_rows of the gather
+  // (a 1 x (batch*batch_rows) grid), B offset by b*batch_b elements
+  int batch = 1;
+  int batch_rows = 0;
+  long long batch_b = 0;
+  struct { int tile = -1, split = 1; } wino_choice;
 };
 
 struct WgradArgs {
@@ -107,6 +118,10 @@ struct GemmChoice {
   int tile = -1;
   int split = 1;
 };
+// Winograd F(2x2, 3x3) fp32 path (winograd.hip), tile id 70
+size_t wino_ws_bytes(long long T, int Cg, int N);
+bool wino_applies(const IgemmArgs& a);
+hipError_t launch_wino(const IgemmArgs& a, hipStream_t s);
 // bf16 halo conv with LDS-DMA weights (conv3_dma.hip), tile ids 61-66
 bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch);
 hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);
