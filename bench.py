@@ -16,7 +16,9 @@ of scripts/train.py:108-131 (no per-step .item()).
 Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
 * roofline: the implicit-GEMM conv family (63 GEMM launch sites per step) at
   the MFMA peak of the precision, HIP-event timed on the plan's stream in an
-  extra untimed step; traffic from the committed rocprofv3 PMC passes of this
+  extra untimed step; `achieved` counts the MFMA flops the chosen variants
+  execute (the Winograd layers' point GEMMs), `direct_conv_tflops` the direct
+  convolution's flops over the same time; traffic from the committed rocprofv3 PMC passes of this
   command (profiles/pmc_traffic*.json, per GEMM launch site);
 * bottleneck / stage1: SURVEY.md §8d's two targets (MFMA on the 1024-channel
   set, HBM on the fused stage-1 kernels);
@@ -200,6 +202,7 @@ def run_precision(args, dtype, device, pg, world, rank):
     torch.cuda.synchronize()
     trainer.plan.set_timing(False)
     tim = trainer.plan.timing()
+    xfl = trainer.plan.mfma_flops()
     del trainer, model, x, t, w
     torch.cuda.empty_cache()
 
@@ -208,12 +211,17 @@ def run_precision(args, dtype, device, pg, world, rank):
     conv_ms = sum(c[0] for c in conv)
     conv_fl = sum(c[1] for c in conv)
     launches = sum(c[3] for c in conv)
-    achieved = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    conv_xfl = sum(xfl[k] for k in ("conv_fwd", "conv_dgrad", "conv_wgrad"))
+    # roofline: MFMA flops the GEMMs execute (Winograd layers run 2.25x / 4x fewer
+    # than the direct convolution); the direct-convolution rate beside it
+    achieved = conv_xfl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
+    direct = conv_fl / (conv_ms * 1e-3) / 1e12 if conv_ms > 0 else 0.0
     pmc = pmc_traffic(args, dtype)
     fam = pmc.get("families", {})
     st, bn = tim["stage1"], tim["bottleneck"]
     kernels = {k: {"ms": round(v[0], 3), "launches": v[3],
                    "tflops": round(v[1] / (v[0] * 1e-3) / 1e12, 2) if v[0] > 0 and v[1] else None,
+                   "mfma_tflops": round(xfl[k] / (v[0] * 1e-3) / 1e12, 2) if v[0] > 0 and xfl[k] else None,
                    "gbs": round(v[2] / (v[0] * 1e-3) / 1e9, 1) if v[0] > 0 and v[2] else None}
                for k, v in tim.items()}
     imgs = world * args.batch * args.steps
@@ -228,7 +236,12 @@ def run_precision(args, dtype, device, pg, world, rank):
                      "traffic_unit": "HBM bytes per GEMM launch site (rocprofv3 --pmc 2*FETCH_SIZE + WRITE_SIZE of "
                                      "this command's conv family incl. split-K epilogues, summed over one step / "
                                      f"{launches}; profiles/pmc_traffic{'' if dtype == 'fp32' else '_' + dtype}.json)",
-                     "flops_per_step": conv_fl, "launches_per_step": launches,
+                     "flops": "MFMA flops the chosen GEMM variants execute (Winograd F(2x2,3x3) / F(4x4,3x3) "
+                              "point GEMMs: 2 x points x tiles x Cin x Cout; else the direct 2 x M x N x K)",
+                     "mfma_flops_per_step": conv_xfl,
+                     "direct_conv_flops_per_step": conv_fl,
+                     "direct_conv_tflops": round(direct, 2),
+                     "launches_per_step": launches,
                      "avg_launch_ms": round(conv_ms / max(launches, 1), 4),
                      "timing": "HIP events on the plan's stream over one extra step after the timed steps, "
                                "weight-gradient side stream serialised; in the timed steps wgrad overlaps dgrad "
@@ -236,8 +249,9 @@ def run_precision(args, dtype, device, pg, world, rank):
         # SURVEY.md §8d target: >= 50 % MFMA on the 1024-channel bottleneck set
         "bottleneck": {"layers": "down4.c0, down4.c1, up1.convT, up1.c0 (fwd + dgrad + wgrad)",
                        "ms": round(bn[0], 3),
-                       "tflops": round(bn[1] / (bn[0] * 1e-3) / 1e12, 2) if bn[0] > 0 else None,
-                       "frac": round(bn[1] / (bn[0] * 1e-3) / 1e12 / peak, 4) if bn[0] > 0 else None},
+                       "tflops": round(xfl["bottleneck"] / (bn[0] * 1e-3) / 1e12, 2) if bn[0] > 0 else None,
+                       "frac": round(xfl["bottleneck"] / (bn[0] * 1e-3) / 1e12 / peak, 4) if bn[0] > 0 else None,
+                       "direct_conv_tflops": round(bn[1] / (bn[0] * 1e-3) / 1e12, 2) if bn[0] > 0 else None},
         # SURVEY.md §8d target: >= 40 % HBM on stage 1 (inc.c0 + BN0 stats fwd;
         # BN0 backward fused into inc.c0's weight gradient)
         "stage1": {"bound": "hbm", "ms": round(st[0], 3), "launches": st[3],

@@ -123,6 +123,11 @@ enum {
 };
 int unet_plan_set_timing(unet_plan* p, int enable);
 int unet_plan_timing(const unet_plan* p, double* ms, double* flops, double* bytes, int* launches);
+/* MFMA flops the chosen GEMM variants executed per class over the intervals the
+ * last unet_plan_timing() call reported: equal to its `flops` (the direct
+ * convolution's 2*M*N*K) except where a Winograd variant ran (igemm tiles
+ * 70/71, wgrad tile 71: 2 * points * tiles * Cin * Cout). */
+int unet_plan_timing_mfma_flops(const unet_plan* p, double* mfma_flops);
 
 /* ------------------------------------------------------------------------
  * Loss: WeightedCrossEntropyLoss (utils/losses.py:29-57) fused fwd+bwd.

@@ -934,7 +934,9 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int i0 = blockIdx.x * BM, j0 = blockIdx.y * BN;
-  const int pbeg = blockIdx.z * args.pix_per_split;
+  const int nz = gridDim.z / args.batch;  // pixel splits per batch entry
+  const int zb = blockIdx.z / nz;
+  const int pbeg = (blockIdx.z - zb * nz) * args.pix_per_split;
   const int pend = min(args.P, pbeg + args.pix_per_split);
   const Gather& ga = args.ga;
   const Gather& gb = args.gb;
@@ -943,6 +945,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
   const int acol4 = tid % AR, arow = tid / AR;
   const int ac = i0 + acol4 * 4;
   const Src& as = ga.s[0];
+  const float* const aptr = as.ptr + zb * args.batch_a;
   // B: fixed (tap, channel) per thread.
   const int bcol4 = tid % BR, brow = tid / BR;
   const int bj = j0 + bcol4 * 4;
@@ -952,6 +955,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
   const Src& bs = bsecond ? gb.s[1] : gb.s[0];
   const int bc = bsecond ? bc0 - gb.c_split : bc0;
   const int bty = btap / gb.taps_w, btx = btap - bty * gb.taps_w;
+  const float* const bptr = bs.ptr + zb * args.batch_b;
 
   float4 asc = make_float4(0, 0, 0, 0), ash = asc, bsc = asc, bsh = asc;
   if (as.scale) { asc = ld4(as.scale + ac); ash = ld4(as.shift + ac); }
@@ -971,7 +975,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
       const int p = p0 + arow + ASTEP * q;
       ain[q] = p < pend && (arow + ASTEP * q) < BK;
       const int pix = (ait[q].n * as.H + ait[q].y * ga.stride + as.oy) * as.W + ait[q].x * ga.stride + as.ox;
-      ra[q] = ld4(as.ptr + (size_t)pix * as.C + ac);
+      ra[q] = ld4(aptr + (size_t)pix * as.C + ac);
       if (p + BK < pend) ait[q].advance(BK, ga.Hg, ga.Wg);
     }
 #pragma unroll
@@ -980,7 +984,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
       bin[q] = p < pend && (brow + BSTEP * q) < BK;
       const int pix = (bit[q].n * bs.H + bit[q].y * gb.stride + bty + bs.oy) * bs.W + bit[q].x * gb.stride + btx +
                       bs.ox;
-      rb[q] = ld4(bs.ptr + (size_t)pix * bs.C + bc);
+      rb[q] = ld4(bptr + (size_t)pix * bs.C + bc);
       if (p + BK < pend) bit[q].advance(BK, gb.Hg, gb.Wg);
     }
   };
@@ -1045,7 +1049,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
       for (int r = 0; r < 16; ++r) {
         const int row = i0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = j0 + wn * TN * 32 + j * 32 + li;
-        atomicAdd(args.out + (size_t)row * args.No + col, acc[i][j][r]);
+        atomicAdd(args.out + zb * args.batch_out + (size_t)row * args.No + col, acc[i][j][r]);
       }
 }
 
@@ -1116,7 +1120,7 @@ static TileInfo tile_info(int id) {
     case 66: return {512, 64, 288, 1};
     case 67: return {256, 64, 144, 2};
     // Winograd F(2x2, 3x3) (winograd.hip): no K split
-    case 70: return {256, 64, 9, 2};
+    case 70: case 71: return {256, 64, 9, 2};
     // fp32 halo-tiled 3x3 (k_conv3_f32): bk = one 16-channel chunk x 9 taps
     case 51: return {256, 64, 144, 2};
     case 52: return {256, 64, 144, 2};
@@ -1140,7 +1144,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   if (is_halo_tile(tile))  // 3x3 stride-1 gathers only (conv fwd / dgrad), K = 9 x Cg
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
-  if (tile == 70) return wino_applies(a);
+  if (tile == 70 || tile == 71) return wino_applies(a, tile == 70 ? 2 : 4);
   if (is_dma_tile(tile)) {  // bf16-stored A sources, no split operands
     const int ch = tile_info(tile).bk / 9;
     const bool two = a.a.c_split < a.a.Cg;
@@ -1239,7 +1243,8 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 31: case 32: case 33: case 34: case 35: case 36:
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
     case 63: case 65: case 66: case 67: return go_conv3_dma_tile(a, s, tile);
-    case 70: return launch_wino(a, s);
+    case 70: return launch_wino(a, s, 2);
+    case 71: return launch_wino(a, s, 4);
     case 51: return go_halo32<8, 32, 64, 8, 1, 4>(a, s);
     case 52: return go_halo32<16, 16, 64, 8, 1, 4>(a, s);
     case 53: return go_halo32<8, 32, 64, 4, 1, 2>(a, s);
@@ -1295,7 +1300,7 @@ hipError_t launch_igemm_v(const IgemmArgs& a0, hipStream_t s, GemmChoice c) {
   if (!igemm_args_ok(a0) || !igemm_tile_fits(a0, c.tile)) return hipErrorInvalidValue;
   IgemmArgs a = a0;
   const int nk = a.K / tile_info(c.tile).bk;
-  int ks = c.split < 1 || c.tile == 70 ? 1 : (c.split > nk ? nk : c.split);
+  int ks = c.split < 1 || c.tile == 70 || c.tile == 71 ? 1 : (c.split > nk ? nk : c.split);
   if (ks > 1) {  // no empty slice: ks = ceil(nk / ceil(nk / ks))
     const int per = (nk + ks - 1) / ks;
     ks = (nk + per - 1) / per;
@@ -1318,6 +1323,8 @@ static void wgrad_tile(int id, int& bm, int& bn) {
   if (id >= 10 && id < 15) { bm = tb[id - 10][0]; bn = tb[id - 10][1]; }
 }
 bool wgrad_tile_fits(const WgradArgs& a, int tile) {
+  if (tile == 71) return wino_wgrad_applies(a);
+  if (a.batch > 1 && (tile < 0 || tile > 4)) return false;  // batched: fp32 pixel-column tiles only
   if (tile == 20 || tile == 21) return wgrad3_fits(a);  // halo-tiled 3x3, all taps
   if (tile == 22 || tile == 23) return wgrad3_f32_fits(a);  // fp32 twin
   int bm, bn;
@@ -1337,7 +1344,7 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     else if (a.No % 128 == 0) tile = 12;
     else tile = 13;
   } else if (tile < 0) {
-    if ((g_tune_wgrad == 22 || g_tune_wgrad == 23) && wgrad_tile_fits(a, g_tune_wgrad))
+    if ((g_tune_wgrad == 22 || g_tune_wgrad == 23 || g_tune_wgrad == 71) && wgrad_tile_fits(a, g_tune_wgrad))
       tile = g_tune_wgrad;  // forced fp32 halo tile (tests)
     else if (g_tune_wgrad == 1) tile = 4;  // force the small tile (A/B tests)
     else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 0;
@@ -1347,12 +1354,13 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     else tile = 4;
   }
   if (!wgrad_tile_fits(a, tile)) return hipErrorInvalidValue;
+  if (tile == 71) return launch_wino_wgrad(a, s, c.split > 0 ? c.split : 8);
   if (tile == 20 || tile == 21) return go_wgrad3_bf16(a, s, tile, c.split > 0 ? c.split : 4);
   if (tile == 22) return go_wgrad3_f32<8, 16>(a, s, c.split > 0 ? c.split : 4);
   if (tile == 23) return go_wgrad3_f32<4, 32>(a, s, c.split > 0 ? c.split : 4);
   int bm, bn;
   wgrad_tile(tile, bm, bn);
-  const int tiles = (a.Mo / bm) * (a.No / bn);
+  const int tiles = (a.Mo / bm) * (a.No / bn) * a.batch;
   // split the pixel reduction so that the grid has ~`per_cu` workgroups per CU
   const int per_cu = c.tile >= 0 ? (c.split > 0 ? c.split : 8) : (g_tune_wgrad >= 2 ? g_tune_wgrad : 8);
   const int target = per_cu * num_cus();
@@ -1365,7 +1373,7 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   pps = (pps + kq - 1) / kq * kq;
   splits = (a.P + pps - 1) / pps;
   a.pix_per_split = pps;
-  dim3 grid(a.Mo / bm, a.No / bn, splits);
+  dim3 grid(a.Mo / bm, a.No / bn, splits * a.batch);
   if (tile >= 10) return go_wgrad_bf16(a, s, tile, grid);
   switch (tile) {
     case 0: hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
@@ -1378,5 +1386,26 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
 }
 
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad_v(a, s, GemmChoice{}); }
+
+double igemm_exec_flops(const IgemmArgs& a, GemmChoice c) {
+  int t = c.tile;
+  if (t < 0 && (g_tune_igemm == 70 || g_tune_igemm == 71) && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;
+  if (t == 70 || t == 71) {
+    const int mt = t == 70 ? 2 : 4;
+    const Gather& g = a.a;
+    const double T = (double)g.nimg * ((g.Hg + mt - 1) / mt) * ((g.Wg + mt - 1) / mt);
+    return 2.0 * (mt + 2) * (mt + 2) * T * g.Cg * a.N;
+  }
+  return 2.0 * a.M * (double)a.N * a.K;
+}
+
+double wgrad_exec_flops(const WgradArgs& a, GemmChoice c) {
+  const bool wino = c.tile == 71 || (c.tile < 0 && !a.bf16 && g_tune_wgrad == 71 && wino_wgrad_applies(a));
+  if (wino) {
+    const double T = (double)a.gb.nimg * ((a.gb.Hg + 3) / 4) * ((a.gb.Wg + 3) / 4);
+    return 2.0 * 36 * T * a.Mo * a.gb.Cg;
+  }
+  return 2.0 * a.P * (double)a.Mo * a.No;
+}
 
 }  // namespace unet

@@ -100,7 +100,8 @@ struct unet_plan {
   hipEvent_t ev_dy[18] = {}, ev_du[4] = {}, ev_join = nullptr;
   int bwd_full = 0;  // completed whole backward passes (the first one tunes, serially)
   Buf slab;          // split-K partial tiles (igemm sites the tuner splits)
-  Buf wino;          // Winograd F(2x2, 3x3) scratch (fp32 plans; U, M, V of one GEMM)
+  Buf wino;          // Winograd F(2x2, 3x3) / F(4x4, 3x3) scratch (fp32 plans; U, M, V of one GEMM)
+  Buf wino_w;        // the weight-gradient twin (U, Vd, Mw; backward part of the workspace)
   Buf tune_scratch;  // atomic targets of the autotuner's trial launches
   size_t ws_bytes = 0;
   size_t fwd_ws_bytes = 0;  // prefix of the workspace a forward uses (no backward buffers)
@@ -109,10 +110,14 @@ struct unet_plan {
   struct Ev {
     hipEvent_t a, b;
     int cls;
-    double flops, bytes;
+    double flops, bytes, xflops;
   };
   std::vector<Ev> evs;
+  // MFMA flops the chosen GEMM variants execute (Winograd: its point GEMMs),
+  // summed on the host as launches are enqueued; Timer intervals take deltas
+  double xfl = 0;
   double t_ms[UNET_KC_COUNT] = {0}, t_fl[UNET_KC_COUNT] = {0}, t_by[UNET_KC_COUNT] = {0};
+  double t_xf[UNET_KC_COUNT] = {0}, t_xf_last[UNET_KC_COUNT] = {0};
   int t_n[UNET_KC_COUNT] = {0};
 };
 
@@ -153,9 +158,9 @@ struct Timer {
   hipEvent_t a{}, b{};
   bool ok = false;
   int cls;
-  double fl, by;
+  double fl, by, x0;
   Timer(unet_plan* p_, hipStream_t s_, int c, double f, double by_, bool on = true)
-      : p(p_), s(s_), cls(c), fl(f), by(by_) {
+      : p(p_), s(s_), cls(c), fl(f), by(by_), x0(p_->xfl) {
     // timing is best effort (bench / tools only): a failed event leaves the
     // interval out of the report instead of failing the plan call
     if (p->timing && on) {
@@ -170,7 +175,7 @@ struct Timer {
   ~Timer() {
     if (p->timing && ok) {
       if (hipEventRecord(b, s) == hipSuccess) {
-        p->evs.push_back({a, b, cls, fl, by});
+        p->evs.push_back({a, b, cls, fl, by, p->xfl - x0});
       } else {
         (void)hipEventDestroy(a);
         (void)hipEventDestroy(b);
@@ -219,10 +224,10 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
-                36, 41, 42, 43, 44, 63, 65, 66, 67, 70}) {  // fits() filters by precision and gather
+                36, 41, 42, 43, 44, 63, 65, 66, 67, 70, 71}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t)) continue;
     v.push_back({t, 1});
-    if (t == 70) continue;  // Winograd: no K split
+    if (t == 70 || t == 71) continue;  // Winograd: no K split
     const long long cnt = igemm_tile_count(a, t);
     const long long slots = (long long)igemm_tile_slots(t) * cus;
     if (cnt >= 4 * slots || a.N % 64 != 0) continue;  // enough workgroup rounds already
@@ -236,7 +241,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
 
 std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   std::vector<GemmChoice> v;
-  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23}) {  // fits() filters by precision
+  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 71}) {  // fits() filters by precision
     if (!wgrad_tile_fits(a, t)) continue;
     if (t >= 20) {  // halo-tiled: workgroups per CU (2 resident)
       for (int per_cu : {2, 4, 8}) v.push_back({t, per_cu});
@@ -364,13 +369,21 @@ hipError_t run_igemm(const Ctx& c, IgemmArgs a) {
     if (c.p->prec == UNET_PREC_BF16X3) a.bl = hi + c.p->pack_region.bytes / 4 + el;
     a.b = nullptr;
   }
-  return launch_igemm_v(a, c.s, choose_igemm(c, a));
+  const GemmChoice ch = choose_igemm(c, a);
+  if (c.p->timing) c.p->xfl += igemm_exec_flops(a, ch);
+  return launch_igemm_v(a, c.s, ch);
 }
 
 hipError_t run_wgrad(const Ctx& c, WgradArgs a) {
   a.bf16 = c.p->prec != UNET_PREC_FP32;
   a.split = c.p->prec == UNET_PREC_BF16X3;
-  return launch_wgrad_v(a, c.s, choose_wgrad(c, a));
+  if (c.p->wino_w.bytes) {  // fp32 training plans: the Winograd weight-gradient scratch (side stream)
+    a.wino_ws = c.f(c.p->wino_w);
+    a.wino_ws_bytes = c.p->wino_w.bytes;
+  }
+  const GemmChoice ch = choose_wgrad(c, a);
+  if (c.p->timing) c.p->xfl += wgrad_exec_flops(a, ch);
+  return launch_wgrad_v(a, c.s, ch);
 }
 
 Src src_of(const Ctx& c, const Conv& L, bool transform) {
@@ -921,17 +934,14 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     p->slab = al.take(std::min(mx, kSlabBudget));
     p->tune_scratch = al.take(wmax);
     if (prec == UNET_PREC_FP32) {
-      // Winograd candidates: the 3x3 GEMMs with >= 128 input and output
-      // channels (forward: Cg = ci, N = co over the output grid; input
-      // gradient: Cg = co, N = ci over the input grid)
+      // Winograd candidates: every 3x3 GEMM after inc.c0 (forward: Cg = ci,
+      // N = co over the output grid; input gradient: Cg = co, N = ci over the
+      // input grid); the autotuner decides per shape
       size_t wmx = 0;
       for (int l = 1; l < 18; ++l) {
         const Conv& L = p->L[l];
-        if (std::min(L.ci, L.co) < 128) continue;
-        const long long tf = (long long)n * ((L.ho + 1) / 2) * ((L.wo + 1) / 2);
-        const long long td = (long long)n * ((L.hi + 1) / 2) * ((L.wi + 1) / 2);
-        wmx = std::max(wmx, wino_ws_bytes(tf, L.ci, L.co));
-        wmx = std::max(wmx, wino_ws_bytes(td, L.co, L.ci));
+        wmx = std::max(wmx, wino_ws_bytes_grid(n, L.ho, L.wo, L.ci, L.co));
+        wmx = std::max(wmx, wino_ws_bytes_grid(n, L.hi, L.wi, L.co, L.ci));
       }
       p->wino = al.take(wmx);
     }
@@ -994,6 +1004,16 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
   for (int k = 0; k < 4; ++k) {
     Pool& pl = p->P[k];
     pl.dp = al.take(fsz((long long)n * (pl.h / 2) * (pl.w / 2) * pl.c));
+  }
+  if (prec == UNET_PREC_FP32) {
+    // Winograd weight-gradient candidate (wgrad tile 71): its own scratch, as the
+    // weight gradients run on the side stream next to the dgrad GEMMs
+    size_t wmx = 0;
+    for (int l = 1; l < 18; ++l) {
+      const Conv& L = p->L[l];
+      wmx = std::max(wmx, wino_ws_bytes_grid(n, L.ho, L.wo, L.ci, L.co));
+    }
+    p->wino_w = al.take(wmx);
   }
   p->ws_bytes = al.top;
   return p;
@@ -1101,6 +1121,7 @@ int unet_plan_timing(const unet_plan* pc, double* ms, double* fl, double* by, in
       p->t_ms[e.cls] += t;
       p->t_fl[e.cls] += e.flops;
       p->t_by[e.cls] += e.bytes;
+      p->t_xf[e.cls] += e.xflops;
       p->t_n[e.cls] += 1;
     }
     (void)hipEventDestroy(e.a);
@@ -1112,10 +1133,17 @@ int unet_plan_timing(const unet_plan* pc, double* ms, double* fl, double* by, in
     if (fl) fl[i] = p->t_fl[i];
     if (by) by[i] = p->t_by[i];
     if (cnt) cnt[i] = p->t_n[i];
-    p->t_ms[i] = p->t_fl[i] = p->t_by[i] = 0;
+    p->t_xf_last[i] = p->t_xf[i];
+    p->t_ms[i] = p->t_fl[i] = p->t_by[i] = p->t_xf[i] = 0;
     p->t_n[i] = 0;
   }
   return rc;
+}
+
+int unet_plan_timing_mfma_flops(const unet_plan* p, double* xfl) {
+  if (!p || !xfl) return -EINVAL;
+  for (int i = 0; i < UNET_KC_COUNT; ++i) xfl[i] = p->t_xf_last[i];
+  return 0;
 }
 
 }  // extern "C"

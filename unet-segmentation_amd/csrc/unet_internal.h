@@ -106,6 +106,13 @@ struct WgradArgs {
   float* out;        // [Mo][No] fp32, accumulated with atomics (zeroed by caller)
   int bf16 = 0;      // 1: operands rounded to bf16 when staged (bf16 tiles 10-14)
   int split = 0;     // 1 (with bf16): operands as hi/lo bf16 pairs (UNET_PREC_BF16X3)
+  // batched (fp32 tiles 0-4): blockIdx.z = b * splits + split; operand b's
+  // pointers offset by b * batch_a / batch_b elements, its output by b * batch_out
+  int batch = 1;
+  long long batch_a = 0, batch_b = 0, batch_out = 0;
+  // Winograd F(4x4, 3x3) weight gradient (wgrad tile 71, winograd.hip): scratch
+  float* wino_ws = nullptr;
+  size_t wino_ws_bytes = 0;
 };
 
 // ---------------- launchers (kernels.hip) ----------------
@@ -120,8 +127,15 @@ struct GemmChoice {
 };
 // Winograd F(2x2, 3x3) fp32 path (winograd.hip), tile id 70
 size_t wino_ws_bytes(long long T, int Cg, int N);
-bool wino_applies(const IgemmArgs& a);
-hipError_t launch_wino(const IgemmArgs& a, hipStream_t s);
+size_t wino_ws_bytes_grid(int nimg, int H, int W, int Cg, int N);
+bool wino_applies(const IgemmArgs& a, int mt);           // mt = 2: F(2x2, 3x3), 4: F(4x4, 3x3)
+hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt);
+bool wino_wgrad_applies(const WgradArgs& a);
+// MFMA flops a GEMM launch executes with variant c (Winograd: 2 * points *
+// tiles * Cg * N; otherwise the direct 2 * M * N * K)
+double igemm_exec_flops(const IgemmArgs& a, GemmChoice c);
+double wgrad_exec_flops(const WgradArgs& a, GemmChoice c);
+hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu);
 // bf16 halo conv with LDS-DMA weights (conv3_dma.hip), tile ids 61-66
 bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch);
 hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);

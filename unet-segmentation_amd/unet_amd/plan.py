@@ -70,3 +70,12 @@ class Plan:
         _lib.check(self.lib.unet_plan_timing(self.handle, ms, fl, by, cnt), "unet_plan_timing")
         names = ["conv_fwd", "conv_dgrad", "conv_wgrad", "stage1", "elementwise", "bottleneck"]
         return {names[i]: (ms[i], fl[i], by[i], cnt[i]) for i in range(n)}
+
+    def mfma_flops(self):
+        """{class: MFMA flops executed} over the intervals of the last timing()
+        call (Winograd variants execute fewer than the direct-conv flops)."""
+        n = 6
+        xf = (ctypes.c_double * n)()
+        _lib.check(self.lib.unet_plan_timing_mfma_flops(self.handle, xf), "unet_plan_timing_mfma_flops")
+        names = ["conv_fwd", "conv_dgrad", "conv_wgrad", "stage1", "elementwise", "bottleneck"]
+        return {names[i]: xf[i] for i in range(n)}
