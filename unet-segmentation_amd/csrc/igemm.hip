@@ -1121,6 +1121,7 @@ static TileInfo tile_info(int id) {
     case 67: return {256, 64, 144, 2};
     // Winograd F(2x2, 3x3) (winograd.hip): no K split
     case 70: case 71: return {256, 64, 9, 2};
+    case 72: return {32, 32, 16, 1};
     // fp32 halo-tiled 3x3 (k_conv3_f32): bk = one 16-channel chunk x 9 taps
     case 51: return {256, 64, 144, 2};
     case 52: return {256, 64, 144, 2};
@@ -1145,6 +1146,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
   if (tile == 70 || tile == 71) return wino_applies(a, tile == 70 ? 2 : 4);
+  if (tile == 72) return wino_fused_applies(a);
   if (is_dma_tile(tile)) {  // bf16-stored A sources, no split operands
     const int ch = tile_info(tile).bk / 9;
     const bool two = a.a.c_split < a.a.Cg;
@@ -1245,6 +1247,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 63: case 65: case 66: case 67: return go_conv3_dma_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);
     case 71: return launch_wino(a, s, 4);
+    case 72: return launch_wino_fused(a, s);
     case 51: return go_halo32<8, 32, 64, 8, 1, 4>(a, s);
     case 52: return go_halo32<16, 16, 64, 8, 1, 4>(a, s);
     case 53: return go_halo32<8, 32, 64, 4, 1, 2>(a, s);
@@ -1300,7 +1303,7 @@ hipError_t launch_igemm_v(const IgemmArgs& a0, hipStream_t s, GemmChoice c) {
   if (!igemm_args_ok(a0) || !igemm_tile_fits(a0, c.tile)) return hipErrorInvalidValue;
   IgemmArgs a = a0;
   const int nk = a.K / tile_info(c.tile).bk;
-  int ks = c.split < 1 || c.tile == 70 || c.tile == 71 ? 1 : (c.split > nk ? nk : c.split);
+  int ks = c.split < 1 || (c.tile >= 70 && c.tile <= 72) ? 1 : (c.split > nk ? nk : c.split);
   if (ks > 1) {  // no empty slice: ks = ceil(nk / ceil(nk / ks))
     const int per = (nk + ks - 1) / ks;
     ks = (nk + per - 1) / per;
@@ -1389,8 +1392,8 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad
 
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c) {
   int t = c.tile;
-  if (t < 0 && (g_tune_igemm == 70 || g_tune_igemm == 71) && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;
-  if (t == 70 || t == 71) {
+  if (t < 0 && g_tune_igemm >= 70 && g_tune_igemm <= 72 && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;
+  if (t >= 70 && t <= 72) {
     const int mt = t == 70 ? 2 : 4;
     const Gather& g = a.a;
     const double T = (double)g.nimg * ((g.Hg + mt - 1) / mt) * ((g.Wg + mt - 1) / mt);

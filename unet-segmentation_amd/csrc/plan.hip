@@ -224,10 +224,10 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
-                36, 41, 42, 43, 44, 63, 65, 66, 67, 70, 71}) {  // fits() filters by precision and gather
+                36, 41, 42, 43, 44, 63, 65, 66, 67, 70, 71, 72}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t)) continue;
     v.push_back({t, 1});
-    if (t == 70 || t == 71) continue;  // Winograd: no K split
+    if (t >= 70 && t <= 72) continue;  // Winograd: no K split
     const long long cnt = igemm_tile_count(a, t);
     const long long slots = (long long)igemm_tile_slots(t) * cus;
     if (cnt >= 4 * slots || a.N % 64 != 0) continue;  // enough workgroup rounds already
@@ -313,15 +313,20 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
   GemmChoice best{};
   float tb = th;
   std::string log = key + " | heuristic " + std::to_string(th * 1e3f) + " us";
+  static const bool verbose = getenv("UNET_TUNE_VERBOSE") != nullptr;
+  std::string all;
   for (const GemmChoice& g : igemm_candidates(a, c.p->slab.bytes)) {
     const float tm = time_launch(c.s, [&] { return launch_igemm_v(t, c.s, g); });
+    if (verbose)
+      all += " " + std::to_string(g.tile) + (g.split > 1 ? "s" + std::to_string(g.split) : "") + ":" +
+             std::to_string((int)(tm * 1e3f));
     if (tm > 0.f && (tb < 0.f || tm < tb)) {
       tb = tm;
       best = g;
     }
   }
   log += " | best tile " + std::to_string(best.tile) + " split " + std::to_string(best.split) + " " +
-         std::to_string(tb * 1e3f) + " us";
+         std::to_string(tb * 1e3f) + " us" + (verbose ? " |" + all : "");
   g_tuned[key] = best;
   g_tune_log[key] = log;
   return best;
@@ -339,15 +344,18 @@ GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
   GemmChoice best{};
   float tb = th;
   std::string log = key + " | heuristic " + std::to_string(th * 1e3f) + " us";
+  static const bool verbose = getenv("UNET_TUNE_VERBOSE") != nullptr;
+  std::string all;
   for (const GemmChoice& g : wgrad_candidates(a)) {
     const float tm = time_launch(c.s, [&] { return launch_wgrad_v(t, c.s, g); });
+    if (verbose) all += " " + std::to_string(g.tile) + "/" + std::to_string(g.split) + ":" + std::to_string((int)(tm * 1e3f));
     if (tm > 0.f && (tb < 0.f || tm < tb)) {
       tb = tm;
       best = g;
     }
   }
   log += " | best tile " + std::to_string(best.tile) + " per_cu " + std::to_string(best.split) + " " +
-         std::to_string(tb * 1e3f) + " us";
+         std::to_string(tb * 1e3f) + " us" + (verbose ? " |" + all : "");
   g_tuned[key] = best;
   g_tune_log[key] = log;
   return best;

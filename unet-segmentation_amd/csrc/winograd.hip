@@ -80,12 +80,10 @@ __global__ __launch_bounds__(256) void k_wino_in(Gather g, int Th, int Tw, long 
 #pragma unroll
     for (int xx = 0; xx < 4; ++xx) {
       const int y = 2 * ty + yy, x = 2 * tx + xx;
-      float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (y < g.Hg + 2 && x < g.Wg + 2) {
-        v = ld4(s.ptr + ((size_t)(n * s.H + y + s.oy) * s.W + x + s.ox) * s.C + cl);
-        if (s.scale) v = affine_relu4(v, sc, sh);
-      }
-      d[yy][xx] = v;
+      const bool in = y < g.Hg + 2 && x < g.Wg + 2;  // unconditional load, clamped address
+      float4 v = ld4(s.ptr + ((size_t)(n * s.H + (in ? y : 0) + s.oy) * s.W + (in ? x : 0) + s.ox) * s.C + cl);
+      if (s.scale) v = affine_relu4(v, sc, sh);
+      d[yy][xx] = in ? v : make_float4(0.f, 0.f, 0.f, 0.f);
     }
   // B^T d (rows), then (.) B (columns)
   float4 e[4][4];
@@ -287,12 +285,10 @@ __global__ __launch_bounds__(256) void k_wino4_in(Gather g, int Th, int Tw, long
 #pragma unroll
     for (int yy = 0; yy < 6; ++yy) {
       const int y = 4 * ty + yy, x = 4 * tx + xx;
-      float v = 0.f;
-      if (y < g.Hg + 2 && x < g.Wg + 2) {
-        v = s.ptr[((size_t)(n * s.H + y + s.oy) * s.W + x + s.ox) * s.C + cl];
-        if (s.scale) v = fmaxf(fmaf(v, sc, sh), 0.f);
-      }
-      d[yy] = v;
+      const bool in = y < g.Hg + 2 && x < g.Wg + 2;  // unconditional load, clamped address
+      float v = s.ptr[((size_t)(n * s.H + (in ? y : 0) + s.oy) * s.W + (in ? x : 0) + s.ox) * s.C + cl];
+      if (s.scale) v = fmaxf(fmaf(v, sc, sh), 0.f);
+      d[yy] = in ? v : 0.f;
     }
     float rr[6];
     bt6(d, rr);
@@ -493,6 +489,329 @@ hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt) {
 }
 
 // ---------------------------------------------------------------------------
+// Fused F(4x4, 3x3) (tile 72): one kernel per GEMM, no U / M in HBM.
+// A workgroup (8 waves) owns 32 output tiles (4x4 pixels each, linear tile
+// order) x 32 output channels and loops over the input channels in chunks of 16:
+//   * thread (tile = tid / 16, channel = tid % 16) loads its 6x6 input patch
+//     into registers (prefetched one chunk ahead), applies the producer's
+//     BatchNorm + ReLU, computes B^T d B and writes the 36 points to LDS
+//     U[p][tile][16];
+//   * the pre-transformed weights V (k_wino4f_w, layout [Cg/16][36][N][16]) are
+//     staged the same way into V[p][n][16];
+//   * wave w multiplies the 16-tile half w & 1 for points 9 (w >> 1) .. +8 and
+//     both 16-channel halves with v_mfma_f32_16x16x4_f32: per point one
+//     ds_read_b128 of U, two of V, eight MFMAs (lane quarter q takes channels
+//     4q .. 4q+3 as its k: any order works as long as A and B agree);
+//   * the 36 accumulators of every (tile, channel) leave through LDS
+//     ([36][32][32], reusing the staging space) and each thread applies
+//     A^T M A and the epilogue of k_wino4_out to the 16 pixels of two pairs.
+// LDS rows are 16 floats (64 B) with 16-B piece q stored at q ^ (2 * ((row >> 3)
+// & 1)): the ds_read_b128 lane groups then hit 64 distinct banks.  147 KB of
+// LDS, one workgroup (2 waves per SIMD) per CU.
+// ---------------------------------------------------------------------------
+template <int CK>
+__global__ void k_wino4f_w(const float* __restrict__ b, int N, int Cg, float* __restrict__ v) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)N * Cg) return;
+  const int n = (int)(i / Cg), c = (int)(i - (long long)n * Cg);
+  float tg[6][3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float col[3] = {b[((size_t)n * 9 + 0 + k) * Cg + c], b[((size_t)n * 9 + 3 + k) * Cg + c],
+                    b[((size_t)n * 9 + 6 + k) * Cg + c]};
+    float r[6];
+    g6(col, r);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) tg[a][k] = r[a];
+  }
+  const size_t base = (size_t)(c / CK) * 36 * N;
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    float r[6];
+    g6(tg[a], r);
+#pragma unroll
+    for (int bb = 0; bb < 6; ++bb) v[(base + (size_t)(a * 6 + bb) * N + n) * CK + (c % CK)] = r[bb];
+  }
+}
+
+// float offset of 16-B piece q of LDS row `row` (16 floats per row)
+__device__ __forceinline__ int wf_off(int row, int q) { return row * 16 + ((q ^ (((row >> 3) & 1) << 1)) << 2); }
+
+typedef float floatx4 __attribute__((ext_vector_type(4)));
+
+__global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __restrict__ V, int N, long long T,
+                                                   int Th, int Tw, int NB, Epilogue e) {
+  constexpr int PS = 32 * 16;  // floats per point plane of U / V
+  __shared__ __attribute__((aligned(16))) float lds[2 * 36 * PS];
+  float* Us = lds;
+  float* Vs = lds + 36 * PS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  long long bid = blockIdx.x;
+  const long long G = gridDim.x;
+  if ((G & 7) == 0) bid = (bid & 7) * (G >> 3) + (bid >> 3);  // an XCD's workgroups share tiles
+  const int nb = (int)(bid % NB);
+  const long long t0 = (bid / NB) * 32;
+  const int n0 = nb * 32;
+
+  // ---- loader role: (tile lt, channel lc of the chunk) ----
+  const int lt = tid >> 4, lc = tid & 15;
+  const long long t = t0 + lt;
+  int img = 0, ty = 0, tx = 0;
+  if (t < T) {
+    tx = (int)(t % Tw);
+    const long long r = t / Tw;
+    ty = (int)(r % Th);
+    img = (int)(r / Th);
+  }
+  // patch rows / columns inside the (Hg+2) x (Wg+2) input window (all of them
+  // except in the last tile row / column)
+  const int vrows = t < T ? min(6, g.Hg + 2 - 4 * ty) : 0;
+  const int vcols = t < T ? min(6, g.Wg + 2 - 4 * tx) : 0;
+  const bool full = vrows == 6 && vcols == 6;
+  const int uoff = wf_off(lt, lc >> 2) + (lc & 3);
+  float raw[36];
+  float4 vr[9];
+  const int nk = g.Cg >> 4;
+  auto load = [&](int kc) {
+    // chunks never straddle the concat split (c_split % 16 == 0): uniform source
+    const bool second = kc * 16 >= g.c_split;
+    const float* sp = second ? g.s[1].ptr : g.s[0].ptr;
+    const int sH = second ? g.s[1].H : g.s[0].H, sW = second ? g.s[1].W : g.s[0].W;
+    const int sC = second ? g.s[1].C : g.s[0].C;
+    const int soy = second ? g.s[1].oy : g.s[0].oy, sox = second ? g.s[1].ox : g.s[0].ox;
+    const int cl = kc * 16 - (second ? g.c_split : 0) + lc;
+    // unsigned 32-bit byte offsets from a uniform base (sources are below 4 GB,
+    // wino_fused_applies): one v_add per load, SGPR-base addressing
+    const char* sb = reinterpret_cast<const char*>(sp);
+    const unsigned o0 = ((unsigned)((img * sH + 4 * ty + soy) * sW + 4 * tx + sox) * sC + cl) * 4u;
+    const unsigned rs = (unsigned)sW * sC * 4u, cs = (unsigned)sC * 4u;
+    if (full) {
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 6; ++xx)
+          raw[yy * 6 + xx] = *reinterpret_cast<const float*>(sb + (o0 + (yy * rs + xx * cs)));
+    } else {
+      // edge tiles: positions outside the window read the patch origin (always
+      // in bounds) and are zeroed in commit
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 6; ++xx)
+          raw[yy * 6 + xx] =
+              *reinterpret_cast<const float*>(sb + (o0 + (yy < vrows && xx < vcols ? yy * rs + xx * cs : 0u)));
+    }
+    const char* vb = reinterpret_cast<const char*>(V + ((size_t)kc * 36 * N + n0) * 16);
+    const unsigned vo = ((unsigned)(tid >> 7) * N * 16u + ((tid >> 2) & 31) * 16u + (tid & 3) * 4u) * 4u;
+    const unsigned vstep = 4u * N * 16u * 4u;  // 4 points per 512 float4
+#pragma unroll
+    for (int j = 0; j < 9; ++j) vr[j] = *reinterpret_cast<const float4*>(vb + (vo + j * vstep));
+  };
+  auto commit = [&](int kc) {
+    const bool second = kc * 16 >= g.c_split;
+    const float* scp = second ? g.s[1].scale : g.s[0].scale;
+    const float* shp = second ? g.s[1].shift : g.s[0].shift;
+    const int cl = kc * 16 - (second ? g.c_split : 0) + lc;
+    if (scp) {
+      const float sc = scp[cl], sh = shp[cl];
+#pragma unroll
+      for (int q = 0; q < 36; ++q) raw[q] = fmaxf(fmaf(raw[q], sc, sh), 0.f);
+    }
+    if (!full) {
+#pragma unroll
+      for (int q = 0; q < 36; ++q) raw[q] = (q / 6 < vrows && q % 6 < vcols) ? raw[q] : 0.f;
+    }
+#pragma unroll
+    for (int xx = 0; xx < 6; ++xx) {  // columns in place: raw[a][xx] = (B^T d)[a][xx]
+      float d[6];
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy) d[yy] = raw[yy * 6 + xx];
+      float rr[6];
+      bt6(d, rr);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) raw[a * 6 + xx] = rr[a];
+    }
+#pragma unroll
+    for (int a = 0; a < 6; ++a) {
+      float d[6];
+#pragma unroll
+      for (int xx = 0; xx < 6; ++xx) d[xx] = raw[a * 6 + xx];
+      float rr[6];
+      bt6(d, rr);
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) Us[(a * 6 + bb) * PS + uoff] = rr[bb];
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int q = tid + 512 * j;
+      const int p = q >> 7, n = (q >> 2) & 31, piece = q & 3;
+      st4(Vs + p * PS + wf_off(n, piece), vr[j]);
+    }
+  };
+
+  // ---- MFMA role: tile half th, points 9 pg .. 9 pg + 8, both channel halves ----
+  const int th = wave & 1, pg = wave >> 1;
+  const int mi = lane & 15, mq = lane >> 4;
+  const int aoff = wf_off(16 * th + mi, mq);
+  const int boff0 = wf_off(mi, mq), boff1 = wf_off(16 + mi, mq);
+  floatx4 acc[9][2];
+#pragma unroll
+  for (int j = 0; j < 9; ++j)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) acc[j][hh] = (floatx4){0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int kc = 0; kc < nk; ++kc) {
+    commit(kc);
+    __syncthreads();
+    if (kc + 1 < nk) load(kc + 1);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int p = pg * 9 + j;
+      const float4 a = ld4(Us + p * PS + aoff);
+      const float4 b0 = ld4(Vs + p * PS + boff0);
+      const float4 b1 = ld4(Vs + p * PS + boff1);
+      acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b0.x, acc[j][0], 0, 0, 0);
+      acc[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b1.x, acc[j][1], 0, 0, 0);
+      acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b0.y, acc[j][0], 0, 0, 0);
+      acc[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b1.y, acc[j][1], 0, 0, 0);
+      acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b0.z, acc[j][0], 0, 0, 0);
+      acc[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b1.z, acc[j][1], 0, 0, 0);
+      acc[j][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b0.w, acc[j][0], 0, 0, 0);
+      acc[j][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b1.w, acc[j][1], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // ---- accumulators -> LDS X[36][32 tiles][32 channels] ----
+  // 16x16 accumulator: lane l holds column l & 15, rows 4 (l >> 4) + r
+  float* X = lds;
+#pragma unroll
+  for (int j = 0; j < 9; ++j)
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh)
+#pragma unroll
+      for (int r = 0; r < 4; ++r)
+        X[(pg * 9 + j) * 1024 + (16 * th + 4 * mq + r) * 32 + 16 * hh + mi] = acc[j][hh][r];
+  __syncthreads();
+
+  // ---- output transform + epilogue: thread = channel oc of tiles ot, ot + 16 ----
+  const int oc = tid & 31;
+  const int col = n0 + oc;
+  const bool second = col >= e.n_split;
+  float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
+  const int dC = second ? e.d[1].C : e.d[0].C;
+  const int dcol = second ? col - e.n_split : col;
+  const bool bwd_mask = e.yref != nullptr && !second;
+  const float bias = e.bias ? e.bias[col] : 0.f;
+  float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
+  if (bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int ot = (tid >> 5) + 16 * k;
+    const long long tt = t0 + ot;
+    if (tt >= T) continue;
+    float w[4][6];
+#pragma unroll
+    for (int xx = 0; xx < 6; ++xx) {
+      float m[6];
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy) m[yy] = X[(yy * 6 + xx) * 1024 + ot * 32 + oc];
+      float o[4];
+      at4(m, o);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) w[a][xx] = o[a];
+    }
+    const int ox = (int)(tt % Tw);
+    const long long r = tt / Tw;
+    const int oy = (int)(r % Th), on = (int)(r / Th);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float o[4];
+      at4(w[a], o);
+      const int y = 4 * oy + a;
+      if (y >= g.Hg) continue;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const int x = 4 * ox + bb;
+        if (x >= g.Wg) continue;
+        float v = o[bb] + bias;
+        const size_t idx = ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol;
+        if (bwd_mask) {
+          const float yv = e.yref[idx];
+          v = fmaf(yv, bsc, bsh) > 0.f ? v : 0.f;
+          s1 += v;
+          s2 += v * ((yv - bmu) * bis);
+        } else if (e.stats) {
+          s1 += v;
+          s2 += v * v;
+        } else if (second && e.colsum1) {
+          s1 += v;
+        }
+        dptr[idx] = v;
+      }
+    }
+  }
+  const bool want = e.stats || e.yref || e.colsum1;
+  if (!want) return;
+  __syncthreads();
+  float* red = lds;  // [2][16][32]
+  red[tid] = s1;
+  red[512 + tid] = s2;
+  __syncthreads();
+  if (tid < 32) {
+    float a = 0.f, b2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      a += red[q * 32 + tid];
+      b2 += red[512 + q * 32 + tid];
+    }
+    const int grp = blockIdx.x % kStatGroups;
+    const int nsplit = e.n_split < N ? e.n_split : N;
+    if (col < nsplit) {
+      double* st = e.yref ? e.bstats : e.stats;
+      if (st) {
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b2);
+      }
+    } else if (e.colsum1) {
+      atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (col - nsplit), (double)a);
+    }
+  }
+}
+
+bool wino_fused_applies(const IgemmArgs& a) {
+  constexpr int ck = 16;
+  const Gather& g = a.a;
+  if (a.b == nullptr || a.bh != nullptr || a.batch != 1) return false;
+  if (g.taps_h != 3 || g.taps_w != 3 || g.stride != 1 || a.K != 9 * g.Cg || g.Cg % ck != 0 ||
+      g.c_split % ck != 0 || a.N % 32 != 0)
+    return false;
+  if (g.s[0].h16 || g.s[1].h16 || a.e.shuffle_co || a.e.d[0].h16 || a.e.d[1].h16 || a.e.yref_h16) return false;
+  if (a.e.d[0].oy || a.e.d[0].ox || a.e.d[0].H != g.Hg || a.e.d[0].W != g.Wg) return false;
+  if (a.e.n_split < a.N && (a.e.d[1].oy || a.e.d[1].ox || a.e.d[1].H != g.Hg || a.e.d[1].W != g.Wg)) return false;
+  for (int k = 0; k < 2; ++k)  // 32-bit byte offsets into the sources
+    if ((long long)g.nimg * g.s[k].H * g.s[k].W * g.s[k].C * 4 >= (1ll << 32)) return false;
+  const long long T = (long long)g.nimg * ((g.Hg + 3) / 4) * ((g.Wg + 3) / 4);
+  if ((T + 31) / 32 * (a.N / 32) > 0x7fffffffLL) return false;
+  return a.wino_ws != nullptr && (size_t)36 * a.N * g.Cg * 4 <= a.wino_ws_bytes;
+}
+
+hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s) {
+  if (!wino_fused_applies(a)) return hipErrorInvalidValue;
+  const Gather& g = a.a;
+  const int Th = (g.Hg + 3) / 4, Tw = (g.Wg + 3) / 4;
+  const long long T = (long long)g.nimg * Th * Tw;
+  float* V = reinterpret_cast<float*>(a.wino_ws);
+  const long long nw = (long long)a.N * g.Cg;
+  const int NB = a.N / 32;
+  const long long G = (T + 31) / 32 * NB;
+  hipLaunchKernelGGL(k_wino4f_w<16>, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
+  hipLaunchKernelGGL(k_wino4f, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradient, F(4x4, 3x3) (wgrad tile 71).  The forward bilinear form
 // sum_p (A y)_p (G g)_p (B^T d)_p gives, differentiated by g,
 //   dW = G^T [ sum_tiles (A dY A^T) . (B^T X B) ] G,
@@ -533,7 +852,9 @@ __global__ __launch_bounds__(256) void k_wino4_dy(Src dy, int Hg, int Wg, int Th
 #pragma unroll
     for (int yy = 0; yy < 4; ++yy) {
       const int y = 4 * ty + yy, x = 4 * tx + xx;
-      d[yy] = (y < Hg && x < Wg) ? dy.ptr[((size_t)(n * dy.H + y + dy.oy) * dy.W + x + dy.ox) * dy.C + c] : 0.f;
+      const bool in = y < Hg && x < Wg;
+      const float v = dy.ptr[((size_t)(n * dy.H + (in ? y : 0) + dy.oy) * dy.W + (in ? x : 0) + dy.ox) * dy.C + c];
+      d[yy] = in ? v : 0.f;
     }
     float rr[6];
     a6(d, rr);
