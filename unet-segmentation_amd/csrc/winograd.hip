@@ -537,6 +537,97 @@ __global__ void k_wino4f_w(const float* __restrict__ b, int N, int Cg, float* __
 // float offset of 16-B piece q of LDS row `row` (16 floats per row)
 __device__ __forceinline__ int wf_off(int row, int q) { return row * 16 + ((q ^ (((row >> 3) & 1) << 1)) << 2); }
 
+// Output stage of the fused kernels (512 threads): X = LDS [36][32 tiles][32
+// channels] holds the point accumulators; thread = channel oc of tiles ot and
+// ot + 16 applies A^T M A and the epilogue of k_wino4_out to their 16 pixels.
+__device__ __forceinline__ void wf_output(float* lds, int tid, long long t0, int n0, long long T, int Th, int Tw,
+                                          int N, const Gather& g, const Epilogue& e) {
+  const float* X = lds;
+  const int oc = tid & 31;
+  const int col = n0 + oc;
+  const bool second = col >= e.n_split;
+  float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
+  const int dC = second ? e.d[1].C : e.d[0].C;
+  const int dcol = second ? col - e.n_split : col;
+  const bool bwd_mask = e.yref != nullptr && !second;
+  const float bias = e.bias ? e.bias[col] : 0.f;
+  float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
+  if (bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int k = 0; k < 2; ++k) {
+    const int ot = (tid >> 5) + 16 * k;
+    const long long tt = t0 + ot;
+    if (tt >= T) continue;
+    float w[4][6];
+#pragma unroll
+    for (int xx = 0; xx < 6; ++xx) {
+      float m[6];
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy) m[yy] = X[(yy * 6 + xx) * 1024 + ot * 32 + oc];
+      float o[4];
+      at4(m, o);
+#pragma unroll
+      for (int a = 0; a < 4; ++a) w[a][xx] = o[a];
+    }
+    const int ox = (int)(tt % Tw);
+    const long long r = tt / Tw;
+    const int oy = (int)(r % Th), on = (int)(r / Th);
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float o[4];
+      at4(w[a], o);
+      const int y = 4 * oy + a;
+      if (y >= g.Hg) continue;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const int x = 4 * ox + bb;
+        if (x >= g.Wg) continue;
+        float v = o[bb] + bias;
+        const size_t idx = ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol;
+        if (bwd_mask) {
+          const float yv = e.yref[idx];
+          v = fmaf(yv, bsc, bsh) > 0.f ? v : 0.f;
+          s1 += v;
+          s2 += v * ((yv - bmu) * bis);
+        } else if (e.stats) {
+          s1 += v;
+          s2 += v * v;
+        } else if (second && e.colsum1) {
+          s1 += v;
+        }
+        dptr[idx] = v;
+      }
+    }
+  }
+  const bool want = e.stats || e.yref || e.colsum1;
+  if (!want) return;
+  __syncthreads();
+  float* red = lds;  // [2][16][32]
+  red[tid] = s1;
+  red[512 + tid] = s2;
+  __syncthreads();
+  if (tid < 32) {
+    float a = 0.f, b2 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      a += red[q * 32 + tid];
+      b2 += red[512 + q * 32 + tid];
+    }
+    const int grp = blockIdx.x % kStatGroups;
+    const int nsplit = e.n_split < N ? e.n_split : N;
+    if (col < nsplit) {
+      double* st = e.yref ? e.bstats : e.stats;
+      if (st) {
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b2);
+      }
+    } else if (e.colsum1) {
+      atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (col - nsplit), (double)a);
+    }
+  }
+}
+
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
 __global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __restrict__ V, int N, long long T,
@@ -694,90 +785,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __rest
         X[(pg * 9 + j) * 1024 + (16 * th + 4 * mq + r) * 32 + 16 * hh + mi] = acc[j][hh][r];
   __syncthreads();
 
-  // ---- output transform + epilogue: thread = channel oc of tiles ot, ot + 16 ----
-  const int oc = tid & 31;
-  const int col = n0 + oc;
-  const bool second = col >= e.n_split;
-  float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
-  const int dC = second ? e.d[1].C : e.d[0].C;
-  const int dcol = second ? col - e.n_split : col;
-  const bool bwd_mask = e.yref != nullptr && !second;
-  const float bias = e.bias ? e.bias[col] : 0.f;
-  float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
-  if (bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
-  float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-  for (int k = 0; k < 2; ++k) {
-    const int ot = (tid >> 5) + 16 * k;
-    const long long tt = t0 + ot;
-    if (tt >= T) continue;
-    float w[4][6];
-#pragma unroll
-    for (int xx = 0; xx < 6; ++xx) {
-      float m[6];
-#pragma unroll
-      for (int yy = 0; yy < 6; ++yy) m[yy] = X[(yy * 6 + xx) * 1024 + ot * 32 + oc];
-      float o[4];
-      at4(m, o);
-#pragma unroll
-      for (int a = 0; a < 4; ++a) w[a][xx] = o[a];
-    }
-    const int ox = (int)(tt % Tw);
-    const long long r = tt / Tw;
-    const int oy = (int)(r % Th), on = (int)(r / Th);
-#pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      float o[4];
-      at4(w[a], o);
-      const int y = 4 * oy + a;
-      if (y >= g.Hg) continue;
-#pragma unroll
-      for (int bb = 0; bb < 4; ++bb) {
-        const int x = 4 * ox + bb;
-        if (x >= g.Wg) continue;
-        float v = o[bb] + bias;
-        const size_t idx = ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol;
-        if (bwd_mask) {
-          const float yv = e.yref[idx];
-          v = fmaf(yv, bsc, bsh) > 0.f ? v : 0.f;
-          s1 += v;
-          s2 += v * ((yv - bmu) * bis);
-        } else if (e.stats) {
-          s1 += v;
-          s2 += v * v;
-        } else if (second && e.colsum1) {
-          s1 += v;
-        }
-        dptr[idx] = v;
-      }
-    }
-  }
-  const bool want = e.stats || e.yref || e.colsum1;
-  if (!want) return;
-  __syncthreads();
-  float* red = lds;  // [2][16][32]
-  red[tid] = s1;
-  red[512 + tid] = s2;
-  __syncthreads();
-  if (tid < 32) {
-    float a = 0.f, b2 = 0.f;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      a += red[q * 32 + tid];
-      b2 += red[512 + q * 32 + tid];
-    }
-    const int grp = blockIdx.x % kStatGroups;
-    const int nsplit = e.n_split < N ? e.n_split : N;
-    if (col < nsplit) {
-      double* st = e.yref ? e.bstats : e.stats;
-      if (st) {
-        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
-        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b2);
-      }
-    } else if (e.colsum1) {
-      atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (col - nsplit), (double)a);
-    }
-  }
+  wf_output(lds, tid, t0, n0, T, Th, Tw, N, g, e);
 }
 
 bool wino_fused_applies(const IgemmArgs& a) {
