@@ -203,6 +203,13 @@ def run_precision(args, dtype, device, pg, world, rank):
     trainer.plan.set_timing(False)
     tim = trainer.plan.timing()
     xfl = trainer.plan.mfma_flops()
+    comm = None
+    if pg is not None:
+        comm = {"collective": f"all_reduce(SUM) of {len(trainer.reducer.buckets)} gradient buckets, each issued as its "
+                              "backward segment finishes" if trainer.overlap else "one all_reduce after backward",
+                "dtype": str(trainer.comm_dtype).replace("torch.", ""),
+                "bytes_per_step": trainer.reducer.bytes_per_step,
+                "buffers": "rank 0's BatchNorm running statistics broadcast at each step start (one flat buffer)"}
     del trainer, model, x, t, w
     torch.cuda.empty_cache()
 
@@ -264,6 +271,7 @@ def run_precision(args, dtype, device, pg, world, rank):
                    "traffic": fam.get("stage1", {}).get("bytes_per_step")},
         "kernels": kernels,
         "final_loss": round(final_loss, 5),
+        "comm": comm,
     }
 
 
@@ -333,6 +341,8 @@ def main():
         }
         for k in ("roofline", "bottleneck", "stage1", "kernels", "final_loss"):
             out[k] = main_res[k]
+        if main_res["comm"] is not None:
+            out["comm"] = main_res["comm"]
         for d, r in extras.items():
             out[d] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
                       "config": f"same workload, {GEMM_DESC[d]} GEMMs (global batch {world * args.batch}"

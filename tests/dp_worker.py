@@ -4,7 +4,7 @@ backward, the bucketed asynchronous all-reduce and the 1/world SGD scale --
 on this rank's shard.  Ranks share the one GPU of the test box and talk over
 gloo (RCCL needs one GPU per rank; the all-reduce call pattern is the same).
 
-    python tests/dp_worker.py <out.npz> <overlap 0|1> <steps>
+    python tests/dp_worker.py <out.npz> <overlap 0|1> <steps> [comm dtype fp32|bf16]
     env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT
 """
 import os
@@ -31,6 +31,7 @@ def shard(rank):
 
 def main():
     out, overlap, steps = sys.argv[1], bool(int(sys.argv[2])), int(sys.argv[3])
+    comm = {"fp32": torch.float32, "bf16": torch.bfloat16}[sys.argv[4] if len(sys.argv) > 4 else "fp32"]
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
@@ -40,7 +41,8 @@ def main():
     m = UNet(1, 2)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     m = m.cuda().train()
-    tr = Trainer(m, BATCH, SIZE, SIZE, lr=1e-4, momentum=0.99, process_group=dist.group.WORLD, overlap=overlap)
+    tr = Trainer(m, BATCH, SIZE, SIZE, lr=1e-4, momentum=0.99, process_group=dist.group.WORLD, overlap=overlap,
+                 comm_dtype=comm)
     x, t, w = (torch.from_numpy(a).cuda() for a in shard(rank))
     res = {}
     for s in range(steps):

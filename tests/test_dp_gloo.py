@@ -121,3 +121,71 @@ def test_sharded_indices_cover_dataset():
         assert all(len(s.indices()) == len(s) for s in shards)
         if world * shards[0].per_rank == n:
             assert len(set(idx)) == n  # disjoint when n divides evenly
+
+
+def _bf16_worker(rank, world, port, q):
+    try:
+        import torch
+        import torch.distributed as dist
+        from unet_amd.dist import GradBucketReducer
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world))
+        torch.set_num_threads(1)
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        g = torch.Generator().manual_seed(7 + rank)
+        flat = torch.randn(1000, generator=g, dtype=torch.float32)
+        red = GradBucketReducer(flat, [(0, 400), (400, 1000)], comm_dtype=torch.bfloat16)
+        assert red.bytes_per_step == 2000
+        red.reduce(1)
+        red.reduce(0)
+        red.wait()
+        q.put((rank, flat.numpy().copy(), None))
+        dist.destroy_process_group()
+    except Exception:  # pragma: no cover - reported to the parent
+        import traceback
+        q.put((rank, None, traceback.format_exc()))
+
+
+@pytest.mark.timeout(300)
+def test_bf16_bucket_allreduce():
+    """comm_dtype=bf16 (the bf16 plans' default): each bucket goes over the wire
+    as bf16 and comes back widened; equals the bf16 sum of the bf16-rounded
+    shards, identical on both ranks."""
+    import torch
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bf16_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    out = {}
+    for _ in procs:
+        rank, v, err = q.get(timeout=280)
+        assert err is None, err
+        out[rank] = v
+    for p in procs:
+        p.join(timeout=60)
+    shards = [torch.randn(1000, generator=torch.Generator().manual_seed(7 + r), dtype=torch.float32) for r in range(2)]
+    ref = (shards[0].bfloat16() + shards[1].bfloat16()).float().numpy()
+    np.testing.assert_array_equal(out[0], out[1])
+    np.testing.assert_array_equal(out[0], ref)
+
+
+def test_flat_buffers_rehome_running_stats():
+    """Trainer's FlatBuffers: every floating BatchNorm buffer becomes a view of
+    one flat tensor (one broadcast per step), values and state_dict unchanged."""
+    import torch
+    from unet_amd.train import FlatBuffers
+    m = torch.nn.Sequential(torch.nn.Conv2d(1, 4, 3), torch.nn.BatchNorm2d(4), torch.nn.BatchNorm2d(4))
+    with torch.no_grad():
+        for b in m.buffers():
+            if b.is_floating_point():
+                b.copy_(torch.rand_like(b))
+    before = {k: v.clone() for k, v in m.state_dict().items()}
+    fb = FlatBuffers(m)
+    assert fb.flat.numel() == 4 * 4
+    after = m.state_dict()
+    for k, v in before.items():
+        assert torch.equal(after[k], v), k
+    fb.flat.fill_(3.0)
+    assert all(torch.all(b == 3.0) for b in m.buffers() if b.is_floating_point())
+    assert all(b.dtype == torch.int64 for b in m.buffers() if not b.is_floating_point())

@@ -32,7 +32,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(tmp_path, overlap, world=2):
+def run_ranks(tmp_path, overlap, world=2, comm="fp32"):
     port = _free_port()
     procs, outs = [], []
     for r in range(world):
@@ -44,7 +44,7 @@ def run_ranks(tmp_path, overlap, world=2):
         out = str(tmp_path / f"rank{r}.npz")
         outs.append(out)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, str(int(overlap)),
-                                       str(STEPS)], env=env))
+                                       str(STEPS), comm], env=env))
     rcs = []
     for p in procs:
         try:
@@ -115,3 +115,19 @@ def test_two_rank_trainer_matches_shard_average(tmp_path, overlap):
     # sync_buffers broadcasts rank 0's (DDP buffer semantics)
     assert not np.array_equal(ranks[0]["buffers_before_sync"], ranks[1]["buffers_before_sync"])
     np.testing.assert_array_equal(ranks[1]["buffers"], ranks[0]["buffers_before_sync"])
+
+
+def test_two_rank_trainer_bf16_gradient_allreduce(tmp_path):
+    """comm_dtype=bf16 (default of the bf16 plans): the buckets travel as bf16.
+    Both ranks end identical; the first step's all-reduced gradient equals the
+    fp32 shard sum to bf16 rounding (each shard and the sum rounded once:
+    rel-L2 well under 2^-7)."""
+    ranks = run_ranks(tmp_path, True, comm="bf16")
+    sums, _ = single_process_reference()
+    for s in range(STEPS):
+        np.testing.assert_array_equal(ranks[0][f"grad{s}"], ranks[1][f"grad{s}"])
+    np.testing.assert_array_equal(ranks[0]["params"], ranks[1]["params"])
+    g, ref = ranks[0]["grad0"], sums[0]
+    rel = np.linalg.norm(g - ref) / np.linalg.norm(ref)
+    assert rel <= 2.0 ** -7, rel
+    assert rel > 0  # the wire really was bf16

@@ -73,13 +73,22 @@ class GradBucketReducer:
     ``buckets`` is a list of (start, stop) element ranges of ``flat``; call
     ``reduce(b)`` when bucket b is final (asynchronous), ``wait()`` before the
     optimizer.  The optimizer divides by the world size (the fused SGD takes a
-    gradient scale), so the buffer holds the SUM afterwards."""
+    gradient scale), so the buffer holds the SUM afterwards.
 
-    def __init__(self, flat, buckets, group=None):
+    ``comm_dtype=torch.bfloat16`` sends the buckets as bf16 (half the bytes on
+    xGMI: 62 instead of 124 MB per step for the U-Net): each bucket is rounded
+    into a bf16 shadow, reduced there and widened back into ``flat`` on
+    ``wait()``.  The bf16 GEMM plans use it by default (Trainer)."""
+
+    def __init__(self, flat, buckets, group=None, comm_dtype=None):
         self.flat = flat
         self.buckets = list(buckets)
         self.group = group
         self.works = []
+        comm_dtype = flat.dtype if comm_dtype is None else comm_dtype  # None: the buffer's own dtype
+        self.comm_dtype = comm_dtype
+        self.shadow = None if comm_dtype == flat.dtype else torch.empty(flat.numel(), dtype=comm_dtype,
+                                                                         device=flat.device)
         cover = sorted(self.buckets)
         for (a, b), (c, d) in zip(cover, cover[1:]):
             if b > c:
@@ -89,19 +98,31 @@ class GradBucketReducer:
     def world(self):
         return dist.get_world_size(self.group) if dist.is_initialized() else 1
 
+    @property
+    def bytes_per_step(self):
+        elem = torch.tensor([], dtype=self.comm_dtype).element_size()
+        return sum(z - a for a, z in self.buckets) * elem
+
     def reduce(self, b):
         if self.world == 1:
             return
         a, z = self.buckets[b]
-        self.works.append(dist.all_reduce(self.flat[a:z], group=self.group, async_op=True))
+        if self.shadow is None:
+            self.works.append((dist.all_reduce(self.flat[a:z], group=self.group, async_op=True), a, z))
+            return
+        buf = self.shadow[a:z]
+        buf.copy_(self.flat[a:z])
+        self.works.append((dist.all_reduce(buf, group=self.group, async_op=True), a, z))
 
     def reduce_all(self):
         for b in range(len(self.buckets)):
             self.reduce(b)
 
     def wait(self):
-        for w in self.works:
+        for w, a, z in self.works:
             w.wait()
+            if self.shadow is not None:
+                self.flat[a:z].copy_(self.shadow[a:z])
         self.works.clear()
 
 

@@ -14,7 +14,9 @@ SGD(lr, momentum=0.99).step() -- with the same arithmetic as the drop-in
   bf16 matrix cores (operands split into bf16 hi/lo pairs, three products);
   weights, gradients and the optimizer stay fp32 in every mode;
 * with a process group, the backward runs in 9 segments and each segment's
-  gradient bucket is all-reduced (RCCL over xGMI) while later segments compute.
+  gradient bucket is all-reduced (RCCL over xGMI) while later segments compute
+  (bf16 on the wire for bf16 plans), and every step starts by broadcasting rank
+  0's BatchNorm running statistics (one flat buffer), as DDP does.
 """
 from __future__ import annotations
 
@@ -61,9 +63,27 @@ class FlatParams:
         return a, b
 
 
+class FlatBuffers:
+    """Re-home a module's floating-point buffers (BatchNorm running statistics)
+    into one flat buffer, so that DDP's per-step buffer broadcast is a single
+    collective instead of one per tensor."""
+
+    def __init__(self, module: torch.nn.Module):
+        bufs = [b for b in module.buffers() if b.is_floating_point()]
+        total = sum(b.numel() for b in bufs)
+        self.flat = torch.zeros(total, dtype=torch.float32, device=bufs[0].device) if bufs else None
+        o = 0
+        with torch.no_grad():
+            for b in bufs:
+                view = self.flat[o:o + b.numel()].view_as(b)
+                view.copy_(b.data)
+                b.data = view
+                o += b.numel()
+
+
 class Trainer:
     def __init__(self, model, batch, height, width, lr=1e-4, momentum=0.99, process_group=None,
-                 overlap=True, precision="fp32"):
+                 overlap=True, precision="fp32", comm_dtype=None, broadcast_buffers=True):
         from .modules import UNet
         if not isinstance(model, UNet):
             raise TypeError("Trainer drives the MI355X UNet")
@@ -73,6 +93,9 @@ class Trainer:
         self.overlap = overlap
         self.world = torch.distributed.get_world_size(process_group) if process_group is not None else 1
         self.flat = FlatParams(model)
+        self.flat_buffers = FlatBuffers(model)
+        # DDP default: every step starts from rank 0's BatchNorm running statistics
+        self.broadcast_buffers = broadcast_buffers and self.world > 1
         dev = self.flat.flat.device
         self.plan = Plan(batch, model.n_channels, height, width, model.n_classes, precision)
         self.ws = torch.empty(self.plan.workspace_bytes, dtype=torch.uint8, device=dev)
@@ -87,8 +110,13 @@ class Trainer:
         self.first_step = True
         self.lib = _lib.load()
         buckets = [self.flat.range_for(*self.plan.segment_grads(s)) for s in range(N_SEGMENTS)]
-        self.reducer = GradBucketReducer(self.flat.grad, buckets, process_group)
-        self.reducer_whole = GradBucketReducer(self.flat.grad, [(0, self.flat.numel)], process_group)
+        # gradient all-reduce dtype: bf16 for the bf16 GEMM plans (half the xGMI
+        # bytes), fp32 otherwise
+        if comm_dtype is None:
+            comm_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
+        self.comm_dtype = comm_dtype
+        self.reducer = GradBucketReducer(self.flat.grad, buckets, process_group, comm_dtype)
+        self.reducer_whole = GradBucketReducer(self.flat.grad, [(0, self.flat.numel)], process_group, comm_dtype)
 
     @property
     def out_hw(self):
@@ -141,14 +169,20 @@ class Trainer:
 
     def step(self, x, targets, weights):
         """One train.py step; returns the (device) loss without synchronising."""
+        if self.broadcast_buffers and self.flat_buffers.flat is not None:
+            torch.distributed.broadcast(self.flat_buffers.flat, 0, group=self.pg)
         loss = self.forward_loss(x, targets, weights)
         self.backward_and_reduce(x)
         self.optimizer_step()
         return loss
 
     def sync_buffers(self, src=0):
-        """DDP buffer semantics: broadcast rank-src BatchNorm running stats."""
+        """Broadcast rank-src BatchNorm running statistics now (``step`` does it
+        at the start of every step unless ``broadcast_buffers=False``)."""
         if self.pg is None:
             return
+        if self.flat_buffers.flat is not None:
+            torch.distributed.broadcast(self.flat_buffers.flat, src, group=self.pg)
         for name, t in self.model.named_buffers():
-            torch.distributed.broadcast(t, src, group=self.pg)
+            if not t.is_floating_point():
+                torch.distributed.broadcast(t, src, group=self.pg)
