@@ -34,13 +34,15 @@ def last_step(d):
 
 def family(name):
     """Kernel family of a dispatch, matching bench.py's timing classes: the
-    implicit-GEMM conv family (every igemm / halo conv / wgrad kernel and the
-    split-K epilogue its launch site runs) and the stage-1 kernels (inc.c0
+    implicit-GEMM conv family (every igemm / halo conv / wgrad / Winograd kernel,
+    the split-K epilogue and the accumulator fills its launch sites run) and the
+    stage-1 kernels (inc.c0
     forward and its fused BN0-backward weight gradient + slab reduction)."""
     if "conv_first" in name or "reduce_slabs" in name:
         return "stage1"
-    if "igemm" in name or "conv3" in name or "splitk_epi" in name or "wgrad" in name:
-        return "conv"
+    if ("igemm" in name or "conv3" in name or "splitk_epi" in name or "wgrad" in name or "wino" in name or
+            "fillBuffer" in name):
+        return "conv"  # Winograd transforms / point GEMMs and the zeroing of its wgrad accumulators included
     return "other"
 
 

@@ -22,6 +22,8 @@
 // Transform arithmetic is exact in the +-1, 1/2 coefficients; the fp32
 // rounding of the 16-term products differs from the direct sum's, at the same
 // order (tests/test_gpu_ops.py, tests/test_gpu_model.py force tile 70).
+#include <cstdlib>
+
 #include "gemm_common.h"
 
 namespace unet {
@@ -262,47 +264,81 @@ __global__ void k_wino4_w(const float* __restrict__ b, int N, int Cg, float* __r
   }
 }
 
+// Thread = (tile, V consecutive channels): V-wide loads and stores (V = 4 when
+// the channel count allows), 32-bit byte offsets from the source base.
+template <int V>
 __global__ __launch_bounds__(256) void k_wino4_in(Gather g, int Th, int Tw, long long T, float* __restrict__ u) {
+  typedef float vec __attribute__((ext_vector_type(V)));
+  const int CV = g.Cg / V;
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (i >= T * g.Cg) return;
-  const long long t = i / g.Cg;
-  const int c = (int)(i - t * g.Cg);
+  if (i >= T * CV) return;
+  const long long t = i / CV;
+  const int c = (int)(i - t * CV) * V;
   const int tx = (int)(t % Tw);
   const long long r = t / Tw;
   const int ty = (int)(r % Th), n = (int)(r / Th);
   const bool second = c >= g.c_split;
   const Src s = pick_src(g, second);
   const int cl = second ? c - g.c_split : c;
-  float sc = 1.f, sh = 0.f;
+  vec sc, sh;
   if (s.scale) {
-    sc = s.scale[cl];
-    sh = s.shift[cl];
+    sc = *reinterpret_cast<const vec*>(s.scale + cl);
+    sh = *reinterpret_cast<const vec*>(s.shift + cl);
   }
-  float e[6][6];  // B^T d (rows), per column
+  const int vr = min(6, g.Hg + 2 - 4 * ty), vc = min(6, g.Wg + 2 - 4 * tx);  // in-window rows / columns
+  const char* base = reinterpret_cast<const char*>(s.ptr) +
+                     ((size_t)(n * s.H + 4 * ty + s.oy) * s.W + 4 * tx + s.ox) * s.C * 4 + (size_t)cl * 4;
+  const unsigned rs = (unsigned)s.W * s.C * 4u, cs = (unsigned)s.C * 4u;
+  vec e[6][6];  // B^T d (rows), per column
 #pragma unroll
   for (int xx = 0; xx < 6; ++xx) {
-    float d[6];
+    vec d[6];
 #pragma unroll
     for (int yy = 0; yy < 6; ++yy) {
-      const int y = 4 * ty + yy, x = 4 * tx + xx;
-      const bool in = y < g.Hg + 2 && x < g.Wg + 2;  // unconditional load, clamped address
-      float v = s.ptr[((size_t)(n * s.H + (in ? y : 0) + s.oy) * s.W + (in ? x : 0) + s.ox) * s.C + cl];
-      if (s.scale) v = fmaxf(fmaf(v, sc, sh), 0.f);
-      d[yy] = in ? v : 0.f;
-    }
-    float rr[6];
-    bt6(d, rr);
+      const bool in = yy < vr && xx < vc;  // unconditional load, clamped address
+      vec v = *reinterpret_cast<const vec*>(base + (in ? yy * rs + xx * cs : 0u));
+      if (s.scale) {
 #pragma unroll
-    for (int a = 0; a < 6; ++a) e[a][xx] = rr[a];
+        for (int k = 0; k < V; ++k) v[k] = fmaxf(fmaf(v[k], sc[k], sh[k]), 0.f);
+      }
+      d[yy] = in ? v : (vec)0.f;
+    }
+    e[0][xx] = 4.f * d[0] - 5.f * d[2] + d[4];
+    e[1][xx] = -4.f * (d[1] + d[2]) + d[3] + d[4];
+    e[2][xx] = 4.f * (d[1] - d[2]) - d[3] + d[4];
+    e[3][xx] = 2.f * (d[3] - d[1]) - d[2] + d[4];
+    e[4][xx] = 2.f * (d[1] - d[3]) - d[2] + d[4];
+    e[5][xx] = 4.f * d[1] - 5.f * d[3] + d[5];
   }
   const size_t plane = (size_t)T * g.Cg, o = (size_t)t * g.Cg + c;
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    float rr[6];
-    bt6(e[a], rr);
+    const vec* d = e[a];
+    vec rr[6];
+    rr[0] = 4.f * d[0] - 5.f * d[2] + d[4];
+    rr[1] = -4.f * (d[1] + d[2]) + d[3] + d[4];
+    rr[2] = 4.f * (d[1] - d[2]) - d[3] + d[4];
+    rr[3] = 2.f * (d[3] - d[1]) - d[2] + d[4];
+    rr[4] = 2.f * (d[1] - d[3]) - d[2] + d[4];
+    rr[5] = 4.f * d[1] - 5.f * d[3] + d[5];
 #pragma unroll
-    for (int bb = 0; bb < 6; ++bb) u[(a * 6 + bb) * plane + o] = rr[bb];
+    for (int bb = 0; bb < 6; ++bb) *reinterpret_cast<vec*>(u + (a * 6 + bb) * plane + o) = rr[bb];
   }
+}
+
+static int wino4_in_vec() {
+  static const int v = getenv("UNET_WINO_IN_VEC") ? atoi(getenv("UNET_WINO_IN_VEC")) : 2;
+  return v;
+}
+
+static void launch_wino4_in(const Gather& g, int Th, int Tw, long long T, float* U, hipStream_t s) {
+  int V = wino4_in_vec();
+  while (V > 1 && (g.Cg % V || g.c_split % V)) V >>= 1;
+  const long long n = T * (g.Cg / V);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (V == 4) hipLaunchKernelGGL(k_wino4_in<4>, grid, dim3(256), 0, s, g, Th, Tw, T, U);
+  else if (V == 2) hipLaunchKernelGGL(k_wino4_in<2>, grid, dim3(256), 0, s, g, Th, Tw, T, U);
+  else hipLaunchKernelGGL(k_wino4_in<1>, grid, dim3(256), 0, s, g, Th, Tw, T, U);
 }
 
 // Block = 64 channels x 4 tile lanes; grid-stride over tiles.
@@ -436,8 +472,7 @@ hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt) {
     hipLaunchKernelGGL(k_wino_in, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, s, g, Th, Tw, T, U);
   } else {
     hipLaunchKernelGGL(k_wino4_w, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
-    const long long ni = T * g.Cg;
-    hipLaunchKernelGGL(k_wino4_in, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, s, g, Th, Tw, T, U);
+    launch_wino4_in(g, Th, Tw, T, U, s);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -934,8 +969,8 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu) {
   float* U = reinterpret_cast<float*>(w);
   float* Vd = reinterpret_cast<float*>(w + al((size_t)36 * T * Ci * 4));
   float* Mw = reinterpret_cast<float*>(w + al((size_t)36 * T * Ci * 4) + al((size_t)36 * T * Co * 4));
-  const long long ni = T * Ci, nd = T * Co;
-  hipLaunchKernelGGL(k_wino4_in, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, s, gb, Th, Tw, T, U);
+  const long long nd = T * Co;
+  launch_wino4_in(gb, Th, Tw, T, U, s);
   hipLaunchKernelGGL(k_wino4_dy, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg, gb.Wg, Th,
                      Tw, T, Co, Vd);
   hipError_t e = hipMemsetAsync(Mw, 0, (size_t)36 * Co * Ci * 4, s);
