@@ -665,6 +665,10 @@ __device__ __forceinline__ void wf_output(float* lds, int tid, long long t0, int
 
 typedef float floatx4 __attribute__((ext_vector_type(4)));
 
+// ABL: ablation switches for timing experiments only (UNET_WF_ABL; results are
+// wrong with any bit set): 1 = no input transform / BatchNorm, 2 = no MFMA,
+// 4 = no global loads in the chunk loop
+template <int ABL>
 __global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __restrict__ V, int N, long long T,
                                                    int Th, int Tw, int NB, Epilogue e) {
   constexpr int PS = 32 * 16;  // floats per point plane of U / V
@@ -694,6 +698,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __rest
   const int vrows = t < T ? min(6, g.Hg + 2 - 4 * ty) : 0;
   const int vcols = t < T ? min(6, g.Wg + 2 - 4 * tx) : 0;
   const bool full = vrows == 6 && vcols == 6;
+  const bool wfull = __all(full);
   const int uoff = wf_off(lt, lc >> 2) + (lc & 3);
   float raw[36];
   float4 vr[9];
@@ -711,21 +716,22 @@ __global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __rest
     const char* sb = reinterpret_cast<const char*>(sp);
     const unsigned o0 = ((unsigned)((img * sH + 4 * ty + soy) * sW + 4 * tx + sox) * sC + cl) * 4u;
     const unsigned rs = (unsigned)sW * sC * 4u, cs = (unsigned)sC * 4u;
-    if (full) {
+    if (wfull) {  // wave-uniform: no edge tile in this wave
 #pragma unroll
       for (int yy = 0; yy < 6; ++yy)
 #pragma unroll
         for (int xx = 0; xx < 6; ++xx)
           raw[yy * 6 + xx] = *reinterpret_cast<const float*>(sb + (o0 + (yy * rs + xx * cs)));
     } else {
-      // edge tiles: positions outside the window read the patch origin (always
-      // in bounds) and are zeroed in commit
+      // edge tiles: rows / columns past the window re-read the last in-window
+      // one (branch-free clamp; zeroed in commit)
+      const unsigned lr = (unsigned)max(vrows - 1, 0), lcn = (unsigned)max(vcols - 1, 0);
 #pragma unroll
       for (int yy = 0; yy < 6; ++yy)
 #pragma unroll
         for (int xx = 0; xx < 6; ++xx)
-          raw[yy * 6 + xx] =
-              *reinterpret_cast<const float*>(sb + (o0 + (yy < vrows && xx < vcols ? yy * rs + xx * cs : 0u)));
+          raw[yy * 6 + xx] = *reinterpret_cast<const float*>(
+              sb + (o0 + (min((unsigned)yy, lr) * rs + min((unsigned)xx, lcn) * cs)));
     }
     const char* vb = reinterpret_cast<const char*>(V + ((size_t)kc * 36 * N + n0) * 16);
     const unsigned vo = ((unsigned)(tid >> 7) * N * 16u + ((tid >> 2) & 31) * 16u + (tid & 3) * 4u) * 4u;
@@ -738,12 +744,16 @@ __global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __rest
     const float* scp = second ? g.s[1].scale : g.s[0].scale;
     const float* shp = second ? g.s[1].shift : g.s[0].shift;
     const int cl = kc * 16 - (second ? g.c_split : 0) + lc;
+    if constexpr (ABL & 1) {
+#pragma unroll
+      for (int q = 0; q < 36; ++q) Us[q * PS + uoff] = raw[q];
+    } else {
     if (scp) {
       const float sc = scp[cl], sh = shp[cl];
 #pragma unroll
       for (int q = 0; q < 36; ++q) raw[q] = fmaxf(fmaf(raw[q], sc, sh), 0.f);
     }
-    if (!full) {
+    if (!wfull) {
 #pragma unroll
       for (int q = 0; q < 36; ++q) raw[q] = (q / 6 < vrows && q % 6 < vcols) ? raw[q] : 0.f;
     }
@@ -767,6 +777,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __rest
 #pragma unroll
       for (int bb = 0; bb < 6; ++bb) Us[(a * 6 + bb) * PS + uoff] = rr[bb];
     }
+    }
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       const int q = tid + 512 * j;
@@ -789,7 +800,8 @@ __global__ __launch_bounds__(512, 1) void k_wino4f(Gather g, const float* __rest
   for (int kc = 0; kc < nk; ++kc) {
     commit(kc);
     __syncthreads();
-    if (kc + 1 < nk) load(kc + 1);
+    if (!(ABL & 4) && kc + 1 < nk) load(kc + 1);
+    if constexpr (!(ABL & 2))
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       const int p = pg * 9 + j;
@@ -850,9 +862,18 @@ hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s) {
   const int NB = a.N / 32;
   const long long G = (T + 31) / 32 * NB;
   hipLaunchKernelGGL(k_wino4f_w<16>, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
-  hipLaunchKernelGGL(k_wino4f, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  static const int abl = getenv("UNET_WF_ABL") ? atoi(getenv("UNET_WF_ABL")) : 0;
+  switch (abl) {
+    case 1: hipLaunchKernelGGL(k_wino4f<1>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;
+    case 2: hipLaunchKernelGGL(k_wino4f<2>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;
+    case 4: hipLaunchKernelGGL(k_wino4f<4>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;
+    case 6: hipLaunchKernelGGL(k_wino4f<6>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;
+    default: hipLaunchKernelGGL(k_wino4f<0>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  }
   return hipGetLastError();
 }
+
+
 
 // ---------------------------------------------------------------------------
 // Weight gradient, F(4x4, 3x3) (wgrad tile 71).  The forward bilinear form
