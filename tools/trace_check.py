@@ -22,7 +22,7 @@ import os
 import sqlite3
 import sys
 
-GEMM = ("k_igemm", "k_conv3", "k_wgrad")
+GEMM = ("k_igemm", "k_conv3", "k_wgrad", "k_wino", "fillBuffer")  # Winograd + its wgrad accumulator fills
 
 
 def short(name):
