@@ -1303,6 +1303,7 @@ hipError_t launch_igemm_v(const IgemmArgs& a0, hipStream_t s, GemmChoice c) {
   if (!igemm_args_ok(a0) || !igemm_tile_fits(a0, c.tile)) return hipErrorInvalidValue;
   IgemmArgs a = a0;
   const int nk = a.K / tile_info(c.tile).bk;
+  if ((c.tile == 70 || c.tile == 71) && c.split >= 100) a.wino_choice.tile = c.split - 100;  // point-GEMM tile
   int ks = c.split < 1 || (c.tile >= 70 && c.tile <= 72) ? 1 : (c.split > nk ? nk : c.split);
   if (ks > 1) {  // no empty slice: ks = ceil(nk / ceil(nk / ks))
     const int per = (nk + ks - 1) / ks;
@@ -1357,7 +1358,7 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     else tile = 4;
   }
   if (!wgrad_tile_fits(a, tile)) return hipErrorInvalidValue;
-  if (tile == 71) return launch_wino_wgrad(a, s, c.split > 0 ? c.split : 8);
+  if (tile == 71) return launch_wino_wgrad(a, s, c.split);
   if (tile == 20 || tile == 21) return go_wgrad3_bf16(a, s, tile, c.split > 0 ? c.split : 4);
   if (tile == 22) return go_wgrad3_f32<8, 16>(a, s, c.split > 0 ? c.split : 4);
   if (tile == 23) return go_wgrad3_f32<4, 32>(a, s, c.split > 0 ? c.split : 4);

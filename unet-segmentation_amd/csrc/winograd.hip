@@ -501,8 +501,8 @@ hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt) {
     q.batch_b = (long long)a.N * g.Cg;
     // 256 x 128 tiles when they give two rounds of workgroups, else 128 x 128
     // (register-staged k_igemm: the batched launch form)
-    int tile = a.wino_choice.tile;
-    if (tile != 1 && tile != 3 && tile != 4) {
+    int tile = a.wino_choice.tile;  // autotuned (GemmChoice split 100 + tile), else the heuristic
+    if (tile <= 0 || !igemm_tile_fits(q, tile)) {
       const long long t256 = ((T + 255) / 256) * (a.N / 128) * P;
       tile = (a.N % 128 == 0 && t256 >= 2 * num_cus()) ? 4 : (a.N % 128 == 0 ? 1 : 8);
     }
@@ -978,7 +978,12 @@ bool wino_wgrad_applies(const WgradArgs& a) {
   return wino_bytes(36, wino_wgrad_tiles(a), gb.Cg, a.Mo) <= a.wino_ws_bytes;
 }
 
+// per_cu: workgroups per CU of the point GEMMs' pixel split, + 100 * (1 + k_wgrad
+// tile id) to force their tile (autotuner candidates)
 hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu) {
+  const int forced = per_cu >= 100 ? per_cu / 100 - 1 : -1;
+  per_cu %= 100;
+  if (per_cu <= 0) per_cu = 8;
   if (!wino_wgrad_applies(a)) return hipErrorInvalidValue;
   const Gather& gb = a.gb;
   const int Th = (gb.Hg + 3) / 4, Tw = (gb.Wg + 3) / 4;
@@ -1026,7 +1031,8 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu) {
     q.batch_a = T * Co;
     q.batch_b = T * Ci;
     q.batch_out = (long long)Co * Ci;
-    const int tile = (Co % 128 == 0 && Ci % 128 == 0) ? 0 : (Ci % 128 == 0 ? 3 : 4);
+    int tile = (Co % 128 == 0 && Ci % 128 == 0) ? 0 : (Ci % 128 == 0 ? 3 : 4);
+    if (forced >= 0 && wgrad_tile_fits(q, forced)) tile = forced;
     if ((e = launch_wgrad_v(q, s, GemmChoice{tile, per_cu})) != hipSuccess) return e;
   }
   const long long no = (long long)Co * Ci;
