@@ -171,7 +171,7 @@ def run_precision(args, dtype, device, pg, world, rank):
         for t in model.state_dict().values():
             dist.broadcast(t, 0)
     trainer = Trainer(model, args.batch, args.size, args.size, lr=1e-4, momentum=0.99, process_group=pg,
-                      overlap=not args.no_overlap, precision=dtype)
+                      overlap=not args.no_overlap, precision=dtype, graph=args.graph)
     oh, ow = trainer.out_hw
     x, t, w = synthetic_batch(args.batch, args.size, oh, device, seed=1234 + rank, channels=args.channels)
 
@@ -292,6 +292,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-iou", action="store_true")
     ap.add_argument("--no-overlap", action="store_true")
+    ap.add_argument("--graph", action="store_true",
+                    help="single process: replay the whole train step as one hipGraph after the autotuned warm-up")
     ap.add_argument("--tuning-report", default=None, help="write the GEMM autotuner's choices to this file")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (ranks may share a GPU; rehearsal only)")

@@ -615,3 +615,48 @@ def test_hela_train_step_real_data():
         r = float(z[f"dnorm/{k}"])
         floor = abs(float(z[f"dnorm32/{k}"]) - r)
         assert abs(d - r) <= max(1e-2 * r, 2 * floor), (k, d, r, floor)
+
+
+def test_trainer_hipgraph_replay_matches_eager():
+    """Trainer(graph=True) captures the whole step (two streams) after two eager
+    steps.  From one snapshot of the full training state (weights, momentum,
+    BN running statistics), one graph replay and one eager step must give the
+    same loss, weights, momentum and statistics (up to the fp32 atomic order
+    of the weight gradients, which already differs between two eager runs)."""
+    from unet_amd import UNet
+    from unet_amd.train import Trainer
+    params = O.hash_init(1, 2, seed=77, bn_random=True)
+    x, t, w = (torch.from_numpy(a).cuda() for a in F.make_inputs(77, 2, 1, 188))
+    m = UNet(1, 2)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    m = m.cuda().train()
+    tr = Trainer(m, 2, 188, 188, lr=1e-4, momentum=0.99, graph=True)
+    for _ in range(2):
+        tr.step(x, t, w)
+    assert tr._graph is not None, tr.graph_error
+    state = [tr.flat.flat, tr.flat.momentum, tr.flat_buffers.flat]
+    snap = [v.clone() for v in state]
+    nbt = [b for b in m.buffers() if not b.is_floating_point()]
+    nbt0 = [b.clone() for b in nbt]
+
+    def run(graph):
+        for v, s0 in zip(state, snap):
+            v.copy_(s0)
+        for b, b0 in zip(nbt, nbt0):
+            b.copy_(b0)
+        if graph:
+            loss = tr.step(x, t, w)  # replay
+        else:
+            loss = tr.forward_loss(x, t, w)
+            tr.backward_and_reduce(x)
+            tr.optimizer_step()
+        torch.cuda.synchronize()
+        return float(loss.item()), [v.cpu().numpy().copy() for v in state], [int(b.item()) for b in nbt]
+
+    lg, sg, ng = run(True)
+    le, se, ne = run(False)
+    assert abs(lg - le) <= 1e-5 * abs(le), (lg, le)
+    for a, b, s0 in zip(sg, se, snap):
+        upd = np.abs(b - s0.cpu().numpy()).max()
+        assert np.abs(a - b).max() <= 1e-4 * upd + 1e-7 * np.abs(b).max()
+    assert ng == ne == [int(b.item()) + 1 for b in nbt0]

@@ -306,11 +306,12 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
       if (igemm_tile_fits(a, t)) return GemmChoice{t, ks};
     return GemmChoice{};
   }
-  if (!env_autotune() || capturing(c.s)) return GemmChoice{};
+  if (!env_autotune()) return GemmChoice{};
   const std::string key = igemm_key(a);
   std::lock_guard<std::mutex> lk(g_tune_mu);
   auto it = g_tuned.find(key);
   if (it != g_tuned.end()) return it->second;
+  if (capturing(c.s)) return GemmChoice{};  // hipGraph capture: replay the tuned choice, never time
   IgemmArgs t = a;
   double* scr = c.d(c.p->tune_scratch);
   if (t.e.stats) t.e.stats = scr;
@@ -340,11 +341,12 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
 }
 
 GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
-  if (!env_autotune() || capturing(c.s)) return GemmChoice{};
+  if (!env_autotune()) return GemmChoice{};
   const std::string key = wgrad_key(a);
   std::lock_guard<std::mutex> lk(g_tune_mu);
   auto it = g_tuned.find(key);
   if (it != g_tuned.end()) return it->second;
+  if (capturing(c.s)) return GemmChoice{};
   WgradArgs t = a;
   t.out = c.f(c.p->tune_scratch);
   const float th = time_launch(c.s, [&] { return launch_wgrad(t, c.s); });
@@ -591,8 +593,9 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
   const int n = p->n;
   // Weight gradients of layer l need only dY(l) and forward tensors: they go to
   // the side stream once the plan is tuned (timing runs stay serial so that
-  // per-kernel event times stay clean).
-  const bool conc = unet::g_concurrent && !p->timing && p->bwd_full > 0 && !capturing(s);
+  // per-kernel event times stay clean).  Under hipGraph capture the side stream
+  // joins the capture through the fork / join events.
+  const bool conc = unet::g_concurrent && !p->timing && p->bwd_full > 0;
   if (conc) CK(ensure_side_stream(p));
   Ctx cw{p, ws, conc ? p->side : s};
   const hipStream_t sw = cw.s;

@@ -57,8 +57,11 @@ class Plan:
                                                ws.data_ptr(), seg_begin, seg_end, _lib.stream_of(x.device)),
                    "unet_plan_backward")
 
+    timing_on = False
+
     def set_timing(self, enable):
         _lib.check(self.lib.unet_plan_set_timing(self.handle, int(bool(enable))), "unet_plan_set_timing")
+        self.timing_on = bool(enable)
 
     def timing(self):
         """{class: (ms, flops, bytes, launches)} accumulated since the last call."""

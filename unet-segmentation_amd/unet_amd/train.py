@@ -83,7 +83,7 @@ class FlatBuffers:
 
 class Trainer:
     def __init__(self, model, batch, height, width, lr=1e-4, momentum=0.99, process_group=None,
-                 overlap=True, precision="fp32", comm_dtype=None, broadcast_buffers=True):
+                 overlap=True, precision="fp32", comm_dtype=None, broadcast_buffers=True, graph=False):
         from .modules import UNet
         if not isinstance(model, UNet):
             raise TypeError("Trainer drives the MI355X UNet")
@@ -108,6 +108,11 @@ class Trainer:
         self.loss = torch.empty((), dtype=torch.float32, device=dev)
         self.acc = torch.empty(8, dtype=torch.float64, device=dev)
         self.first_step = True
+        self.use_graph = bool(graph)
+        self._graph = None
+        self._graph_key = None
+        self._eager_steps = 0
+        self.graph_error = None
         self.lib = _lib.load()
         buckets = [self.flat.range_for(*self.plan.segment_grads(s)) for s in range(N_SEGMENTS)]
         # gradient all-reduce dtype: bf16 for the bf16 GEMM plans (half the xGMI
@@ -168,13 +173,49 @@ class Trainer:
         self.first_step = False
 
     def step(self, x, targets, weights):
-        """One train.py step; returns the (device) loss without synchronising."""
+        """One train.py step; returns the (device) loss without synchronising.
+
+        Single-process training with ``graph=True`` replays the whole step
+        (forward, loss, backward, SGD: ~190 kernels on two streams) as one
+        hipGraph once the GEMM autotuner has settled (from the third step on,
+        for the same input tensors); any other call runs eagerly."""
+        if (self._graph is not None and not self.plan.timing_on and
+                self._graph_key == self._key(x, targets, weights)):
+            self._graph.replay()
+            return self.loss
         if self.broadcast_buffers and self.flat_buffers.flat is not None:
             torch.distributed.broadcast(self.flat_buffers.flat, 0, group=self.pg)
         loss = self.forward_loss(x, targets, weights)
         self.backward_and_reduce(x)
         self.optimizer_step()
+        self._eager_steps += 1
+        if (self.use_graph and self.pg is None and self._graph is None and self._eager_steps >= 2 and
+                not self.plan.timing_on):
+            self._capture(x, targets, weights)
         return loss
+
+    @staticmethod
+    def _key(x, targets, weights):
+        return tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride())) for t in (x, targets, weights))
+
+    def _capture(self, x, targets, weights):
+        """Capture one eager-equivalent step (first_step is already False, so
+        the captured SGD is the steady-state update).  A capture failure leaves
+        the trainer eager."""
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        try:
+            with torch.cuda.graph(g):
+                self.forward_loss(x, targets, weights)
+                self.backward_and_reduce(x)
+                self.optimizer_step()
+        except Exception as e:  # pragma: no cover - depends on the runtime
+            self.use_graph = False
+            self.graph_error = repr(e)
+            torch.cuda.synchronize()
+            return
+        # (capture launches nothing: the step that triggered it has already run eagerly)
+        self._graph, self._graph_key = g, self._key(x, targets, weights)
 
     def sync_buffers(self, src=0):
         """Broadcast rank-src BatchNorm running statistics now (``step`` does it
