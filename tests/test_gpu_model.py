@@ -110,7 +110,7 @@ def gemm_mode(request):
 @pytest.mark.parametrize("gemm_mode", ["heuristic", "split3", "split8", "tile11", "tile12", "tile13", "tile14",
                                        "tile12+split4", "tile14+split3", "tile3", "tile6", "tile51", "tile52",
                                        "tile53", "tile54", "tile51+split3", "heuristic+wgrad22",
-                                       "heuristic+wgrad23", "tile70", "tile71", "tile72", "heuristic+wgrad71",
+                                       "heuristic+wgrad23", "tile70", "tile71", "tile72", "tile74", "heuristic+wgrad71", "heuristic+wgrad74",
                                        "tile71+wgrad71"], indirect=True)
 def test_train_step_gemm_variants_vs_oracle(gemm_mode):
     """Built-in tiles, the LDS-DMA staged tiles (11-14), the fp32 halo-tiled 3x3

@@ -1120,7 +1120,7 @@ static TileInfo tile_info(int id) {
     case 66: return {512, 64, 288, 1};
     case 67: return {256, 64, 144, 2};
     // Winograd F(2x2, 3x3) (winograd.hip): no K split
-    case 70: case 71: return {256, 64, 9, 2};
+    case 70: case 71: case 74: return {256, 64, 9, 2};
     case 72: return {32, 32, 16, 1};
     // fp32 halo-tiled 3x3 (k_conv3_f32): bk = one 16-channel chunk x 9 taps
     case 51: return {256, 64, 144, 2};
@@ -1145,7 +1145,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   if (is_halo_tile(tile))  // 3x3 stride-1 gathers only (conv fwd / dgrad), K = 9 x Cg
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
-  if (tile == 70 || tile == 71) return wino_applies(a, tile == 70 ? 2 : 4);
+  if (tile == 70 || tile == 71 || tile == 74) return wino_applies(a, tile == 70 ? 2 : tile == 71 ? 4 : 6);
   if (tile == 72) return wino_fused_applies(a);
   if (is_dma_tile(tile)) {  // bf16-stored A sources, no split operands
     const int ch = tile_info(tile).bk / 9;
@@ -1247,6 +1247,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 63: case 65: case 66: case 67: return go_conv3_dma_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);
     case 71: return launch_wino(a, s, 4);
+    case 74: return launch_wino(a, s, 6);
     case 72: return launch_wino_fused(a, s);
     case 51: return go_halo32<8, 32, 64, 8, 1, 4>(a, s);
     case 52: return go_halo32<16, 16, 64, 8, 1, 4>(a, s);
@@ -1303,8 +1304,9 @@ hipError_t launch_igemm_v(const IgemmArgs& a0, hipStream_t s, GemmChoice c) {
   if (!igemm_args_ok(a0) || !igemm_tile_fits(a0, c.tile)) return hipErrorInvalidValue;
   IgemmArgs a = a0;
   const int nk = a.K / tile_info(c.tile).bk;
-  if ((c.tile == 70 || c.tile == 71) && c.split >= 100) a.wino_choice.tile = c.split - 100;  // point-GEMM tile
-  int ks = c.split < 1 || (c.tile >= 70 && c.tile <= 72) ? 1 : (c.split > nk ? nk : c.split);
+  const bool wino = c.tile >= 70 && c.tile <= 74;
+  if ((c.tile == 70 || c.tile == 71 || c.tile == 74) && c.split >= 100) a.wino_choice.tile = c.split - 100;  // point GEMMs
+  int ks = c.split < 1 || wino ? 1 : (c.split > nk ? nk : c.split);
   if (ks > 1) {  // no empty slice: ks = ceil(nk / ceil(nk / ks))
     const int per = (nk + ks - 1) / ks;
     ks = (nk + per - 1) / per;
@@ -1327,7 +1329,7 @@ static void wgrad_tile(int id, int& bm, int& bn) {
   if (id >= 10 && id < 15) { bm = tb[id - 10][0]; bn = tb[id - 10][1]; }
 }
 bool wgrad_tile_fits(const WgradArgs& a, int tile) {
-  if (tile == 71) return wino_wgrad_applies(a);
+  if (tile == 71 || tile == 74) return wino_wgrad_applies(a, tile == 71 ? 4 : 6);
   if (a.batch > 1 && (tile < 0 || tile > 4)) return false;  // batched: fp32 pixel-column tiles only
   if (tile == 20 || tile == 21) return wgrad3_fits(a);  // halo-tiled 3x3, all taps
   if (tile == 22 || tile == 23) return wgrad3_f32_fits(a);  // fp32 twin
@@ -1348,7 +1350,8 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     else if (a.No % 128 == 0) tile = 12;
     else tile = 13;
   } else if (tile < 0) {
-    if ((g_tune_wgrad == 22 || g_tune_wgrad == 23 || g_tune_wgrad == 71) && wgrad_tile_fits(a, g_tune_wgrad))
+    if ((g_tune_wgrad == 22 || g_tune_wgrad == 23 || g_tune_wgrad == 71 || g_tune_wgrad == 74) &&
+        wgrad_tile_fits(a, g_tune_wgrad))
       tile = g_tune_wgrad;  // forced fp32 halo tile (tests)
     else if (g_tune_wgrad == 1) tile = 4;  // force the small tile (A/B tests)
     else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 0;
@@ -1358,7 +1361,7 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     else tile = 4;
   }
   if (!wgrad_tile_fits(a, tile)) return hipErrorInvalidValue;
-  if (tile == 71) return launch_wino_wgrad(a, s, c.split);
+  if (tile == 71 || tile == 74) return launch_wino_wgrad(a, s, c.split, tile == 71 ? 4 : 6);
   if (tile == 20 || tile == 21) return go_wgrad3_bf16(a, s, tile, c.split > 0 ? c.split : 4);
   if (tile == 22) return go_wgrad3_f32<8, 16>(a, s, c.split > 0 ? c.split : 4);
   if (tile == 23) return go_wgrad3_f32<4, 32>(a, s, c.split > 0 ? c.split : 4);
@@ -1393,9 +1396,9 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad
 
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c) {
   int t = c.tile;
-  if (t < 0 && g_tune_igemm >= 70 && g_tune_igemm <= 72 && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;
-  if (t >= 70 && t <= 72) {
-    const int mt = t == 70 ? 2 : 4;
+  if (t < 0 && g_tune_igemm >= 70 && g_tune_igemm <= 74 && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;
+  if ((t >= 70 && t <= 72) || t == 74) {
+    const int mt = t == 70 ? 2 : t == 74 ? 6 : 4;
     const Gather& g = a.a;
     const double T = (double)g.nimg * ((g.Hg + mt - 1) / mt) * ((g.Wg + mt - 1) / mt);
     return 2.0 * (mt + 2) * (mt + 2) * T * g.Cg * a.N;
@@ -1404,10 +1407,13 @@ double igemm_exec_flops(const IgemmArgs& a, GemmChoice c) {
 }
 
 double wgrad_exec_flops(const WgradArgs& a, GemmChoice c) {
-  const bool wino = c.tile == 71 || (c.tile < 0 && !a.bf16 && g_tune_wgrad == 71 && wino_wgrad_applies(a));
-  if (wino) {
-    const double T = (double)a.gb.nimg * ((a.gb.Hg + 3) / 4) * ((a.gb.Wg + 3) / 4);
-    return 2.0 * 36 * T * a.Mo * a.gb.Cg;
+  int t = c.tile;
+  if (t < 0 && !a.bf16 && (g_tune_wgrad == 71 || g_tune_wgrad == 74) && wgrad_tile_fits(a, g_tune_wgrad))
+    t = g_tune_wgrad;
+  if (t == 71 || t == 74) {
+    const int mt = t == 71 ? 4 : 6;
+    const double T = (double)a.gb.nimg * ((a.gb.Hg + mt - 1) / mt) * ((a.gb.Wg + mt - 1) / mt);
+    return 2.0 * (mt + 2) * (mt + 2) * T * a.Mo * a.gb.Cg;
   }
   return 2.0 * a.P * (double)a.Mo * a.No;
 }

@@ -224,12 +224,12 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
-                36, 41, 42, 43, 44, 63, 65, 66, 67, 70, 71, 72}) {  // fits() filters by precision and gather
+                36, 41, 42, 43, 44, 63, 65, 66, 67, 70, 71, 72, 74}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t)) continue;
     v.push_back({t, 1});
-    if (t == 70 || t == 71)  // Winograd: no K split; the tile of its batched point GEMMs
+    if (t == 70 || t == 71 || t == 74)  // Winograd: no K split; the tile of its batched point GEMMs
       for (int inner : {1, 2, 3, 4, 6, 7, 8, 9}) v.push_back({t, 100 + inner});
-    if (t >= 70 && t <= 72) continue;
+    if (t >= 70) continue;
     const long long cnt = igemm_tile_count(a, t);
     const long long slots = (long long)igemm_tile_slots(t) * cus;
     if (cnt >= 4 * slots || a.N % 64 != 0) continue;  // enough workgroup rounds already
@@ -243,9 +243,9 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
 
 std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   std::vector<GemmChoice> v;
-  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 71}) {  // fits() filters by precision
+  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 71, 74}) {  // fits() filters by precision
     if (!wgrad_tile_fits(a, t)) continue;
-    if (t == 71) {  // Winograd: point-GEMM tile (k_wgrad 0, 3, 4) x workgroups per CU
+    if (t == 71 || t == 74) {  // Winograd: point-GEMM tile (k_wgrad 0-4) x workgroups per CU
       for (int inner : {0, 1, 2, 3, 4})
         for (int per_cu : {4, 8, 16}) v.push_back({t, per_cu + 100 * (inner + 1)});
       continue;

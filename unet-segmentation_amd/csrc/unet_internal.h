@@ -130,14 +130,14 @@ size_t wino_ws_bytes(long long T, int Cg, int N);
 size_t wino_ws_bytes_grid(int nimg, int H, int W, int Cg, int N);
 bool wino_applies(const IgemmArgs& a, int mt);           // mt = 2: F(2x2, 3x3), 4: F(4x4, 3x3)
 hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt);
-bool wino_wgrad_applies(const WgradArgs& a);
+bool wino_wgrad_applies(const WgradArgs& a, int mt);  // weight gradient, mt = 4 (wgrad tile 71) / 6 (74)
 bool wino_fused_applies(const IgemmArgs& a);  // tile 72: fused F(4x4, 3x3)
 hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s);
 // MFMA flops a GEMM launch executes with variant c (Winograd: 2 * points *
 // tiles * Cg * N; otherwise the direct 2 * M * N * K)
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c);
 double wgrad_exec_flops(const WgradArgs& a, GemmChoice c);
-hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu);
+hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int mt);
 // bf16 halo conv with LDS-DMA weights (conv3_dma.hip), tile ids 61-66
 bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch);
 hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);

@@ -22,6 +22,7 @@
 // Transform arithmetic is exact in the +-1, 1/2 coefficients; the fp32
 // rounding of the 16-term products differs from the direct sum's, at the same
 // order (tests/test_gpu_ops.py, tests/test_gpu_model.py force tile 70).
+#include <algorithm>
 #include <cstdlib>
 
 #include "gemm_common.h"
@@ -424,6 +425,217 @@ __global__ __launch_bounds__(256) void k_wino4_out(const float* __restrict__ m, 
   }
 }
 
+// ---------------------------------------------------------------------------
+// F(6x6, 3x3) (tile 74): 8x8 input patches, 64 points, 6x6 outputs -- 1.78
+// point products per output instead of 2.25 (F4) and 1.78 U / M values per
+// pixel instead of 2.25, at ~2.5x F4's fp32 rounding (interpolation points
+// 0, +-1, +-2, +-1/2, inf; Lavin & Gray 2016; the matrices were checked
+// against direct correlation to 3e-14 in fp64 before use).
+// ---------------------------------------------------------------------------
+template <int R, int C>
+__device__ __forceinline__ void mat_apply(const float (&m)[R][C], const float (&in)[C], float (&out)[R]) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    float acc = 0.f;
+    bool first = true;
+#pragma unroll
+    for (int c = 0; c < C; ++c) {
+      const float k = m[r][c];
+      if (k == 0.f) continue;  // compile-time after unrolling: zero terms vanish
+      const float t = k == 1.f ? in[c] : k == -1.f ? -in[c] : k * in[c];
+      acc = first ? t : acc + t;
+      first = false;
+    }
+    out[r] = acc;
+  }
+}
+
+__device__ __forceinline__ void bt8(const float (&d)[8], float (&r)[8]) {
+  constexpr float B[8][8] = {{1, 0, -5.25f, 0, 5.25f, 0, -1, 0},
+                             {0, 1, 1, -4.25f, -4.25f, 1, 1, 0},
+                             {0, -1, 1, 4.25f, -4.25f, -1, 1, 0},
+                             {0, 0.5f, 0.25f, -2.5f, -1.25f, 2, 1, 0},
+                             {0, -0.5f, 0.25f, 2.5f, -1.25f, -2, 1, 0},
+                             {0, 2, 4, -2.5f, -5, 0.5f, 1, 0},
+                             {0, -2, 4, 2.5f, -5, -0.5f, 1, 0},
+                             {0, -1, 0, 5.25f, 0, -5.25f, 0, 1}};
+  mat_apply(B, d, r);
+}
+__device__ __forceinline__ void g8(const float (&g)[3], float (&r)[8]) {
+  constexpr float G[8][3] = {{1, 0, 0},
+                             {-2.f / 9, -2.f / 9, -2.f / 9},
+                             {-2.f / 9, 2.f / 9, -2.f / 9},
+                             {1.f / 90, 1.f / 45, 2.f / 45},
+                             {1.f / 90, -1.f / 45, 2.f / 45},
+                             {32.f / 45, 16.f / 45, 8.f / 45},
+                             {32.f / 45, -16.f / 45, 8.f / 45},
+                             {0, 0, 1}};
+  mat_apply(G, g, r);
+}
+__device__ __forceinline__ void at6(const float (&m)[8], float (&o)[6]) {
+  constexpr float A[6][8] = {{1, 1, 1, 1, 1, 1, 1, 0},
+                             {0, 1, -1, 2, -2, 0.5f, -0.5f, 0},
+                             {0, 1, 1, 4, 4, 0.25f, 0.25f, 0},
+                             {0, 1, -1, 8, -8, 0.125f, -0.125f, 0},
+                             {0, 1, 1, 16, 16, 0.0625f, 0.0625f, 0},
+                             {0, 1, -1, 32, -32, 0.03125f, -0.03125f, 1}};
+  mat_apply(A, m, o);
+}
+
+__global__ void k_wino6_w(const float* __restrict__ b, int N, int Cg, float* __restrict__ v) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)N * Cg) return;
+  const int n = (int)(i / Cg), c = (int)(i - (long long)n * Cg);
+  float tg[8][3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float col[3] = {b[((size_t)n * 9 + 0 + k) * Cg + c], b[((size_t)n * 9 + 3 + k) * Cg + c],
+                    b[((size_t)n * 9 + 6 + k) * Cg + c]};
+    float r[8];
+    g8(col, r);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) tg[a][k] = r[a];
+  }
+  const size_t plane = (size_t)N * Cg, o = (size_t)n * Cg + c;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    float r[8];
+    g8(tg[a], r);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) v[(a * 8 + bb) * plane + o] = r[bb];
+  }
+}
+
+// Thread = (tile, channel); 8x8 patch with clamped unconditional loads
+__global__ __launch_bounds__(256) void k_wino6_in(Gather g, int Th, int Tw, long long T, float* __restrict__ u) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= T * g.Cg) return;
+  const long long t = i / g.Cg;
+  const int c = (int)(i - t * g.Cg);
+  const int tx = (int)(t % Tw);
+  const long long r = t / Tw;
+  const int ty = (int)(r % Th), n = (int)(r / Th);
+  const bool second = c >= g.c_split;
+  const Src s = pick_src(g, second);
+  const int cl = second ? c - g.c_split : c;
+  float sc = 1.f, sh = 0.f;
+  if (s.scale) {
+    sc = s.scale[cl];
+    sh = s.shift[cl];
+  }
+  const int vr = min(8, g.Hg + 2 - 6 * ty), vc = min(8, g.Wg + 2 - 6 * tx);
+  const char* base = reinterpret_cast<const char*>(s.ptr) +
+                     (((size_t)(n * s.H + 6 * ty + s.oy) * s.W + 6 * tx + s.ox) * s.C + cl) * 4;
+  const unsigned rs = (unsigned)s.W * s.C * 4u, cs = (unsigned)s.C * 4u;
+  float e[8][8];
+#pragma unroll
+  for (int xx = 0; xx < 8; ++xx) {
+    float d[8];
+#pragma unroll
+    for (int yy = 0; yy < 8; ++yy) {
+      const bool in = yy < vr && xx < vc;
+      float v = *reinterpret_cast<const float*>(base + (in ? yy * rs + xx * cs : 0u));
+      if (s.scale) v = fmaxf(fmaf(v, sc, sh), 0.f);
+      d[yy] = in ? v : 0.f;
+    }
+    float rr[8];
+    bt8(d, rr);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) e[a][xx] = rr[a];
+  }
+  const size_t plane = (size_t)T * g.Cg, o = (size_t)t * g.Cg + c;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    float rr[8];
+    bt8(e[a], rr);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) u[(a * 8 + bb) * plane + o] = rr[bb];
+  }
+}
+
+// Block = 64 channels x 4 tile lanes; grid-stride over tiles (k_wino4_out's epilogue)
+__global__ __launch_bounds__(256) void k_wino6_out(const float* __restrict__ m, long long T, int Th, int Tw, int N,
+                                                   Gather g, Epilogue e) {
+  const int col = blockIdx.y * 64 + (int)(threadIdx.x & 63);
+  const int tl = threadIdx.x >> 6;
+  const bool active = col < N;
+  const bool second = col >= e.n_split;
+  float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
+  const int dC = second ? e.d[1].C : e.d[0].C;
+  const int dcol = second ? col - e.n_split : col;
+  const bool bwd_mask = e.yref != nullptr && !second;
+  float bias = 0.f, bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
+  if (active && e.bias) bias = e.bias[col];
+  if (active && bwd_mask) { bsc = e.bn_scale[col]; bsh = e.bn_shift[col]; bmu = e.bn_mean[col]; bis = e.bn_invstd[col]; }
+  float s1 = 0.f, s2 = 0.f;
+  const size_t plane = (size_t)T * N;
+  if (active) {
+    for (long long t = blockIdx.x * 4ll + tl; t < T; t += (long long)gridDim.x * 4) {
+      float w[6][8];
+#pragma unroll
+      for (int xx = 0; xx < 8; ++xx) {
+        float q[8];
+#pragma unroll
+        for (int yy = 0; yy < 8; ++yy) q[yy] = m[(yy * 8 + xx) * plane + (size_t)t * N + col];
+        float o[6];
+        at6(q, o);
+#pragma unroll
+        for (int a = 0; a < 6; ++a) w[a][xx] = o[a];
+      }
+      const int tx = (int)(t % Tw);
+      const long long r = t / Tw;
+      const int ty = (int)(r % Th), n = (int)(r / Th);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) {
+        float o[6];
+        at6(w[a], o);
+        const int y = 6 * ty + a;
+        if (y >= g.Hg) continue;
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) {
+          const int x = 6 * tx + bb;
+          if (x >= g.Wg) continue;
+          float v = o[bb] + bias;
+          const size_t idx = ((size_t)(n * g.Hg + y) * g.Wg + x) * dC + dcol;
+          if (bwd_mask) {
+            const float yv = e.yref[idx];
+            v = fmaf(yv, bsc, bsh) > 0.f ? v : 0.f;
+            s1 += v;
+            s2 += v * ((yv - bmu) * bis);
+          } else if (e.stats) {
+            s1 += v;
+            s2 += v * v;
+          } else if (second && e.colsum1) {
+            s1 += v;
+          }
+          dptr[idx] = v;
+        }
+      }
+    }
+  }
+  const bool want = e.stats || e.yref || e.colsum1;
+  if (!want) return;
+  __shared__ float red[2][256];
+  red[0][threadIdx.x] = s1;
+  red[1][threadIdx.x] = s2;
+  __syncthreads();
+  if (threadIdx.x < 64 && active) {
+    const float a = red[0][threadIdx.x] + red[0][threadIdx.x + 64] + red[0][threadIdx.x + 128] + red[0][threadIdx.x + 192];
+    const float b2 = red[1][threadIdx.x] + red[1][threadIdx.x + 64] + red[1][threadIdx.x + 128] + red[1][threadIdx.x + 192];
+    const int grp = blockIdx.x % kStatGroups;
+    const int nsplit = e.n_split < N ? e.n_split : N;
+    if (col < nsplit) {
+      double* st = e.yref ? e.bstats : e.stats;
+      if (st) {
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)a);
+        atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)b2);
+      }
+    } else if (e.colsum1) {
+      atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (col - nsplit), (double)a);
+    }
+  }
+}
+
 // workspace of the Winograd path for one GEMM (U, M, V; 256-B aligned pieces):
 // P points over T output tiles
 static size_t wino_bytes(int P, long long T, int Cg, int N) {
@@ -435,8 +647,9 @@ size_t wino_ws_bytes(long long T, int Cg, int N) { return wino_bytes(16, T, Cg, 
 size_t wino_ws_bytes_grid(int nimg, int H, int W, int Cg, int N) {
   const long long t2 = (long long)nimg * ((H + 1) / 2) * ((W + 1) / 2);
   const long long t4 = (long long)nimg * ((H + 3) / 4) * ((W + 3) / 4);
-  const size_t a = wino_bytes(16, t2, Cg, N), b = wino_bytes(36, t4, Cg, N);
-  return a > b ? a : b;
+  const long long t6 = (long long)nimg * ((H + 5) / 6) * ((W + 5) / 6);
+  const size_t a = wino_bytes(16, t2, Cg, N), b = wino_bytes(36, t4, Cg, N), c = wino_bytes(64, t6, Cg, N);
+  return std::max(a, std::max(b, c));
 }
 
 bool wino_applies(const IgemmArgs& a, int mt) {
@@ -470,9 +683,13 @@ hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt) {
     hipLaunchKernelGGL(k_wino_w, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
     const long long ni = T * (g.Cg / 4);
     hipLaunchKernelGGL(k_wino_in, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, s, g, Th, Tw, T, U);
-  } else {
+  } else if (mt == 4) {
     hipLaunchKernelGGL(k_wino4_w, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
     launch_wino4_in(g, Th, Tw, T, U, s);
+  } else {
+    hipLaunchKernelGGL(k_wino6_w, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
+    const long long ni = T * g.Cg;
+    hipLaunchKernelGGL(k_wino6_in, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, s, g, Th, Tw, T, U);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -518,7 +735,8 @@ hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt) {
     long long gx = (T + 15) / 16;  // 4 tile lanes x ~4 tiles per thread
     if (gx > 65535) gx = 65535;
     dim3 grid((unsigned)gx, (unsigned)((a.N + 63) / 64));
-    hipLaunchKernelGGL(k_wino4_out, grid, dim3(256), 0, s, Mm, T, Th, Tw, a.N, g, a.e);
+    if (mt == 4) hipLaunchKernelGGL(k_wino4_out, grid, dim3(256), 0, s, Mm, T, Th, Tw, a.N, g, a.e);
+    else hipLaunchKernelGGL(k_wino6_out, grid, dim3(256), 0, s, Mm, T, Th, Tw, a.N, g, a.e);
   }
   return hipGetLastError();
 }
@@ -962,11 +1180,92 @@ __global__ __launch_bounds__(256) void k_wino4_wout(const float* __restrict__ mw
   }
 }
 
-static long long wino_wgrad_tiles(const WgradArgs& a) {
-  return (long long)a.gb.nimg * ((a.gb.Hg + 3) / 4) * ((a.gb.Wg + 3) / 4);
+// F(6x6) weight-gradient transforms (wgrad tile 74): Vd = A dY A^T with
+// A = (A^T of at6)^T (8x6), dW = G^T Mw G with G of g8 (8x3)
+__device__ __forceinline__ void a8(const float (&y)[6], float (&r)[8]) {
+  constexpr float A[8][6] = {{1, 0, 0, 0, 0, 0},
+                             {1, 1, 1, 1, 1, 1},
+                             {1, -1, 1, -1, 1, -1},
+                             {1, 2, 4, 8, 16, 32},
+                             {1, -2, 4, -8, 16, -32},
+                             {1, 0.5f, 0.25f, 0.125f, 0.0625f, 0.03125f},
+                             {1, -0.5f, 0.25f, -0.125f, 0.0625f, -0.03125f},
+                             {0, 0, 0, 0, 0, 1}};
+  mat_apply(A, y, r);
+}
+__device__ __forceinline__ void gt8(const float (&m)[8], float (&r)[3]) {
+  constexpr float GT[3][8] = {{1, -2.f / 9, -2.f / 9, 1.f / 90, 1.f / 90, 32.f / 45, 32.f / 45, 0},
+                              {0, -2.f / 9, 2.f / 9, 1.f / 45, -1.f / 45, 16.f / 45, -16.f / 45, 0},
+                              {0, -2.f / 9, -2.f / 9, 2.f / 45, 2.f / 45, 8.f / 45, 8.f / 45, 1}};
+  mat_apply(GT, m, r);
 }
 
-bool wino_wgrad_applies(const WgradArgs& a) {
+__global__ __launch_bounds__(256) void k_wino6_dy(Src dy, int Hg, int Wg, int Th, int Tw, long long T, int Co,
+                                                  float* __restrict__ vd) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= T * Co) return;
+  const long long t = i / Co;
+  const int c = (int)(i - t * Co);
+  const int tx = (int)(t % Tw);
+  const long long r = t / Tw;
+  const int ty = (int)(r % Th), n = (int)(r / Th);
+  float e[8][6];
+#pragma unroll
+  for (int xx = 0; xx < 6; ++xx) {
+    float d[6];
+#pragma unroll
+    for (int yy = 0; yy < 6; ++yy) {
+      const int y = 6 * ty + yy, x = 6 * tx + xx;
+      const bool in = y < Hg && x < Wg;
+      const float v = dy.ptr[((size_t)(n * dy.H + (in ? y : 0) + dy.oy) * dy.W + (in ? x : 0) + dy.ox) * dy.C + c];
+      d[yy] = in ? v : 0.f;
+    }
+    float rr[8];
+    a8(d, rr);
+#pragma unroll
+    for (int a = 0; a < 8; ++a) e[a][xx] = rr[a];
+  }
+  const size_t plane = (size_t)T * Co, o = (size_t)t * Co + c;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    float rr[8];
+    a8(e[a], rr);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) vd[(a * 8 + bb) * plane + o] = rr[bb];
+  }
+}
+
+__global__ __launch_bounds__(256) void k_wino6_wout(const float* __restrict__ mw, int Co, int Ci,
+                                                    float* __restrict__ out) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)Co * Ci) return;
+  const int co = (int)(i / Ci), ci = (int)(i - (long long)co * Ci);
+  const size_t plane = (size_t)Co * Ci;
+  float w[3][8];
+#pragma unroll
+  for (int bb = 0; bb < 8; ++bb) {
+    float m[8];
+#pragma unroll
+    for (int a = 0; a < 8; ++a) m[a] = mw[(a * 8 + bb) * plane + i];
+    float r[3];
+    gt8(m, r);
+#pragma unroll
+    for (int k = 0; k < 3; ++k) w[k][bb] = r[k];
+  }
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float r[3];
+    gt8(w[k], r);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) out[((size_t)co * 9 + k * 3 + kx) * Ci + ci] = r[kx];
+  }
+}
+
+static long long wino_wgrad_tiles(const WgradArgs& a, int mt) {
+  return (long long)a.gb.nimg * ((a.gb.Hg + mt - 1) / mt) * ((a.gb.Wg + mt - 1) / mt);
+}
+
+bool wino_wgrad_applies(const WgradArgs& a, int mt) {
   const Gather& ga = a.ga;
   const Gather& gb = a.gb;
   if (a.bf16 || a.batch != 1 || a.wino_ws == nullptr) return false;
@@ -975,35 +1274,44 @@ bool wino_wgrad_applies(const WgradArgs& a) {
   if (gb.taps_h != 3 || gb.taps_w != 3 || gb.stride != 1 || gb.s[0].h16 || gb.s[1].h16) return false;
   if (ga.Hg != gb.Hg || ga.Wg != gb.Wg || ga.nimg != gb.nimg || a.P != gb.nimg * gb.Hg * gb.Wg) return false;
   if (a.Mo != ga.Cg || a.No != 9 * gb.Cg || a.Mo % 64 != 0 || gb.Cg % 64 != 0 || gb.c_split % 4 != 0) return false;
-  return wino_bytes(36, wino_wgrad_tiles(a), gb.Cg, a.Mo) <= a.wino_ws_bytes;
+  return wino_bytes((mt + 2) * (mt + 2), wino_wgrad_tiles(a, mt), gb.Cg, a.Mo) <= a.wino_ws_bytes;
 }
 
-// per_cu: workgroups per CU of the point GEMMs' pixel split, + 100 * (1 + k_wgrad
-// tile id) to force their tile (autotuner candidates)
-hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu) {
+// mt = 4 (wgrad tile 71) or 6 (tile 74).  per_cu: workgroups per CU of the point
+// GEMMs' pixel split, + 100 * (1 + k_wgrad tile id) to force their tile
+// (autotuner candidates)
+hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int mt) {
   const int forced = per_cu >= 100 ? per_cu / 100 - 1 : -1;
   per_cu %= 100;
   if (per_cu <= 0) per_cu = 8;
-  if (!wino_wgrad_applies(a)) return hipErrorInvalidValue;
+  if ((mt != 4 && mt != 6) || !wino_wgrad_applies(a, mt)) return hipErrorInvalidValue;
   const Gather& gb = a.gb;
-  const int Th = (gb.Hg + 3) / 4, Tw = (gb.Wg + 3) / 4;
-  const long long T = wino_wgrad_tiles(a);
+  const int P = (mt + 2) * (mt + 2);
+  const int Th = (gb.Hg + mt - 1) / mt, Tw = (gb.Wg + mt - 1) / mt;
+  const long long T = wino_wgrad_tiles(a, mt);
   const int Ci = gb.Cg, Co = a.Mo;
-  if (36 * T > 0x7fffffffLL) return hipErrorInvalidValue;
+  if (P * T > 0x7fffffffLL) return hipErrorInvalidValue;
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   char* w = reinterpret_cast<char*>(a.wino_ws);
   float* U = reinterpret_cast<float*>(w);
-  float* Vd = reinterpret_cast<float*>(w + al((size_t)36 * T * Ci * 4));
-  float* Mw = reinterpret_cast<float*>(w + al((size_t)36 * T * Ci * 4) + al((size_t)36 * T * Co * 4));
+  float* Vd = reinterpret_cast<float*>(w + al((size_t)P * T * Ci * 4));
+  float* Mw = reinterpret_cast<float*>(w + al((size_t)P * T * Ci * 4) + al((size_t)P * T * Co * 4));
   const long long nd = T * Co;
-  launch_wino4_in(gb, Th, Tw, T, U, s);
-  hipLaunchKernelGGL(k_wino4_dy, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg, gb.Wg, Th,
-                     Tw, T, Co, Vd);
-  hipError_t e = hipMemsetAsync(Mw, 0, (size_t)36 * Co * Ci * 4, s);
+  if (mt == 4) {
+    launch_wino4_in(gb, Th, Tw, T, U, s);
+    hipLaunchKernelGGL(k_wino4_dy, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg, gb.Wg, Th,
+                       Tw, T, Co, Vd);
+  } else {
+    const long long ni = T * Ci;
+    hipLaunchKernelGGL(k_wino6_in, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, s, gb, Th, Tw, T, U);
+    hipLaunchKernelGGL(k_wino6_dy, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg, gb.Wg, Th,
+                       Tw, T, Co, Vd);
+  }
+  hipError_t e = hipMemsetAsync(Mw, 0, (size_t)P * Co * Ci * 4, s);
   if (e != hipSuccess) return e;
   if ((e = hipGetLastError()) != hipSuccess) return e;
   {
-    // the 36 point GEMMs Mw[p] = Vd[p]^T U[p] as one batched k_wgrad launch
+    // the P point GEMMs Mw[p] = Vd[p]^T U[p] as one batched k_wgrad launch
     WgradArgs q;
     Src v;
     v.ptr = Vd;
@@ -1027,7 +1335,7 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu) {
     q.No = Ci;
     q.P = (int)T;
     q.out = Mw;
-    q.batch = 36;
+    q.batch = P;
     q.batch_a = T * Co;
     q.batch_b = T * Ci;
     q.batch_out = (long long)Co * Ci;
@@ -1036,7 +1344,10 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu) {
     if ((e = launch_wgrad_v(q, s, GemmChoice{tile, per_cu})) != hipSuccess) return e;
   }
   const long long no = (long long)Co * Ci;
-  hipLaunchKernelGGL(k_wino4_wout, dim3((unsigned)((no + 255) / 256)), dim3(256), 0, s, Mw, Co, Ci, a.out);
+  if (mt == 4)
+    hipLaunchKernelGGL(k_wino4_wout, dim3((unsigned)((no + 255) / 256)), dim3(256), 0, s, Mw, Co, Ci, a.out);
+  else
+    hipLaunchKernelGGL(k_wino6_wout, dim3((unsigned)((no + 255) / 256)), dim3(256), 0, s, Mw, Co, Ci, a.out);
   return hipGetLastError();
 }
 
