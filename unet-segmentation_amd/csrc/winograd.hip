@@ -506,51 +506,76 @@ __global__ void k_wino6_w(const float* __restrict__ b, int N, int Cg, float* __r
   }
 }
 
-// Thread = (tile, channel); 8x8 patch with clamped unconditional loads
+// Thread = (tile, V channels); 8x8 patch with clamped unconditional loads
+template <int V>
 __global__ __launch_bounds__(256) void k_wino6_in(Gather g, int Th, int Tw, long long T, float* __restrict__ u) {
+  typedef float vec __attribute__((ext_vector_type(V)));
+  const int CV = g.Cg / V;
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (i >= T * g.Cg) return;
-  const long long t = i / g.Cg;
-  const int c = (int)(i - t * g.Cg);
+  if (i >= T * CV) return;
+  const long long t = i / CV;
+  const int c = (int)(i - t * CV) * V;
   const int tx = (int)(t % Tw);
   const long long r = t / Tw;
   const int ty = (int)(r % Th), n = (int)(r / Th);
   const bool second = c >= g.c_split;
   const Src s = pick_src(g, second);
   const int cl = second ? c - g.c_split : c;
-  float sc = 1.f, sh = 0.f;
+  vec sc, sh;
   if (s.scale) {
-    sc = s.scale[cl];
-    sh = s.shift[cl];
+    sc = *reinterpret_cast<const vec*>(s.scale + cl);
+    sh = *reinterpret_cast<const vec*>(s.shift + cl);
   }
   const int vr = min(8, g.Hg + 2 - 6 * ty), vc = min(8, g.Wg + 2 - 6 * tx);
   const char* base = reinterpret_cast<const char*>(s.ptr) +
                      (((size_t)(n * s.H + 6 * ty + s.oy) * s.W + 6 * tx + s.ox) * s.C + cl) * 4;
   const unsigned rs = (unsigned)s.W * s.C * 4u, cs = (unsigned)s.C * 4u;
-  float e[8][8];
+  float e[V][8][8];
 #pragma unroll
   for (int xx = 0; xx < 8; ++xx) {
-    float d[8];
+    float d[V][8];
 #pragma unroll
     for (int yy = 0; yy < 8; ++yy) {
       const bool in = yy < vr && xx < vc;
-      float v = *reinterpret_cast<const float*>(base + (in ? yy * rs + xx * cs : 0u));
-      if (s.scale) v = fmaxf(fmaf(v, sc, sh), 0.f);
-      d[yy] = in ? v : 0.f;
-    }
-    float rr[8];
-    bt8(d, rr);
+      vec v = *reinterpret_cast<const vec*>(base + (in ? yy * rs + xx * cs : 0u));
 #pragma unroll
-    for (int a = 0; a < 8; ++a) e[a][xx] = rr[a];
+      for (int k = 0; k < V; ++k) {
+        float x = v[k];
+        if (s.scale) x = fmaxf(fmaf(x, sc[k], sh[k]), 0.f);
+        d[k][yy] = in ? x : 0.f;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float rr[8];
+      bt8(d[k], rr);
+#pragma unroll
+      for (int a = 0; a < 8; ++a) e[k][a][xx] = rr[a];
+    }
   }
   const size_t plane = (size_t)T * g.Cg, o = (size_t)t * g.Cg + c;
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
-    float rr[8];
-    bt8(e[a], rr);
+    float rr[V][8];
 #pragma unroll
-    for (int bb = 0; bb < 8; ++bb) u[(a * 8 + bb) * plane + o] = rr[bb];
+    for (int k = 0; k < V; ++k) bt8(e[k][a], rr[k]);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) {
+      vec o4;
+#pragma unroll
+      for (int k = 0; k < V; ++k) o4[k] = rr[k][bb];
+      *reinterpret_cast<vec*>(u + (a * 8 + bb) * plane + o) = o4;
+    }
   }
+}
+
+static void launch_wino6_in(const Gather& g, int Th, int Tw, long long T, float* U, hipStream_t s) {
+  int V = wino4_in_vec();
+  while (V > 1 && (g.Cg % V || g.c_split % V)) V >>= 1;
+  const long long n = T * (g.Cg / V);
+  const dim3 grid((unsigned)((n + 255) / 256));
+  if (V >= 2) hipLaunchKernelGGL(k_wino6_in<2>, grid, dim3(256), 0, s, g, Th, Tw, T, U);
+  else hipLaunchKernelGGL(k_wino6_in<1>, grid, dim3(256), 0, s, g, Th, Tw, T, U);
 }
 
 // Block = 64 channels x 4 tile lanes; grid-stride over tiles (k_wino4_out's epilogue)
@@ -688,8 +713,7 @@ hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt) {
     launch_wino4_in(g, Th, Tw, T, U, s);
   } else {
     hipLaunchKernelGGL(k_wino6_w, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
-    const long long ni = T * g.Cg;
-    hipLaunchKernelGGL(k_wino6_in, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, s, g, Th, Tw, T, U);
+    launch_wino6_in(g, Th, Tw, T, U, s);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
@@ -1302,8 +1326,7 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
     hipLaunchKernelGGL(k_wino4_dy, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg, gb.Wg, Th,
                        Tw, T, Co, Vd);
   } else {
-    const long long ni = T * Ci;
-    hipLaunchKernelGGL(k_wino6_in, dim3((unsigned)((ni + 255) / 256)), dim3(256), 0, s, gb, Th, Tw, T, U);
+    launch_wino6_in(gb, Th, Tw, T, U, s);
     hipLaunchKernelGGL(k_wino6_dy, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg, gb.Wg, Th,
                        Tw, T, Co, Vd);
   }
