@@ -312,6 +312,8 @@ __global__ __launch_bounds__(256) void k_wino4_in(Gather g, int Th, int Tw, long
     e[5][xx] = 4.f * d[1] - 5.f * d[3] + d[5];
   }
   const size_t plane = (size_t)T * g.Cg, o = (size_t)t * g.Cg + c;
+  char* ub = reinterpret_cast<char*>(u + o);
+  const unsigned pbytes = (unsigned)(plane * 4);
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
     const vec* d = e[a];
@@ -323,7 +325,7 @@ __global__ __launch_bounds__(256) void k_wino4_in(Gather g, int Th, int Tw, long
     rr[4] = 2.f * (d[1] - d[3]) - d[2] + d[4];
     rr[5] = 4.f * d[1] - 5.f * d[3] + d[5];
 #pragma unroll
-    for (int bb = 0; bb < 6; ++bb) *reinterpret_cast<vec*>(u + (a * 6 + bb) * plane + o) = rr[bb];
+    for (int bb = 0; bb < 6; ++bb) *reinterpret_cast<vec*>(ub + (unsigned)(a * 6 + bb) * pbytes) = rr[bb];
   }
 }
 
@@ -359,13 +361,16 @@ __global__ __launch_bounds__(256) void k_wino4_out(const float* __restrict__ m, 
   float s1 = 0.f, s2 = 0.f;
   const size_t plane = (size_t)T * N;
   if (active) {
+    const unsigned pb = (unsigned)(plane * 4);  // bytes per point plane (36 planes < 4 GB: wino_applies)
     for (long long t = blockIdx.x * 4ll + tl; t < T; t += (long long)gridDim.x * 4) {
+      const char* mb = reinterpret_cast<const char*>(m + (size_t)t * N + col);
       float w[4][6];  // A^T q (rows), per column
 #pragma unroll
       for (int xx = 0; xx < 6; ++xx) {
         float q[6];
 #pragma unroll
-        for (int yy = 0; yy < 6; ++yy) q[yy] = m[(yy * 6 + xx) * plane + (size_t)t * N + col];
+        for (int yy = 0; yy < 6; ++yy)
+          q[yy] = *reinterpret_cast<const float*>(mb + (unsigned)(yy * 6 + xx) * pb);  // 32-bit offsets
         float o[4];
         at4(q, o);
 #pragma unroll
@@ -554,6 +559,8 @@ __global__ __launch_bounds__(256) void k_wino6_in(Gather g, int Th, int Tw, long
     }
   }
   const size_t plane = (size_t)T * g.Cg, o = (size_t)t * g.Cg + c;
+  char* ub = reinterpret_cast<char*>(u + o);
+  const unsigned pbytes = (unsigned)(plane * 4);
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
     float rr[V][8];
@@ -564,7 +571,7 @@ __global__ __launch_bounds__(256) void k_wino6_in(Gather g, int Th, int Tw, long
       vec o4;
 #pragma unroll
       for (int k = 0; k < V; ++k) o4[k] = rr[k][bb];
-      *reinterpret_cast<vec*>(u + (a * 8 + bb) * plane + o) = o4;
+      *reinterpret_cast<vec*>(ub + (unsigned)(a * 8 + bb) * pbytes) = o4;
     }
   }
 }
@@ -595,13 +602,16 @@ __global__ __launch_bounds__(256) void k_wino6_out(const float* __restrict__ m, 
   float s1 = 0.f, s2 = 0.f;
   const size_t plane = (size_t)T * N;
   if (active) {
+    const unsigned pb = (unsigned)(plane * 4);  // bytes per point plane (64 planes < 4 GB: wino_applies)
     for (long long t = blockIdx.x * 4ll + tl; t < T; t += (long long)gridDim.x * 4) {
+      const char* mb = reinterpret_cast<const char*>(m + (size_t)t * N + col);
       float w[6][8];
 #pragma unroll
       for (int xx = 0; xx < 8; ++xx) {
         float q[8];
 #pragma unroll
-        for (int yy = 0; yy < 8; ++yy) q[yy] = m[(yy * 8 + xx) * plane + (size_t)t * N + col];
+        for (int yy = 0; yy < 8; ++yy)
+          q[yy] = *reinterpret_cast<const float*>(mb + (unsigned)(yy * 8 + xx) * pb);  // 32-bit offsets
         float o[6];
         at6(q, o);
 #pragma unroll
@@ -689,6 +699,8 @@ bool wino_applies(const IgemmArgs& a, int mt) {
   }
   if (a.e.yref_h16 || a.e.n_split % 4) return false;
   const long long T = (long long)g.nimg * ((g.Hg + mt - 1) / mt) * ((g.Wg + mt - 1) / mt);
+  // the transforms address U / M with 32-bit byte offsets
+  if ((long long)(mt + 2) * (mt + 2) * T * std::max(g.Cg, a.N) * 4 >= (1ll << 32)) return false;
   return a.wino_ws != nullptr && wino_bytes((mt + 2) * (mt + 2), T, g.Cg, a.N) <= a.wino_ws_bytes;
 }
 
@@ -1298,7 +1310,9 @@ bool wino_wgrad_applies(const WgradArgs& a, int mt) {
   if (gb.taps_h != 3 || gb.taps_w != 3 || gb.stride != 1 || gb.s[0].h16 || gb.s[1].h16) return false;
   if (ga.Hg != gb.Hg || ga.Wg != gb.Wg || ga.nimg != gb.nimg || a.P != gb.nimg * gb.Hg * gb.Wg) return false;
   if (a.Mo != ga.Cg || a.No != 9 * gb.Cg || a.Mo % 64 != 0 || gb.Cg % 64 != 0 || gb.c_split % 4 != 0) return false;
-  return wino_bytes((mt + 2) * (mt + 2), wino_wgrad_tiles(a, mt), gb.Cg, a.Mo) <= a.wino_ws_bytes;
+  const long long T = wino_wgrad_tiles(a, mt);
+  if ((long long)(mt + 2) * (mt + 2) * T * std::max(gb.Cg, a.Mo) * 4 >= (1ll << 32)) return false;  // 32-bit offsets
+  return wino_bytes((mt + 2) * (mt + 2), T, gb.Cg, a.Mo) <= a.wino_ws_bytes;
 }
 
 // mt = 4 (wgrad tile 71) or 6 (tile 74).  per_cu: workgroups per CU of the point
