@@ -126,7 +126,7 @@ int unet_plan_timing(const unet_plan* p, double* ms, double* flops, double* byte
 /* MFMA flops the chosen GEMM variants executed per class over the intervals the
  * last unet_plan_timing() call reported: equal to its `flops` (the direct
  * convolution's 2*M*N*K) except where a Winograd variant ran (igemm tiles
- * 70/71, wgrad tile 71: 2 * points * tiles * Cin * Cout). */
+ * 70-72/74, wgrad tiles 71/74: 2 * points * tiles * Cin * Cout). */
 int unet_plan_timing_mfma_flops(const unet_plan* p, double* mfma_flops);
 
 /* ------------------------------------------------------------------------
@@ -266,20 +266,21 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  fastest per shape; 0 = built-in heuristic only.
  *  "igemm_variant" heuristic override for A/B measurements (-1 = off, 1..9 =
  *                  forced tile shape; 21-26, 31-36, 41-44 bf16 tiles, 63,
- *                  65-67 bf16 halo tiles with LDS-DMA weights; 70-72 fp32
- *                  Winograd: F(2x2,3x3), F(4x4,3x3), fused F(4x4,3x3), plan
- *                  GEMMs only -- they need the plan's scratch); "wgrad_variant"
+ *                  65-67 bf16 halo tiles with LDS-DMA weights; 70-72, 74 fp32
+ *                  Winograd: F(2x2,3x3), F(4x4,3x3), fused F(4x4,3x3),
+ *                  F(6x6,3x3), plan GEMMs only -- they need the plan's
+ *                  scratch); "wgrad_variant"
  *                  (-1 = off, 1 = 64x64 tile, 2..9 = workgroups per CU for the
  *                  pixel split; bf16 GEMMs: 10-14, 20-21 = forced bf16 tile;
- *                  22-23 fp32 halo tiles; 71 = Winograd F(4x4,3x3) weight
- *                  gradient, plan GEMMs only);
+ *                  22-23 fp32 halo tiles; 71 / 74 = Winograd F(4x4,3x3) /
+ *                  F(6x6,3x3) weight gradient, plan GEMMs only);
  *  "concurrent"    1 (default, or env UNET_CONCURRENT) = a plan's backward
  *                  runs the weight-gradient GEMMs on a side stream beside the
  *                  dX chain (joined before the call returns); 0 = one stream.
  *  "force_split"   k > 1: every plan igemm runs split-K k (tests), 0 = off.
  *  "force_tile"    id > 0: every plan igemm whose shape admits tile id runs
  *                  it (tests; 1-4, 6-9 register-staged, 11-14 LDS-DMA, 51-54
- *                  fp32 halo, 70-72 fp32 Winograd, 21-26 / 31-36 / 63-67
+ *                  fp32 halo, 70-72 / 74 fp32 Winograd, 21-26 / 31-36 / 63-67
  *                  bf16 operands -- only in UNET_PREC_BF16 / _BF16X3 plans).
  *  "op_precision"  UNET_PREC_* of the per-op GEMM entry points below
  *                  (unet_conv3x3_*, unet_convT2_*); default fp32.
