@@ -296,6 +296,13 @@ int unet_set_tuning(const char* key, int value);
 size_t unet_tuning_report(char* buf, size_t len);
 /* Forget every tuned choice (the next plan run re-tunes). */
 int unet_tuning_reset(void);
+/* Tuning database (cf. MIOpen's perf-db): unet_tuning_save writes every tuned
+ * choice as "key<TAB>tile<TAB>split" lines (returns the count or -errno);
+ * unet_tuning_load merges such a file, overriding equal keys (returns the
+ * entries read or -errno).  With env UNET_TUNE_DB=<path> the first tuner lookup
+ * loads <path> and each newly tuned shape is appended to it. */
+int unet_tuning_save(const char* path);
+int unet_tuning_load(const char* path);
 
 /* ------------------------------------------------------------------------
  * Per-op entry points (used by the op-level parity tests and by tools).

@@ -41,6 +41,34 @@ def test_plan_output_size_matches_reference_rule(h, out):
     assert p.workspace_bytes > 0
 
 
+def test_tuning_db_roundtrip(tmp_path):
+    """unet_tuning_load / _save (host-only: no GPU call): a database file is
+    merged into the tuner's cache, reported, written back line for line."""
+    L = _lib()
+    lib = L.load()
+    src = tmp_path / "tune.db"
+    entries = {"igemm_bf16 M=8 N=64 K=576 Cg=64 taps=3x3 s=1 grid=4x4 epi=18": (31, 1),
+               "wgrad Mo=64 No=576 P=16 Cg=64 taps=3x3 s=1 grid=4x4": (74, 504)}
+    src.write_text("".join(f"{k}\t{t}\t{s}\n" for k, (t, s) in entries.items()) + "malformed line\n")
+    lib.unet_tuning_reset()
+    try:
+        assert lib.unet_tuning_load(str(src).encode()) == 2
+        n = lib.unet_tuning_report(None, 0)
+        buf = ctypes.create_string_buffer(n)
+        lib.unet_tuning_report(buf, n)
+        assert buf.value.decode().count("tuning db") == 2, buf.value
+        out = tmp_path / "out.db"
+        assert lib.unet_tuning_save(str(out).encode()) == 2
+        got = {}
+        for line in out.read_text().splitlines():
+            k, t, s = line.split("\t")
+            got[k] = (int(t), int(s))
+        assert got == entries
+        assert lib.unet_tuning_load(str(tmp_path / "absent.db").encode()) < 0
+    finally:
+        lib.unet_tuning_reset()
+
+
 def test_plan_rejects_too_small_input():
     from unet_amd.plan import Plan
     _lib()

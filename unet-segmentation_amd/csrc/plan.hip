@@ -197,6 +197,53 @@ std::mutex g_tune_mu;
 std::map<std::string, GemmChoice> g_tuned;
 std::map<std::string, std::string> g_tune_log;
 
+// Tuning database (the analogue of MIOpen's perf-db): one "key<TAB>tile<TAB>split"
+// line per tuned GEMM shape.  With UNET_TUNE_DB=<path> the first lookup loads
+// the file and every newly tuned shape is appended to it, so a later process
+// (a profiler pass, a restarted job) replays the same kernel choices instead of
+// re-timing them under different conditions.  Callers hold g_tune_mu.
+int tune_db_read(const char* path, bool overwrite) {
+  FILE* f = fopen(path, "r");
+  if (!f) return -errno;
+  char line[512];
+  int n = 0;
+  while (fgets(line, sizeof line, f)) {
+    char* t1 = strchr(line, '\t');
+    if (!t1) continue;
+    *t1 = 0;
+    int tile = 0, split = 0;
+    if (sscanf(t1 + 1, "%d\t%d", &tile, &split) != 2) continue;
+    const std::string key(line);
+    if (!overwrite && g_tuned.count(key)) continue;
+    g_tuned[key] = GemmChoice{tile, split};
+    g_tune_log[key] = key + " | tuning db: tile " + std::to_string(tile) + " split " + std::to_string(split);
+    ++n;
+  }
+  fclose(f);
+  return n;
+}
+
+const char* tune_db_path() {
+  static const char* p = getenv("UNET_TUNE_DB");
+  return p && *p ? p : nullptr;
+}
+
+void tune_db_load_once() {
+  static bool done = false;
+  if (done) return;
+  done = true;
+  if (const char* p = tune_db_path()) (void)tune_db_read(p, false);
+}
+
+void tune_db_append(const std::string& key, const GemmChoice& g) {
+  const char* p = tune_db_path();
+  if (!p) return;
+  if (FILE* f = fopen(p, "a")) {
+    fprintf(f, "%s\t%d\t%d\n", key.c_str(), g.tile, g.split);
+    fclose(f);
+  }
+}
+
 int env_autotune() { return unet::g_autotune; }
 
 constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
@@ -309,6 +356,7 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
   if (!env_autotune()) return GemmChoice{};
   const std::string key = igemm_key(a);
   std::lock_guard<std::mutex> lk(g_tune_mu);
+  tune_db_load_once();
   auto it = g_tuned.find(key);
   if (it != g_tuned.end()) return it->second;
   if (capturing(c.s)) return GemmChoice{};  // hipGraph capture: replay the tuned choice, never time
@@ -337,6 +385,7 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
          std::to_string(tb * 1e3f) + " us" + (verbose ? " |" + all : "");
   g_tuned[key] = best;
   g_tune_log[key] = log;
+  tune_db_append(key, best);
   return best;
 }
 
@@ -344,6 +393,7 @@ GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
   if (!env_autotune()) return GemmChoice{};
   const std::string key = wgrad_key(a);
   std::lock_guard<std::mutex> lk(g_tune_mu);
+  tune_db_load_once();
   auto it = g_tuned.find(key);
   if (it != g_tuned.end()) return it->second;
   if (capturing(c.s)) return GemmChoice{};
@@ -367,6 +417,7 @@ GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
          std::to_string(tb * 1e3f) + " us" + (verbose ? " |" + all : "");
   g_tuned[key] = best;
   g_tune_log[key] = log;
+  tune_db_append(key, best);
   return best;
 }
 
@@ -1118,6 +1169,22 @@ int unet_tuning_reset(void) {
   g_tuned.clear();
   g_tune_log.clear();
   return 0;
+}
+
+int unet_tuning_save(const char* path) {
+  if (!path) return -EINVAL;
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  FILE* f = fopen(path, "w");
+  if (!f) return -errno;
+  for (const auto& kv : g_tuned) fprintf(f, "%s\t%d\t%d\n", kv.first.c_str(), kv.second.tile, kv.second.split);
+  fclose(f);
+  return (int)g_tuned.size();
+}
+
+int unet_tuning_load(const char* path) {
+  if (!path) return -EINVAL;
+  std::lock_guard<std::mutex> lk(g_tune_mu);
+  return tune_db_read(path, true);
 }
 
 int unet_plan_set_timing(unet_plan* p, int enable) {

@@ -76,6 +76,8 @@ SIGNATURES = {
     "unet_set_tuning": (_i, [ctypes.c_char_p, _i]),
     "unet_tuning_report": (_sz, [ctypes.c_char_p, _sz]),
     "unet_tuning_reset": (_i, []),
+    "unet_tuning_save": (_i, [ctypes.c_char_p]),
+    "unet_tuning_load": (_i, [ctypes.c_char_p]),
 }
 
 _lib = None
