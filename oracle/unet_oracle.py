@@ -436,9 +436,12 @@ class UNetOracle:
     first, every ConvTranspose2d and their input / weight gradients see both
     operands rounded to bf16 (after the producer's BatchNorm+ReLU), products
     accumulated exactly; every raw conv output (the first conv's too) is
-    rounded to bf16 before BatchNorm, as the bf16 plan stores it.  The first
+    rounded to bf16 before BatchNorm, as the bf16 plan stores it.  The
+    activation gradients the bf16 plan stores between kernels are rounded too:
+    every BN-input gradient (after the ReLU mask, before the BN backward and its
+    statistics), the pooled-map gradient and the skip gradient.  The first
     conv's arithmetic (Ci <= 4), the 1x1 head, BatchNorm statistics, pooling,
-    biases, gradients and the loss stay unrounded."""
+    biases, parameter gradients and the loss stay unrounded."""
 
     def __init__(self, params, dtype=np.float64, bn_momentum=BN_MOMENTUM, gemm="fp32"):
         if gemm not in ("fp32", "bf16"):
@@ -493,7 +496,7 @@ class UNetOracle:
         outs = cache[pre]
         d = dout
         for (conv_i, bn_i), (a_in, bn_cache, r) in zip((("3", "4"), ("0", "1")), reversed(outs)):
-            d = relu_bwd(d, r)
+            d = self._q(relu_bwd(d, r))  # bf16 plans store dz bf16
             d, dg, dbt = bn_train_bwd(d, bn_cache, self._w(pre + bn_i + ".weight"))
             grads[pre + bn_i + ".weight"] = dg
             grads[pre + bn_i + ".bias"] = dbt
@@ -544,7 +547,7 @@ class UNetOracle:
             skip_shape, (oy, ox), cs = cache[name + ".crop"]
             dskip = np.zeros(skip_shape, dtype=self.dtype)
             h, w = dcat.shape[1], dcat.shape[2]
-            dskip[:, oy:oy + h, ox:ox + w, :] = dcat[..., :cs]
+            dskip[:, oy:oy + h, ox:ox + w, :] = self._q(dcat[..., :cs])  # stored bf16 in bf16 plans
             dskips[4 - k] = dskip
             dup = np.ascontiguousarray(dcat[..., cs:])
             d, dw, db = convT2_bwd(self._q(cache[name + ".in"]), self._q(self._w(name + ".up.weight")), self._q(dup))
@@ -554,7 +557,7 @@ class UNetOracle:
         for k in range(4, 0, -1):
             dpool = self._double_conv_bwd(_dc_prefix(f"down{k}"), d, cache, grads)
             arg, in_shape = cache[f"pool{k}"]
-            d = maxpool2_bwd(dpool, arg, in_shape) + dskips[k - 1]
+            d = maxpool2_bwd(self._q(dpool), arg, in_shape) + dskips[k - 1]
         self._double_conv_bwd(_dc_prefix("inc"), d, cache, grads, need_dx=False)
         return grads
 

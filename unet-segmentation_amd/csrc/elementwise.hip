@@ -113,8 +113,9 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict_
 // coefficients of k_bnb_finalize (coef[4][64]) -- from dz (dy.ptr, the
 // unpadded (ho, wo) grid) and the saved raw conv output y (Y16: bf16).  inc.c0
 // has no input gradient, so dY(0) is consumed only here and is never written
-// (SURVEY.md §8d's fused stage-1 backward: read dz, y, x once).
-template <int CI, int FUSED = 0, int Y16 = 0>
+// (SURVEY.md §8d's fused stage-1 backward: read dz, y, x once).  Z16: dz stored
+// bf16 (bf16 plans).
+template <int CI, int FUSED = 0, int Y16 = 0, int Z16 = 0>
 __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restrict__ x, int nimg, int h, int w,
                                                           Src dy, float* __restrict__ dw,
                                                           const float* __restrict__ yr = nullptr,
@@ -162,7 +163,10 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restric
         const bool ok = (r0 + pr[j] < ho) && (x0 + pc[j] < wo);
         const int yy = min(r0 + pr[j], ho - 1), xx = min(x0 + pc[j], wo - 1);
         const size_t off = ((size_t)(n * dy.H + yy + dy.oy) * dy.W + xx + dy.ox) * dy.C + cg * 4;
-        g[j] = *reinterpret_cast<const float4*>(dy.ptr + off);
+        if (Z16)
+          g[j] = bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dy.ptr) + off));
+        else
+          g[j] = *reinterpret_cast<const float4*>(dy.ptr + off);
         if (FUSED) {
           const float4 d = g[j];
           const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + off))
@@ -277,21 +281,22 @@ hipError_t reduce_first_slabs(int ci, int grid, float* dw, const float* slabs, h
   return hipGetLastError();
 }
 
-template <int FUSED, int Y16>
+template <int FUSED, int Y16, int Z16 = 0>
 static void first_wgrad_go(int grid, int ci, const float* x, int n, int h, int w, const Src& dy, float* slabs,
                            const float* y, const float* coef, hipStream_t s) {
   switch (ci) {
-    case 1: hipLaunchKernelGGL((k_conv_first_wgrad<1, FUSED, Y16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
-    case 2: hipLaunchKernelGGL((k_conv_first_wgrad<2, FUSED, Y16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
-    case 3: hipLaunchKernelGGL((k_conv_first_wgrad<3, FUSED, Y16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
-    default: hipLaunchKernelGGL((k_conv_first_wgrad<4, FUSED, Y16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+    case 1: hipLaunchKernelGGL((k_conv_first_wgrad<1, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+    case 2: hipLaunchKernelGGL((k_conv_first_wgrad<2, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+    case 3: hipLaunchKernelGGL((k_conv_first_wgrad<3, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+    default: hipLaunchKernelGGL((k_conv_first_wgrad<4, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
   }
 }
 
 // inc.c0 weight gradient straight from the BN0 backward (dz, saved y, coef):
 // no padded dY(0) is written or read.
 hipError_t launch_conv_first_wgrad_bn(const float* x, int n, int ci, int h, int w, const float* dz, const float* y,
-                                      int y_h16, const float* coef, int co, float* dw, float* slabs, hipStream_t s) {
+                                      int y_h16, const float* coef, int co, float* dw, float* slabs, hipStream_t s,
+                                      int dz_h16) {
   if (co != 64 || ci < 1 || ci > 4) return hipErrorInvalidValue;
   const long long items = (long long)n * cdiv(h - 2, 4) * cdiv(w - 2, 64);
   const int grid = (int)(items < kFirstWgradSlabs ? items : kFirstWgradSlabs);
@@ -300,7 +305,9 @@ hipError_t launch_conv_first_wgrad_bn(const float* x, int n, int ci, int h, int 
   d.H = h - 2;
   d.W = w - 2;
   d.C = 64;
-  if (y_h16)
+  if (y_h16 && dz_h16)
+    first_wgrad_go<1, 1, 1>(grid, ci, x, n, h, w, d, slabs, y, coef, s);
+  else if (y_h16)
     first_wgrad_go<1, 1>(grid, ci, x, n, h, w, d, slabs, y, coef, s);
   else
     first_wgrad_go<1, 0>(grid, ci, x, n, h, w, d, slabs, y, coef, s);
@@ -392,7 +399,7 @@ __global__ __launch_bounds__(256) void k_bnb_finalize(const double* __restrict__
 
 // dYpad[n][y+pad][x+pad][c] = k0*dz + k1*(y - mean) + k2 ; border written as 0.
 // H16: dYpad stored bf16 (it is only ever a bf16 GEMM operand then).
-template <int H16, int Y16>  // H16: dYpad stored bf16; Y16: y stored bf16
+template <int H16, int Y16, int Z16 = 0>  // H16: dYpad stored bf16; Y16: y stored bf16; Z16: dz stored bf16
 __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restrict__ yr,
                             const float* __restrict__ coef, int n, int h, int w, int C,
                             float* __restrict__ dyp, int pad) {
@@ -414,7 +421,8 @@ __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restric
     float4 out = make_float4(0.f, 0.f, 0.f, 0.f);
     if (colin && yy >= 0 && yy < h) {
       const size_t src = (((size_t)nn * h + yy) * w + xx) * C + c4 * 4;
-      const float4 d = ld4(dz + src);
+      const float4 d = Z16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dz) + src))
+                           : ld4(dz + src);
       const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + src))
                             : ld4(yr + src);
       out.x = fmaf(k0.x, d.x, fmaf(k1.x, yv.x - mu.x, k2.x));
@@ -451,13 +459,18 @@ hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const 
   return hipGetLastError();
 }
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h, int w, int c,
-                            float* dypad, int pad, hipStream_t s, int out_h16, int y_h16) {
+                            float* dypad, int pad, hipStream_t s, int out_h16, int y_h16, int dz_h16) {
   if (c % 4) return hipErrorInvalidValue;
   const long long rowlen = (long long)(w + 2 * pad) * (c / 4), rows = (long long)n * (h + 2 * pad);
   if (rows >= (1LL << 31) || rowlen >= (1LL << 31)) return hipErrorInvalidValue;
   const int gx = (int)((rowlen + 255) / 256);
   // ~4 rows per block keeps the row loop short while filling the chip
   const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max<long long>(1, 32768 / gx))));
+  if (dz_h16) {  // bf16 plans: dz, y and dYpad all bf16
+    if (!out_h16 || !y_h16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_bnb_apply<1, 1, 1>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad);
+    return hipGetLastError();
+  }
   switch (out_h16 * 2 + y_h16) {
     case 0: hipLaunchKernelGGL((k_bnb_apply<0, 0>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad); break;
     case 1: hipLaunchKernelGGL((k_bnb_apply<0, 1>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad); break;
@@ -533,7 +546,9 @@ hipError_t launch_maxpool_fwd(const Src& s, int n, int h, int w, float* y, uint8
 // Maxpool backward fused with the skip-gradient add (the encoder output feeds
 // both the pool and the center-cropped concat, models/unet_model.py:107,130-142),
 // the ReLU mask and the BN-backward statistics of that layer.
-template <int Y16>  // y stored bf16
+// G16: the gradients (dpool, dskip in; dz out) stored bf16 (bf16 plans; dz is
+// rounded before its BN-backward statistics)
+template <int Y16, int G16 = 0>  // y stored bf16
 __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restrict__ dpool,
                                                            const uint8_t* __restrict__ arg,
                                                            const float* __restrict__ dskip, int soy, int sox,
@@ -567,7 +582,8 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
       if (yo < ho && xo < wo) {
         const size_t pi = (((size_t)nn * ho + yo) * wo + xo) * C + c;
         a = *reinterpret_cast<const uchar4*>(arg + pi);
-        g = ld4(dpool + pi);
+        g = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dpool) + pi))
+                : ld4(dpool + pi);
       }
       float4 d[2], yv[2];
 #pragma unroll
@@ -577,7 +593,11 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
         yv[k] = d[k];
         if (yy >= h) continue;
         if (in_skip_x && yy >= soy && yy < soy + sh)
-          d[k] = ld4(dskip + (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c);
+        {
+          const size_t si = (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c;
+          d[k] = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dskip) + si))
+                     : ld4(dskip + si);
+        }
         const size_t oi = (((size_t)nn * h + yy) * w + xx) * C + c;
         if (scale)
           yv[k] = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
@@ -593,6 +613,12 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
         dd.y += (a.y == sel) ? g.y : 0.f;
         dd.z += (a.z == sel) ? g.z : 0.f;
         dd.w += (a.w == sel) ? g.w : 0.f;
+        if (G16) {
+          dd.x = round_bf(dd.x);
+          dd.y = round_bf(dd.y);
+          dd.z = round_bf(dd.z);
+          dd.w = round_bf(dd.w);
+        }
         if (scale) {
           const float4 y4 = yv[k];
           dd.x = (fmaf(y4.x, sc.x, sf.x) > 0.f) ? dd.x : 0.f;
@@ -605,7 +631,11 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
           sb[2] += dd.z * (y4.z - mu.z) * is.z;
           sb[3] += dd.w * (y4.w - mu.w) * is.w;
         }
-        st4(dz + (((size_t)nn * h + yy) * w + xx) * C + c, dd);
+        const size_t oi = (((size_t)nn * h + yy) * w + xx) * C + c;
+        if (G16)
+          reinterpret_cast<uint2*>(dz)[oi / 4] = make_uint2(bf16pack(dd.x, dd.y), bf16pack(dd.z, dd.w));
+        else
+          st4(dz + oi, dd);
       }
     }
   }
@@ -618,7 +648,7 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
 hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, const float* dskip, int soy, int sox,
                                     int sh, int sw, const float* y, const float* scale, const float* shift,
                                     const float* mean, const float* invstd, int n, int h, int w, int c, float* dz,
-                                    double* bstats, hipStream_t s, int y_h16) {
+                                    double* bstats, hipStream_t s, int y_h16, int g_h16) {
   if (c % 4 || (256 % (c / 4)) != 0) return hipErrorInvalidValue;
   const long long rows = (long long)n * ((h + 1) / 2);  // row pairs
   if ((long long)n * h * w >= (1LL << 31)) return hipErrorInvalidValue;
@@ -629,7 +659,11 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
   // per step at 512^2 x 8: 256 blocks 1.14 ms, 512 0.73, 1024 0.54, 2048 0.71,
   // 4096 0.80, 16384 1.28)
   const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max(1, 1024 / gx))));
-  if (y_h16)
+  if (g_h16) {
+    if (!y_h16) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((k_maxpool_bwd_fused<1, 1>), grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
+                       shift, mean, invstd, n, h, w, c, dz, bstats);
+  } else if (y_h16)
     hipLaunchKernelGGL(k_maxpool_bwd_fused<1>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
                        shift, mean, invstd, n, h, w, c, dz, bstats);
   else
@@ -689,7 +723,8 @@ template <int K>
 __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict__ dl, int n, int h, int w,
                                                   const float* __restrict__ wt, const float* __restrict__ mean,
                                                   const float* __restrict__ invstd, float* __restrict__ dz,
-                                                  double* __restrict__ bstats, double* __restrict__ acc_out) {
+                                                  double* __restrict__ bstats, double* __restrict__ acc_out,
+                                                  int dz16) {
   const int tid = threadIdx.x, sub = tid & 15;
   const long long pixels = (long long)n * h * w;
   const int c = sub * 4;
@@ -734,12 +769,21 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
     d.y = zy > 0.f ? d.y : 0.f;
     d.z = zz > 0.f ? d.z : 0.f;
     d.w = zw > 0.f ? d.w : 0.f;
+    if (dz16) {  // bf16 plans store dz bf16: statistics of the rounded values
+      d.x = round_bf(d.x);
+      d.y = round_bf(d.y);
+      d.z = round_bf(d.z);
+      d.w = round_bf(d.w);
+    }
     sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
     sb[0] += d.x * (yv.x - mu.x) * is.x;
     sb[1] += d.y * (yv.y - mu.y) * is.y;
     sb[2] += d.z * (yv.z - mu.z) * is.z;
     sb[3] += d.w * (yv.w - mu.w) * is.w;
-    st4(dz + (size_t)p * 64 + c, d);
+    if (dz16)
+      reinterpret_cast<uint2*>(dz)[((size_t)p * 64 + c) / 4] = make_uint2(bf16pack(d.x, d.y), bf16pack(d.z, d.w));
+    else
+      st4(dz + (size_t)p * 64 + c, d);
   }
   reduce_pairs_to_global(sa, sb, 16, 64, bstats + (size_t)(blockIdx.x % kStatGroups) * 64 * 2);
   __syncthreads();
@@ -791,7 +835,7 @@ hipError_t launch_head_fwd(const Src& s, int n, int h, int w, int c, const float
 
 hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, int c, const float* wt, int k,
                            const float* yraw, const float* mean, const float* invstd, float* dz, double* bstats,
-                           float* dw, float* db, double* acc, hipStream_t st) {
+                           float* dw, float* db, double* acc, hipStream_t st, int dz_h16) {
   (void)yraw;
   if (c != 64) return hipErrorInvalidValue;
   const long long pixels = (long long)n * h * w;
@@ -801,10 +845,10 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
   hipError_t me = hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
   if (me != hipSuccess) return me;
   switch (k) {
-    case 1: hipLaunchKernelGGL(k_head_bwd<1>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
-    case 2: hipLaunchKernelGGL(k_head_bwd<2>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
-    case 3: hipLaunchKernelGGL(k_head_bwd<3>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
-    case 4: hipLaunchKernelGGL(k_head_bwd<4>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc); break;
+    case 1: hipLaunchKernelGGL(k_head_bwd<1>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16); break;
+    case 2: hipLaunchKernelGGL(k_head_bwd<2>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16); break;
+    case 3: hipLaunchKernelGGL(k_head_bwd<3>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16); break;
+    case 4: hipLaunchKernelGGL(k_head_bwd<4>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16); break;
     default: return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(k_d2f, dim3(cdiv(k * 64, 256)), dim3(256), 0, st, acc, k * 64, dw);

@@ -280,7 +280,9 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
             if (k >= lim) continue;
             const unsigned idx = ib + (unsigned)(k * dC);
             float v = acc[i][j][r] + bias;
-            if (e.stats && dh16) v = round_bf(v);
+            // a bf16-stored conv output / BN-input gradient: the statistics are
+            // those of the rounded values its consumers read
+            if (dh16 && (e.stats || bwd_mask)) v = round_bf(v);
             if (bwd_mask) {
               const float yv = e.yref_h16 ? __uint_as_float((unsigned)reinterpret_cast<const uint16_t*>(e.yref)[idx] << 16)
                                           : e.yref[idx];
@@ -326,7 +328,7 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
         float v = acc[i][j][r] + bias;
         // a bf16-stored conv output: its BatchNorm statistics are those of the
         // rounded values the consumers will normalise
-        if (e.stats && d.h16) v = round_bf(v);
+        if (d.h16 && (e.stats || bwd_mask)) v = round_bf(v);
         size_t idx;
         if (linear) {
           idx = (size_t)m * d.C + dcol;

@@ -852,7 +852,7 @@ __global__ __launch_bounds__(256) void k_splitk_epi(const IgemmArgs args) {
       }
     }
     float vv[4] = {v.x, v.y, v.z, v.w};
-    if (e.stats && d.h16) {  // bf16-stored conv output: statistics of the rounded values
+    if (d.h16 && (e.stats || bwd_mask)) {  // bf16-stored output: statistics of the rounded values
 #pragma unroll
       for (int q = 0; q < 4; ++q) vv[q] = round_bf(vv[q]);
     }
@@ -1076,6 +1076,10 @@ static int env_int(const char* name, int dflt) {
 // unet_set_tuning("igemm_variant", v) or UNET_IGEMM_VARIANT; -1 = heuristic
 int g_tune_igemm = env_int("UNET_IGEMM_VARIANT", -1);
 int g_tune_wgrad = env_int("UNET_WGRAD_VARIANT", -1);
+// unet_set_tuning("wino_max", m) or UNET_WINO_MAX: largest Winograd output tile
+// the fp32 candidates may use (6 = F(6x6) and below, 4 = up to F(4x4), 2, 0 = none)
+int g_wino_max = env_int("UNET_WINO_MAX", 6);
+static int wino_tile_m(int tile) { return tile == 70 ? 2 : tile == 71 || tile == 72 ? 4 : tile == 74 ? 6 : 0; }
 
 // igemm tile table: id -> (BM, BN, waves M x N, BK), resident workgroups per CU
 // (min of the LDS and VGPR limits of the built kernels).
@@ -1139,6 +1143,7 @@ static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 // A tile applies when the shape divides and the packed B operand is in the
 // tile's precision (fp32 `b` for tiles 1-14, bf16 `bh` for 21-26).
 bool igemm_tile_fits(const IgemmArgs& a, int tile) {
+  if (wino_tile_m(tile) > g_wino_max) return false;
   const TileInfo t = tile_info(tile);
   const bool prec_ok = is_bf16_tile(tile) ? a.bh != nullptr && (a.bl == nullptr || bf16_tile_splits(tile))
                                            : a.b != nullptr;
@@ -1329,6 +1334,7 @@ static void wgrad_tile(int id, int& bm, int& bn) {
   if (id >= 10 && id < 15) { bm = tb[id - 10][0]; bn = tb[id - 10][1]; }
 }
 bool wgrad_tile_fits(const WgradArgs& a, int tile) {
+  if (wino_tile_m(tile) > g_wino_max) return false;
   if (tile == 71 || tile == 74) return wino_wgrad_applies(a, tile == 71 ? 4 : 6);
   if (a.batch > 1 && (tile < 0 || tile > 4)) return false;  // batched: fp32 pixel-column tiles only
   if (tile == 20 || tile == 21) return wgrad3_fits(a);  // halo-tiled 3x3, all taps

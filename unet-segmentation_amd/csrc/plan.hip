@@ -642,6 +642,10 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
                  int seg_b, int seg_e, hipStream_t s) {
   Ctx c{p, ws, s};
   const int n = p->n;
+  // bf16 plans store the activation gradients between GEMMs in bf16 (as
+  // autocast does): the BN-input gradients dz, the pooled-map gradient and the
+  // skip gradient; their BN-backward statistics are those of the rounded values
+  const int g16 = p->prec == UNET_PREC_BF16;
   // Weight gradients of layer l need only dY(l) and forward tensors: they go to
   // the side stream once the plan is tuned (timing runs stay serial so that
   // per-kernel event times stay clean).  Under hipGraph capture the side stream
@@ -658,7 +662,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * L.ho * L.wo * (2 * L.co + p->ncls));
     CK(launch_head_bwd(src_of(c, L, true), dlogits, n, L.ho, L.wo, L.co, P<float>(prm, 134), p->ncls, c.f(L.y),
                        c.f(L.mean), c.f(L.invstd), c.f(L.dz), c.d(L.bstats), P<float>(grd, 80), P<float>(grd, 81),
-                       c.d(p->head_acc), s));
+                       c.d(p->head_acc), s, g16));
   }
   for (int l = 17; l >= 0; --l) {
     if (!in_seg(seg_of_layer(l))) continue;
@@ -682,17 +686,17 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
               4.0 * n * ((double)p->cin * p->h * p->w) +
                   (p->prec == UNET_PREC_BF16 ? 6.0 : 8.0) * n * (double)L.ho * L.wo * L.co);
       CK(launch_conv_first_wgrad_bn(x, n, p->cin, p->h, p->w, c.f(L.dz), c.f(L.y), p->prec == UNET_PREC_BF16,
-                                    c.f(L.coef), L.co, P<float>(grd, L.gw), c.f(p->first_slabs), sw));
+                                    c.f(L.coef), L.co, P<float>(grd, L.gw), c.f(p->first_slabs), sw, g16));
       continue;
     }
     CK(launch_bnb_finalize(c.d(L.bstats), L.co, M, P<float>(prm, L.pw + 2), c.f(L.mean), c.f(L.invstd),
                            P<float>(grd, L.gw + 2), P<float>(grd, L.gw + 3), P<float>(grd, L.gw + 1), c.f(L.coef), s));
     {
-      Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * ((double)(L.ho + 4) * (L.wo + 4) + 2.0 * L.ho * L.wo) * L.co);
+      Timer t(p, s, UNET_KC_ELEMWISE, 0, (g16 ? 2.0 : 4.0) * n * ((double)(L.ho + 4) * (L.wo + 4) + 2.0 * L.ho * L.wo) * L.co);
       // bf16 plans store dY(l > 0) in bf16: it only feeds bf16 GEMMs (inc.c0's
       // fp32 direct weight-gradient kernel reads dY(0))
       CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), n, L.ho, L.wo, L.co, c.f(L.dyp), 2, s, dy16,
-                          p->prec == UNET_PREC_BF16));
+                          p->prec == UNET_PREC_BF16, g16));
     }
     if (conc) {
       CK(hipEventRecord(p->ev_dy[l], s));
@@ -740,7 +744,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     a.K = 9 * L.co;
     if (l % 2 == 1) {  // -> dz of layer l-1 (masked + BN-bwd stats)
       Conv& Q = p->L[l - 1];
-      a.e.d[0] = Dst{c.f(Q.dz), Q.ho, Q.wo, Q.co, 0, 0};
+      a.e.d[0] = Dst{c.f(Q.dz), Q.ho, Q.wo, Q.co, 0, 0, g16};
       a.e.yref = c.f(Q.y);
       a.e.yref_h16 = p->prec == UNET_PREC_BF16;
       a.e.bn_scale = c.f(Q.scale);
@@ -754,7 +758,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     } else if (l <= 8) {  // -> gradient of the pooled tensor, then pool backward
       const int k = l / 2 - 1;
       Pool& pl = p->P[k];
-      a.e.d[0] = Dst{c.f(pl.dp), pl.h / 2, pl.w / 2, pl.c, 0, 0};
+      a.e.d[0] = Dst{c.f(pl.dp), pl.h / 2, pl.w / 2, pl.c, 0, 0, g16};
       {
         Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
         Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
@@ -762,15 +766,15 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       }
       Conv& Q = p->L[l - 1];  // encoder output feeding this pool (and a skip)
       const Skip& sk = p->S[3 - k];
-      Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * (double)Q.ho * Q.wo * Q.co * 2.6);
+      Timer t(p, s, UNET_KC_ELEMWISE, 0, (g16 ? 2.0 : 4.0) * n * (double)Q.ho * Q.wo * Q.co * 2.6);
       CK(launch_maxpool_bwd_fused(c.f(pl.dp), c.u8(pl.arg), c.f(sk.d), sk.oy, sk.ox, sk.th, sk.tw, c.f(Q.y),
                                   c.f(Q.scale), c.f(Q.shift), c.f(Q.mean), c.f(Q.invstd), n, Q.ho, Q.wo, Q.co,
-                                  c.f(Q.dz), c.d(Q.bstats), s, p->prec == UNET_PREC_BF16));
+                                  c.f(Q.dz), c.d(Q.bstats), s, p->prec == UNET_PREC_BF16, g16));
     } else {  // first conv of up block: split into skip grad and upsampled grad
       const int k = (l - 10) / 2;
       ConvT& T = p->T[k];
       Skip& sk = p->S[k];
-      a.e.d[0] = Dst{c.f(sk.d), sk.th, sk.tw, sk.c, 0, 0};
+      a.e.d[0] = Dst{c.f(sk.d), sk.th, sk.tw, sk.c, 0, 0, g16};
       a.e.d[1] = Dst{c.f(T.du), 2 * T.h, 2 * T.w, T.co, 0, 0, p->prec == UNET_PREC_BF16};
       a.e.n_split = sk.c;
       a.e.colsum1 = c.d(T.colsum);
@@ -837,7 +841,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       b.M = n * T.h * T.w;
       b.N = T.ci;
       b.K = 4 * T.co;
-      b.e.d[0] = Dst{c.f(Q.dz), Q.ho, Q.wo, Q.co, 0, 0};
+      b.e.d[0] = Dst{c.f(Q.dz), Q.ho, Q.wo, Q.co, 0, 0, g16};
       b.e.yref = c.f(Q.y);
       b.e.yref_h16 = p->prec == UNET_PREC_BF16;
       b.e.bn_scale = c.f(Q.scale);

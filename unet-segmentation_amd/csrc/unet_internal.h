@@ -204,7 +204,8 @@ hipError_t launch_conv_first_wgrad(const float* x_nchw, int n, int ci, int h, in
 // inc.c0 weight gradient with the BN0 backward fused in (reads dz, y, x; coef =
 // k_bnb_finalize's [k0|k1|k2|mean] per channel)
 hipError_t launch_conv_first_wgrad_bn(const float* x, int n, int ci, int h, int w, const float* dz, const float* y,
-                                      int y_h16, const float* coef, int co, float* dw, float* slabs, hipStream_t s);
+                                      int y_h16, const float* coef, int co, float* dw, float* slabs, hipStream_t s,
+                                      int dz_h16 = 0);
 
 // BN finalize (train): stats[G][C][2] -> mean, invstd, scale, shift; running update.
 hipError_t launch_bn_finalize(const double* stats, int c, double count, const float* gamma,
@@ -223,7 +224,7 @@ hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const 
 // dYpad interior = coef0*dz + coef1*y + coef2; border (pad each side) = 0.
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h,
                             int w, int c, float* dypad, int pad, hipStream_t s, int out_h16 = 0,
-                            int y_h16 = 0);
+                            int y_h16 = 0, int dz_h16 = 0);
 // MaxPool2d(2) fwd with BN+ReLU transform on load (src grid H x W, pooled H/2 x W/2).
 hipError_t launch_maxpool_fwd(const Src& src, int n, int h, int w, float* y, uint8_t* arg,
                               hipStream_t s, int out_h16 = 0);
@@ -233,7 +234,8 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
                                     int skip_oy, int skip_ox, int skip_h, int skip_w,
                                     const float* y, const float* scale, const float* shift,
                                     const float* mean, const float* invstd, int n, int h, int w,
-                                    int c, float* dz, double* bstats, hipStream_t s, int y_h16 = 0);
+                                    int c, float* dz, double* bstats, hipStream_t s, int y_h16 = 0,
+                                    int g_h16 = 0);
 // 1x1 head (OutConv, models/unet_model.py:56-63) forward: logits NCHW.
 hipError_t launch_head_fwd(const Src& src, int n, int h, int w, int c, const float* wt,
                            const float* bias, int k, float* logits, hipStream_t s);
@@ -241,7 +243,7 @@ hipError_t launch_head_fwd(const Src& src, int n, int h, int w, int c, const flo
 hipError_t launch_head_bwd(const Src& src, const float* dlogits, int n, int h, int w, int c,
                            const float* wt, int k, const float* yraw, const float* mean,
                            const float* invstd, float* dz, double* bstats, float* dw, float* db,
-                           double* ws_acc, hipStream_t s);
+                           double* ws_acc, hipStream_t s, int dz_h16 = 0);
 hipError_t launch_wce(const float* logits, const int64_t* t, const float* wm, int n, int k, int h,
                       int w, const int64_t* ts, const int64_t* wsd, float* loss, float* dlogits,
                       float grad_scale, double* acc, hipStream_t s);
