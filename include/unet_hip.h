@@ -275,8 +275,10 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  22-23 fp32 halo tiles; 71 / 74 = Winograd F(4x4,3x3) /
  *                  F(6x6,3x3) weight gradient, plan GEMMs only);
  *  "wino_max"      largest fp32 Winograd output tile the autotuner may pick
- *                  (env UNET_WINO_MAX): 6 (default) = F(6x6) and below, 4 =
- *                  F(4x4) / F(2x2) only, 2 = F(2x2) only, 0 = direct GEMMs only.
+ *                  for forward / input-gradient GEMMs (env UNET_WINO_MAX): 6 =
+ *                  F(6x6) and below, 4 (default) = F(4x4) / F(2x2), 2 = F(2x2)
+ *                  only, 0 = direct GEMMs only; "wino_wgrad_max" (env
+ *                  UNET_WINO_WGRAD_MAX, default 6) the same for weight gradients.
  *  "concurrent"    1 (default, or env UNET_CONCURRENT) = a plan's backward
  *                  runs the weight-gradient GEMMs on a side stream beside the
  *                  dX chain (joined before the call returns); 0 = one stream.
