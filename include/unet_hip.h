@@ -266,7 +266,7 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  fastest per shape; 0 = built-in heuristic only.
  *  "igemm_variant" heuristic override for A/B measurements (-1 = off, 1..9 =
  *                  forced tile shape; 21-26, 31-36, 41-44 bf16 tiles, 63,
- *                  65-67 bf16 halo tiles with LDS-DMA weights; 70-72, 74 fp32
+ *                  65-68 bf16 halo tiles with LDS-DMA weights; 70-72, 74 fp32
  *                  Winograd: F(2x2,3x3), F(4x4,3x3), fused F(4x4,3x3),
  *                  F(6x6,3x3), plan GEMMs only -- they need the plan's
  *                  scratch); "wgrad_variant"

@@ -143,7 +143,7 @@ def test_bf16_conv3x3_dgrad(op_bf16, n, h, w, ci, co, variant):
 # k_conv3_dma (conv3_dma.hip): TH x 32 tiles, LDS-DMA weights, 2-stage ring;
 # bf16-stored A only, so the per-op entry points run with op_a16 = 1 (x stored
 # bf16 before its transform / padded dY bf16, as in a bf16 plan)
-DMA = [63, 65, 66, 67]
+DMA = [63, 65, 66, 67, 68]
 
 
 @pytest.mark.parametrize("variant", DMA + [31, 33])

@@ -385,11 +385,19 @@ def test_side_stream_weight_grads_match_serial():
         assert np.abs(got[name] - g).max() <= 1e-5 * scale + 1e-12, name
 
 
+@pytest.mark.parametrize("gemm_mode", ["heuristic"], indirect=True)
 @pytest.mark.parametrize("c,k", [(2, 3), (4, 4), (3, 2)])
-def test_channel_and_class_counts_vs_oracle(c, k):
+def test_channel_and_class_counts_vs_oracle(c, k, gemm_mode):
     """n_channels 2-4 (the first conv's direct kernel) and n_classes 3-4 (head,
     weighted CE over K classes) -- the reference's constructor arguments
-    (models/unet_model.py:66) beyond the 1 -> 2 of scripts/train.py."""
+    (models/unet_model.py:66) beyond the 1 -> 2 of scripts/train.py.
+    GEMMs pinned to the built-in (direct) variants: at 2 x 188 some gradients
+    are sensitive at the 1 % level to ~1e-6 relative changes of the conv
+    outputs (ReLU-mask / max-pool tie flips; a 1e-6 random perturbation of
+    every conv output in the fp64 oracle moves BN-bias gradients by up to
+    0.9 %), so an autotuned Winograd mix (F(4x4) rounding ~2e-6) put one
+    BN-bias gradient at 2.5 % in some runs.  The Winograd variants have their
+    own whole-step tests (test_train_step_gemm_variants_vs_oracle)."""
     from unet_amd import WeightedCrossEntropyLoss
     seed = 60 + 10 * c + k
     params = O.hash_init(c, k, seed=seed, bn_random=True)

@@ -30,7 +30,7 @@ SHAPES = [
     ("up4.c1", 8, 326, 326, 64, 64),
 ]
 VARIANTS = [-1, 21, 22, 23, 24, 31, 32, 33, 34, 35, 36, 41, 42, 43, 44]
-DMA_VARIANTS = [31, 33, 63, 65, 66, 67]
+DMA_VARIANTS = [31, 33, 63, 65, 66, 67, 68]
 
 
 def main():

@@ -324,7 +324,7 @@ static hipError_t go_conv3_dma(const IgemmArgs& a, hipStream_t s) {
   return tf ? go_conv3_dma_t<TH, BN, CH, WM, WN, MINW, 0>(a, s) : go_conv3_dma_t<TH, BN, CH, WM, WN, MINW, 1>(a, s);
 }
 
-// tile ids 63, 65-67 (igemm.hip tile_info): (TH, BN, CH, waves).  Measured and
+// tile ids 63, 65-68 (igemm.hip tile_info): (TH, BN, CH, waves).  Measured and
 // dropped (profiles/r02_conv_dma_variants.txt): one-wave-per-SIMD shapes
 // (8x32/128 and 8x32/64 with 32-channel chunks at 4 waves) and 16x32/128 at 8
 // waves (spills in the register-staged form) ran 1.3-3x slower than k_conv3_bf.
@@ -334,6 +334,7 @@ bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch) {
     case 65: th = 16; bn = 64; ch = 16; return true;
     case 66: th = 16; bn = 64; ch = 32; return true;
     case 67: th = 8; bn = 64; ch = 16; return true;
+    case 68: th = 8; bn = 128; ch = 16; return true;
     default: return false;
   }
 }
@@ -344,6 +345,7 @@ hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 65: return go_conv3_dma<16, 64, 16, 4, 2, 2>(a, s);  // 8 waves, TM 4 x TN 1; 84 KB
     case 66: return go_conv3_dma<16, 64, 32, 4, 2, 2>(a, s);  // 8 waves, TM 4 x TN 1; 160 KB
     case 67: return go_conv3_dma<8, 64, 16, 8, 1, 4>(a, s);   // 8 waves, TM 1 x TN 2; 59 KB: 2 WG/CU, 4 waves/SIMD
+    case 68: return go_conv3_dma<8, 128, 16, 4, 2, 2>(a, s);  // 8 waves, TM 2 x TN 2 (64x64 per wave); 96 KB
     default: return hipErrorInvalidValue;
   }
 }

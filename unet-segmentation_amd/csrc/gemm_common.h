@@ -274,6 +274,22 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
           int mb, lim;
           rows.block(wm * TM + i, h, mb, lim);
           const unsigned ib = (unsigned)mb * (unsigned)dC + (unsigned)dcol;
+          // The ReLU-mask operand of all 16 rows is loaded before the first
+          // store: the destination may alias yref as far as the compiler knows,
+          // so loads interleaved with the stores each waited out a full memory
+          // latency (16 serialised round trips per fragment).  Rows past the
+          // grid re-load the last valid row.
+          float yv[16];
+          if (bwd_mask && lim > 0) {
+            const int kmax = lim - 1;
+#pragma unroll
+            for (int r = 0; r < 16; ++r) {
+              const int k = min((r & 3) + 8 * (r >> 2), kmax);
+              const unsigned idx = ib + (unsigned)(k * dC);
+              yv[r] = e.yref_h16 ? __uint_as_float((unsigned)reinterpret_cast<const uint16_t*>(e.yref)[idx] << 16)
+                                 : e.yref[idx];
+            }
+          }
 #pragma unroll
           for (int r = 0; r < 16; ++r) {
             const int k = (r & 3) + 8 * (r >> 2);
@@ -284,11 +300,9 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
             // those of the rounded values its consumers read
             if (dh16 && (e.stats || bwd_mask)) v = round_bf(v);
             if (bwd_mask) {
-              const float yv = e.yref_h16 ? __uint_as_float((unsigned)reinterpret_cast<const uint16_t*>(e.yref)[idx] << 16)
-                                          : e.yref[idx];
-              v = (fmaf(yv, bsc, bsh) > 0.f) ? v : 0.f;
+              v = (fmaf(yv[r], bsc, bsh) > 0.f) ? v : 0.f;
               s1[j] += v;
-              s2[j] += v * ((yv - bmu) * bis);
+              s2[j] += v * ((yv[r] - bmu) * bis);
             } else if (e.stats) {
               s1[j] += v;
               s2[j] += v * v;

@@ -1130,6 +1130,7 @@ static TileInfo tile_info(int id) {
     case 65: return {512, 64, 144, 1};
     case 66: return {512, 64, 288, 1};
     case 67: return {256, 64, 144, 2};
+    case 68: return {256, 128, 144, 1};
     // Winograd F(2x2, 3x3) (winograd.hip): no K split
     case 70: case 71: case 74: return {256, 64, 9, 2};
     case 72: return {32, 32, 16, 1};
@@ -1143,7 +1144,7 @@ static TileInfo tile_info(int id) {
 }
 
 static bool is_halo_tile(int tile) { return (tile >= 31 && tile <= 36) || (tile >= 41 && tile <= 44); }
-static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 67); }
+static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 68); }
 static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile); }
 static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 
@@ -1257,7 +1258,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 21: case 22: case 23: case 24: case 25: case 26:
     case 31: case 32: case 33: case 34: case 35: case 36:
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
-    case 63: case 65: case 66: case 67: return go_conv3_dma_tile(a, s, tile);
+    case 63: case 65: case 66: case 67: case 68: return go_conv3_dma_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);
     case 71: return launch_wino(a, s, 4);
     case 74: return launch_wino(a, s, 6);

@@ -344,6 +344,22 @@ static void launch_wino4_in(const Gather& g, int Th, int Tw, long long T, float*
   else hipLaunchKernelGGL(k_wino4_in<1>, grid, dim3(256), 0, s, g, Th, Tw, T, U);
 }
 
+// The 4x4 ReLU-mask operands of output tile (n, ty, tx), column dcol, issued as
+// 16 independent loads (coordinates past the grid clamped to its last row /
+// column: those outputs are not stored).
+__device__ __forceinline__ void wf_yref4(const float* __restrict__ yref, const Gather& g, int n, int ty, int tx, int dC,
+                                         int dcol, float (&yv)[4][4]) {
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int y = min(4 * ty + a, g.Hg - 1);
+#pragma unroll
+    for (int bb = 0; bb < 4; ++bb) {
+      const int x = min(4 * tx + bb, g.Wg - 1);
+      yv[a][bb] = yref[((size_t)(n * g.Hg + y) * g.Wg + x) * dC + dcol];
+    }
+  }
+}
+
 // Block = 64 channels x 4 tile lanes; grid-stride over tiles.
 __global__ __launch_bounds__(256) void k_wino4_out(const float* __restrict__ m, long long T, int Th, int Tw, int N,
                                                    Gather g, Epilogue e) {
@@ -379,6 +395,10 @@ __global__ __launch_bounds__(256) void k_wino4_out(const float* __restrict__ m, 
       const int tx = (int)(t % Tw);
       const long long r = t / Tw;
       const int ty = (int)(r % Th), n = (int)(r / Th);
+      // ReLU-mask operands of the 16 outputs loaded before the first store
+      // (wf_yref4: the stores may alias yref for the compiler)
+      float yv[4][4];
+      if (bwd_mask) wf_yref4(e.yref, g, n, ty, tx, dC, dcol, yv);
 #pragma unroll
       for (int a = 0; a < 4; ++a) {
         float o[4];
@@ -392,10 +412,9 @@ __global__ __launch_bounds__(256) void k_wino4_out(const float* __restrict__ m, 
           float v = o[bb] + bias;
           const size_t idx = ((size_t)(n * g.Hg + y) * g.Wg + x) * dC + dcol;
           if (bwd_mask) {
-            const float yv = e.yref[idx];
-            v = fmaf(yv, bsc, bsh) > 0.f ? v : 0.f;
+            v = fmaf(yv[a][bb], bsc, bsh) > 0.f ? v : 0.f;
             s1 += v;
-            s2 += v * ((yv - bmu) * bis);
+            s2 += v * ((yv[a][bb] - bmu) * bis);
           } else if (e.stats) {
             s1 += v;
             s2 += v * v;
@@ -862,6 +881,8 @@ __device__ __forceinline__ void wf_output(float* lds, int tid, long long t0, int
     const int ox = (int)(tt % Tw);
     const long long r = tt / Tw;
     const int oy = (int)(r % Th), on = (int)(r / Th);
+    float yv[4][4];
+    if (bwd_mask) wf_yref4(e.yref, g, on, oy, ox, dC, dcol, yv);
 #pragma unroll
     for (int a = 0; a < 4; ++a) {
       float o[4];
@@ -875,10 +896,9 @@ __device__ __forceinline__ void wf_output(float* lds, int tid, long long t0, int
         float v = o[bb] + bias;
         const size_t idx = ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol;
         if (bwd_mask) {
-          const float yv = e.yref[idx];
-          v = fmaf(yv, bsc, bsh) > 0.f ? v : 0.f;
+          v = fmaf(yv[a][bb], bsc, bsh) > 0.f ? v : 0.f;
           s1 += v;
-          s2 += v * ((yv - bmu) * bis);
+          s2 += v * ((yv[a][bb] - bmu) * bis);
         } else if (e.stats) {
           s1 += v;
           s2 += v * v;
