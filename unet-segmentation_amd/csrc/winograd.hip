@@ -1256,38 +1256,58 @@ __device__ __forceinline__ void gt8(const float (&m)[8], float (&r)[3]) {
   mat_apply(GT, m, r);
 }
 
+// Thread = (tile, V output channels): 6x6 dY patch by clamped unconditional
+// vector loads from a per-thread base (32-bit offsets), 64 points out as V-wide
+// stores (32-bit plane offsets: wino_wgrad_applies)
+template <int V>
 __global__ __launch_bounds__(256) void k_wino6_dy(Src dy, int Hg, int Wg, int Th, int Tw, long long T, int Co,
                                                   float* __restrict__ vd) {
+  typedef float vec __attribute__((ext_vector_type(V)));
+  const int CV = Co / V;
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
-  if (i >= T * Co) return;
-  const long long t = i / Co;
-  const int c = (int)(i - t * Co);
+  if (i >= T * CV) return;
+  const long long t = i / CV;
+  const int c = (int)(i - t * CV) * V;
   const int tx = (int)(t % Tw);
   const long long r = t / Tw;
   const int ty = (int)(r % Th), n = (int)(r / Th);
-  float e[8][6];
+  const int vr = min(6, Hg - 6 * ty), vc = min(6, Wg - 6 * tx);
+  const char* base = reinterpret_cast<const char*>(dy.ptr) +
+                     (((size_t)(n * dy.H + 6 * ty + dy.oy) * dy.W + 6 * tx + dy.ox) * dy.C + c) * 4;
+  const unsigned rs = (unsigned)dy.W * dy.C * 4u, cs = (unsigned)dy.C * 4u;
+  float e[V][8][6];
 #pragma unroll
   for (int xx = 0; xx < 6; ++xx) {
-    float d[6];
+    float d[V][6];
 #pragma unroll
     for (int yy = 0; yy < 6; ++yy) {
-      const int y = 6 * ty + yy, x = 6 * tx + xx;
-      const bool in = y < Hg && x < Wg;
-      const float v = dy.ptr[((size_t)(n * dy.H + (in ? y : 0) + dy.oy) * dy.W + (in ? x : 0) + dy.ox) * dy.C + c];
-      d[yy] = in ? v : 0.f;
-    }
-    float rr[8];
-    a8(d, rr);
+      const bool in = yy < vr && xx < vc;
+      const vec v = *reinterpret_cast<const vec*>(base + (in ? yy * rs + xx * cs : 0u));
 #pragma unroll
-    for (int a = 0; a < 8; ++a) e[a][xx] = rr[a];
+      for (int k = 0; k < V; ++k) d[k][yy] = in ? v[k] : 0.f;
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float rr[8];
+      a8(d[k], rr);
+#pragma unroll
+      for (int a = 0; a < 8; ++a) e[k][a][xx] = rr[a];
+    }
   }
-  const size_t plane = (size_t)T * Co, o = (size_t)t * Co + c;
+  char* ob = reinterpret_cast<char*>(vd + (size_t)t * Co + c);
+  const unsigned pbytes = (unsigned)((size_t)T * Co * 4);
 #pragma unroll
   for (int a = 0; a < 8; ++a) {
-    float rr[8];
-    a8(e[a], rr);
+    float rr[V][8];
 #pragma unroll
-    for (int bb = 0; bb < 8; ++bb) vd[(a * 8 + bb) * plane + o] = rr[bb];
+    for (int k = 0; k < V; ++k) a8(e[k][a], rr[k]);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) {
+      vec o;
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = rr[k][bb];
+      *reinterpret_cast<vec*>(ob + (unsigned)(a * 8 + bb) * pbytes) = o;
+    }
   }
 }
 
@@ -1361,8 +1381,8 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
                        Tw, T, Co, Vd);
   } else {
     launch_wino6_in(gb, Th, Tw, T, U, s);
-    hipLaunchKernelGGL(k_wino6_dy, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg, gb.Wg, Th,
-                       Tw, T, Co, Vd);
+    hipLaunchKernelGGL(k_wino6_dy<2>, dim3((unsigned)((nd / 2 + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg,
+                       gb.Wg, Th, Tw, T, Co, Vd);  // Co % 64 == 0 (wino_wgrad_applies)
   }
   hipError_t e = hipMemsetAsync(Mw, 0, (size_t)P * Co * Ci * 4, s);
   if (e != hipSuccess) return e;
