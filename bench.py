@@ -27,7 +27,15 @@ Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
   the same frames and weights (a checker leg, run after the timing);
 * cpu_baseline: the reference train step restated on torch CPU
   (oracle/torch_cpu_ref.py; the reference .py does not travel to the GPU box)
-  at batch 8 and batch 1 on this host's cores.
+  at batch 8 and batch 1 on this host's cores;
+* c5: configs[4] (3-ch 572^2, batch 8, bf16 train step) with its roofline;
+  farm: configs[3] (1024^2 overlap-tile inference, fp32 and bf16, one GPU);
+* lib: unet_version() with the source hash it was built from, and the tuning
+  database replayed (profiles/tune_db.txt: the GEMM choices this line timed,
+  loaded by the full-size parity tests too).
+
+value / ms_per_step: the MEDIAN per-step time over the timed steps (HIP events
+per step, BASELINE.md's protocol); mean_ms_per_step / wall_value: wall clock.
 """
 from __future__ import annotations
 
@@ -86,23 +94,26 @@ def cpu_model():
     return "unknown"
 
 
-def cpu_baseline():
+def cpu_baseline(steps=5):
     """The reference train step (scripts/train.py:114-131 semantics) restated on
     torch CPU -- the same oneDNN / native kernels the reference runs on -- at
     512x512x1, batch 8 (the metric's batch) and batch 1 (configs[0]), timed on
-    this host.  Bounded: one untimed warm-up step at batch 1, then ~10 s per
-    batch size.  Measurement infrastructure (oracle/torch_cpu_ref.py)."""
+    this host: `steps` steps per batch size after one warm-up step, images/s
+    from the median step.  Measurement infrastructure
+    (oracle/torch_cpu_ref.py)."""
     from oracle import torch_cpu_ref as R
     threads = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     torch.set_num_threads(threads)
     R.train_steps_per_second(1, seconds=0.0, max_steps=1)
-    v1, s1, e1 = R.train_steps_per_second(1, seconds=6.0, max_steps=3)
-    v8, s8, e8 = R.train_steps_per_second(8, seconds=8.0, max_steps=2)
-    return {"value": round(v8, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "cpu_model": cpu_model(), "batch1_value": round(v1, 4),
+    _, t1 = R.train_step_times(1, steps)
+    _, t8 = R.train_step_times(8, steps)
+    med = lambda ts: sorted(ts)[len(ts) // 2]  # noqa: E731
+    return {"value": round(8 / med(t8), 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model(), "batch1_value": round(1 / med(t1), 4),
+            "step_s": {"batch8": [round(v, 3) for v in t8], "batch1": [round(v, 3) for v in t1]},
             "sample": f"torch {torch.__version__} CPU restatement of the reference train step (fwd + weighted CE + "
-                      f"bwd + SGD(0.99), fp32, 512x512x1): batch 8 x {s8} step(s) in {e8:.1f} s; batch 1 x {s1} "
-                      f"step(s) in {e1:.1f} s, after one warm-up step"}
+                      f"bwd + SGD(0.99), fp32, 512x512x1): {steps} steps at batch 8 and {steps} at batch 1 after one "
+                      f"warm-up step, median step time ({sum(t8) + sum(t1):.1f} s of CPU work)"}
 
 
 def pmc_traffic(args, dtype):
@@ -159,6 +170,39 @@ def hela_iou(device, precision):
                     "iou_ref = the reference UNet on the same frames and weights (tests/golden/hela_real.npz)"}
 
 
+def run_farm(args, dtype, device, iters=20, warmup=3):
+    """configs[3] on one GPU: overlap-tile inference of a 1024x1024 image as
+    16 tiles of 512x512 (324x324 out), batch 8, eval mode, uint8 mask out
+    (scripts/predict.py:70-92 per tile; unet_amd/tiling.py).  Tiles farm over N
+    GPUs with no collective (replicas), so N GPUs scale this by N."""
+    from unet_amd import UNet
+    from unet_amd.tiling import TileFarm, TileGeometry
+    torch.manual_seed(0)
+    m = UNet(1, 2)
+    m.apply(init_weights)
+    m.precision = dtype
+    farm = TileFarm(m, devices=[device.index], tile_in=512, batch=8)
+    for r in farm.replicas:
+        r.precision = dtype
+    g = torch.Generator().manual_seed(5)
+    img = torch.rand((1, 1024, 1024), generator=g) * 2 - 1
+    for _ in range(warmup):
+        farm.predict(img, return_mask=True)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(iters):
+        t0 = time.perf_counter()
+        mask = farm.predict(img, return_mask=True)   # includes the host copy of the mask
+        times.append(time.perf_counter() - t0)
+    med = sorted(times)[len(times) // 2]
+    geo = TileGeometry(1024, 1024, 512)
+    return {"value": round(1 / med, 3), "unit": "images/s", "ms_per_image": round(med * 1e3, 3),
+            "tiles_per_s": round(len(geo) / med, 1), "dtype": dtype,
+            "config": {"workload": "overlap-tile inference 1024x1024x1 (configs[3]), 512^2 tiles -> 324^2, "
+                                   f"{len(geo)} tiles, batch 8, eval mode, mask output, 1 GPU (replicas: N GPUs = N x)",
+                       "mask_shape": list(mask.shape)}}
+
+
 def run_precision(args, dtype, device, pg, world, rank):
     """Time args.steps train steps of one GEMM precision; returns its summary."""
     from unet_amd import UNet
@@ -181,18 +225,27 @@ def run_precision(args, dtype, device, pg, world, rank):
     if pg is not None:
         dist.barrier()
     torch.cuda.synchronize()
+    # per-step HIP events on the stream every step joins into (the side stream
+    # and the collectives are waited on before the optimizer): the median step
+    # (BASELINE.md protocol) next to the wall-clock mean; no host sync inside
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    evs[0].record()
+    for i in range(args.steps):
         loss = trainer.step(x, t, w)
+        evs[i + 1].record()
     torch.cuda.synchronize()
     if pg is not None:
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    step_ms = sorted(evs[i].elapsed_time(evs[i + 1]) for i in range(args.steps))
+    median_ms = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1] +
+                                                                              step_ms[len(step_ms) // 2])
     if pg is not None:
-        e = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        e = torch.tensor([elapsed, median_ms], dtype=torch.float64, device=device)
         dist.all_reduce(e, op=dist.ReduceOp.MAX)
-        elapsed = float(e.item())
+        elapsed, median_ms = float(e[0].item()), float(e[1].item())
     final_loss = float(loss.item())
 
     # per-kernel-class timing of one extra (untimed) step: HIP events recorded by
@@ -233,8 +286,12 @@ def run_precision(args, dtype, device, pg, world, rank):
                for k, v in tim.items()}
     imgs = world * args.batch * args.steps
     return {
-        "value": round(imgs / elapsed, 3),
-        "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        # images/s = world * batch / median step time
+        "value": round(world * args.batch / (median_ms * 1e-3), 3),
+        "ms_per_step": round(median_ms, 3),
+        "mean_ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "wall_value": round(imgs / elapsed, 3),
+        "step_ms_range": [round(step_ms[0], 3), round(step_ms[-1], 3)],
         "dtype": dtype,
         "roofline": {"bound": "mfma", "kernel": f"implicit-GEMM conv family (fwd/dgrad igemm + wgrad, {dtype} operands)",
                      "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
@@ -295,6 +352,12 @@ def main():
     ap.add_argument("--graph", action="store_true",
                     help="single process: replay the whole train step as one hipGraph after the autotuned warm-up")
     ap.add_argument("--tuning-report", default=None, help="write the GEMM autotuner's choices to this file")
+    ap.add_argument("--tune-db", default=os.path.join(ROOT, "profiles", "tune_db.txt"),
+                    help="GEMM choices to replay (the committed database the full-size tests load too); shapes it "
+                         "does not hold are tuned live")
+    ap.add_argument("--retune", action="store_true", help="ignore --tune-db: time every GEMM variant afresh")
+    ap.add_argument("--tune-db-out", default=None, help="save the process's GEMM choices to this file at the end")
+    ap.add_argument("--no-extras", action="store_true", help="skip the farm (configs[3]) and c5 (configs[4]) legs")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (ranks may share a GPU; rehearsal only)")
     args = ap.parse_args()
@@ -315,10 +378,29 @@ def main():
             dist.init_process_group(args.dist_backend)
         pg = dist.group.WORLD
 
+    from unet_amd import _lib as _ulib
+    lib = _ulib.load()
+    ident = _ulib.build_identity()
+    tune_db_entries = 0
+    if not args.retune and args.tune_db and os.path.exists(args.tune_db):
+        tune_db_entries = lib.unet_tuning_load(args.tune_db.encode())
+        if tune_db_entries < 0:
+            raise RuntimeError(f"unet_tuning_load({args.tune_db}) failed: {tune_db_entries}")
+
     main_res = run_precision(args, args.dtype, device, pg, world, rank)
     extras = {}
     for d in [d for d in args.extra_dtypes.split(",") if d and d != args.dtype]:
         extras[d] = run_precision(args, d, device, pg, world, rank)
+    farm, c5 = {}, None
+    if not args.no_extras and args.size == 512 and args.channels == 1 and args.batch == 8:
+        # configs[4]: 3-ch 572^2, batch 8 per GPU, bf16 train step
+        c5_args = argparse.Namespace(**{**vars(args), "channels": 3, "size": 572,
+                                        "steps": max(5, args.steps // 2), "warmup": max(3, args.warmup // 2)})
+        c5 = run_precision(c5_args, "bf16", device, pg, world, rank)
+        c5["steps"] = c5_args.steps
+        if world == 1:  # configs[3] farms tiles over GPUs with no collective: one GPU's rate x N
+            for d in ("fp32", "bf16"):
+                farm[d] = run_farm(args, d, device)
 
     if rank == 0:
         comm = f" + {'RCCL' if args.dist_backend == 'nccl' else 'gloo'} all-reduce" if world > 1 else ""
@@ -341,19 +423,32 @@ def main():
                        "global_batch": world * args.batch, "image": args.size,
                        "parallelism": f"dp{world}"},
         }
-        for k in ("roofline", "bottleneck", "stage1", "kernels", "final_loss"):
+        for k in ("mean_ms_per_step", "wall_value", "step_ms_range", "roofline", "bottleneck", "stage1", "kernels",
+                  "final_loss"):
             out[k] = main_res[k]
+        out["lib"] = {**ident, "tune_db": os.path.relpath(args.tune_db, ROOT) if tune_db_entries > 0 else None,
+                      "tune_db_entries": tune_db_entries}
         if main_res["comm"] is not None:
             out["comm"] = main_res["comm"]
         for d, r in extras.items():
             out[d] = {"value": r["value"], "unit": "images/s", "ms_per_step": r["ms_per_step"],
+                      "mean_ms_per_step": r["mean_ms_per_step"],
                       "config": f"same workload, {GEMM_DESC[d]} GEMMs (global batch {world * args.batch}"
                                 f"{'; configs[2] at N=8' if d == 'bf16' else ''})",
                       **{k: r[k] for k in ("roofline", "bottleneck", "stage1", "kernels", "final_loss")}}
+        if c5 is not None:
+            out["c5"] = {"value": c5["value"], "unit": "images/s", "ms_per_step": c5["ms_per_step"],
+                         "steps": c5["steps"], "dtype": "bf16",
+                         "config": f"configs[4]: U-Net train step 572x572x3 (388x388 out), batch {args.batch}/GPU, "
+                                   "bf16-operand/fp32-acc GEMMs: fwd + weighted CE + bwd + SGD(0.99), synthetic",
+                         **{k: c5[k] for k in ("roofline", "bottleneck", "kernels", "final_loss")}}
+        if farm:
+            out["farm"] = farm
         if args.tuning_report:
-            from unet_amd import _lib as _ulib
             with open(args.tuning_report, "w") as f:
                 f.write(_ulib.tuning_report())
+        if args.tune_db_out:
+            lib.unet_tuning_save(args.tune_db_out.encode())
         if not args.no_iou and args.channels == 1:
             out["iou"] = hela_iou(device, args.dtype)
             if "bf16" in extras and out["iou"] is not None:

@@ -38,6 +38,9 @@ extern "C" {
 
 typedef void* unet_stream_t; /* hipStream_t */
 
+/* "unet_hip <ver> gfx950 ... src <hash>": <hash> = the first 16 hex digits of
+ * sha256 over the library's sources (csrc/Makefile SRC_HASH), so a run's record
+ * shows which sources the loaded .so was built from. */
 const char* unet_version(void);
 const char* unet_last_error(void);
 
@@ -49,8 +52,11 @@ const char* unet_last_error(void);
 typedef struct unet_plan unet_plan;
 
 /* Create a plan; returns NULL (and sets unet_last_error) for sizes the valid
- * U-Net cannot take (models/unet_model.py:189: out = in - 184 for clean sizes).
- * unet_plan_create() is unet_plan_create_ex(..., UNET_PREC_FP32). */
+ * U-Net cannot take (models/unet_model.py:189: out = in - 184 for clean sizes)
+ * and for c_in outside 1..16 or n_classes outside 1..32 (the reference's
+ * UNet(n_channels, n_classes), models/unet_model.py:66-85, takes any counts;
+ * the first conv's direct kernel and the register-blocked head / loss bound
+ * them here).  unet_plan_create() is unet_plan_create_ex(..., UNET_PREC_FP32). */
 unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes);
 
 /* Arithmetic of the implicit-GEMM convolutions (the 17 3x3 convs after the
@@ -68,7 +74,7 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes);
  *                  fp32 accumulation; the dropped lo*lo' is <= 2^-16 of the
  *                  product).  Storage as in UNET_PREC_FP32; tested against the
  *                  fp64 oracle at the fp32 tolerances.
- * Everything else -- the first conv (Ci <= 4), the 1x1 head, BatchNorm, the
+ * Everything else -- the first conv (Ci <= 16), the 1x1 head, BatchNorm, the
  * loss, gradients and the optimizer -- is fp32 in all three; UNET_PREC_BF16
  * plans also store the GEMM-only tensors and the raw conv outputs in bf16. */
 enum { UNET_PREC_FP32 = 0, UNET_PREC_BF16 = 1, UNET_PREC_BF16X3 = 2 };
@@ -109,6 +115,21 @@ int unet_plan_segment_grads(const unet_plan* p, int seg, int* first_grad, int* n
 int unet_plan_backward(unet_plan* p, void* const* host_params, void* const* host_grads,
                        const float* x_nchw, const float* dlogits_nchw, void* workspace,
                        int seg_begin, int seg_end, unet_stream_t stream);
+/* The same with flags.  UNET_BWD_DEFER_JOIN: the weight gradients of these
+ * segments (which run on the plan's side stream beside the input-gradient
+ * chain once the plan is tuned) are NOT joined into `stream` on return, so the
+ * next segment's input gradients overlap them; a collective over segment s's
+ * gradients must first make its stream wait with unet_plan_wait_segment(s),
+ * and unet_plan_join() must be called on `stream` before anything reads the
+ * gradients or the workspace again (optimizer step, next forward).  This is
+ * the data-parallel schedule (unet_amd/train.py): all-reduce bucket s while
+ * segment s+1 computes. */
+enum { UNET_BWD_DEFER_JOIN = 1 };
+int unet_plan_backward_ex(unet_plan* p, void* const* host_params, void* const* host_grads,
+                          const float* x_nchw, const float* dlogits_nchw, void* workspace,
+                          int seg_begin, int seg_end, int flags, unet_stream_t stream);
+int unet_plan_wait_segment(unet_plan* p, int seg, unet_stream_t stream);
+int unet_plan_join(unet_plan* p, unet_stream_t stream);
 
 /* Optional per-kernel timing of the next forward/backward: the plan records a
  * hipEvent pair around each launch (class ids below).  unet_plan_timing()
@@ -134,7 +155,11 @@ int unet_plan_timing_mfma_flops(const unet_plan* p, double* mfma_flops);
  * logits (N, K, H, W) contiguous; targets int64 and weights float32 are read
  * through element strides (the caller's center-cropped views,
  * scripts/train.py:118-126, need no copy).  Writes loss (1 float) and
- * dlogits = w*(softmax - onehot)/(N*H*W) * grad_scale.  ws: 64*8 bytes. */
+ * dlogits = w*(softmax - onehot)/(N*H*W) * grad_scale.  ws: 64*8 bytes; on
+ * return-to-host ws[1] (double) is 1 if a target was outside [0, k) and not
+ * ignore_index -100 (such pixels contribute nothing), ws[2] one such target:
+ * torch's nn.CrossEntropyLoss raises for them (utils/losses.py:27), the caller
+ * checks the flag at its next synchronisation point.  1 <= k <= 32. */
 int unet_wce_fwd_bwd(const float* logits, const int64_t* targets, const float* weights,
                      int n, int k, int h, int w,
                      const int64_t* t_strides /*host, 3*/, const int64_t* w_strides /*host, 3*/,

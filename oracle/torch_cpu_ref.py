@@ -38,8 +38,16 @@ def _crop(t, th, tw):
 
 
 class TorchCpuUNet:
-    def __init__(self, params, n_channels=1, n_classes=2):
-        self.p = {k: torch.from_numpy(np.array(v, copy=True)) for k, v in params.items()}
+    """``dtype=torch.float64`` is the reference's own fp64 run (the golden
+    fixtures' arithmetic: tests/golden/make_golden.py runs the reference module
+    in float64 on the same torch CPU kernels); the GPU parity tests use it as the
+    full-tensor oracle at 512^2, where a NumPy fp64 run would take minutes."""
+
+    def __init__(self, params, n_channels=1, n_classes=2, dtype=torch.float32):
+        self.p = {}
+        for k, v in params.items():
+            t = torch.from_numpy(np.array(v, copy=True))
+            self.p[k] = t.to(dtype) if t.is_floating_point() else t
         for k, v in self.p.items():
             if v.is_floating_point() and not O.is_buffer(k):
                 v.requires_grad_(True)
@@ -99,3 +107,23 @@ def train_steps_per_second(batch, size=512, seconds=10.0, max_steps=3, threads=N
         if el > seconds or steps >= max_steps:
             break
     return batch * steps / el, steps, el
+
+
+def train_step_times(batch, steps, size=512, seed=0):
+    """Per-step wall times (s) of `steps` scripts/train.py steps at
+    batch x 1 x size^2 on this host (the optimizer state carries over)."""
+    from . import fixtures as Fx
+    params = O.hash_init(1, 2, seed=seed)
+    net = TorchCpuUNet(params)
+    x, t, w = Fx.make_inputs(seed, batch, 1, size)
+    x, t, w = torch.from_numpy(x), torch.from_numpy(t), torch.from_numpy(w)
+    opt = torch.optim.SGD(net.parameters(), lr=1e-4, momentum=0.99)
+    times = []
+    for _ in range(steps):
+        t0 = time.perf_counter()
+        opt.zero_grad()
+        loss = weighted_ce(net.forward(x), t, w)
+        loss.backward()
+        opt.step()
+        times.append(time.perf_counter() - t0)
+    return batch, times

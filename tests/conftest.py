@@ -1,11 +1,33 @@
 import os
 import sys
 
+import pytest
+
 ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 PKG = os.path.join(ROOT, "unet-segmentation_amd")
-for p in (ROOT, PKG):
+HERE = os.path.dirname(os.path.abspath(__file__))
+for p in (ROOT, PKG, HERE):
     if p not in sys.path:
         sys.path.insert(0, p)
+# the GEMM choices bench.py timed (bench.py --tune-db-out); full-size tests load
+# them so that they check the benchmarked kernel mix
+TUNE_DB = os.path.join(ROOT, "profiles", "tune_db.txt")
+
+
+@pytest.fixture(scope="module")
+def bench_tuning():
+    """Load profiles/tune_db.txt into the library's tuning cache (shapes it does
+    not hold are tuned live); reset the cache afterwards."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    from unet_amd import _lib
+    lib = _lib.load()
+    lib.unet_tuning_reset()
+    n = lib.unet_tuning_load(TUNE_DB.encode()) if os.path.exists(TUNE_DB) else 0
+    print(f"tuning database: {n} entries ({_lib.build_identity()})")
+    yield n
+    lib.unet_tuning_reset()
 
 
 def pytest_configure(config):

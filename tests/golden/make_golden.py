@@ -158,6 +158,37 @@ def full_size_train_case(tag, n, h, n_channels=1, seed=5):
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
+def bf16_oracle_case(tag, n, h, n_channels=1, seed=5):
+    """The bf16 arithmetic's own distance from the reference (configs[2] and
+    configs[4]: bf16-in / fp32-acc GEMMs): the NumPy restatement with the HIP
+    bf16 plan's roundings (UNetOracle(gemm="bf16"), every product and sum in
+    fp64) on the inputs of ``train_{tag}.npz``.  Its gradient digests
+    (gbf16norm/, gbf16val/ at the same sample indices), loss, logit sample and
+    mask give the GPU bf16 tests their per-tensor floor: a bf16 run may sit as
+    far from the reference as bf16 rounding itself puts it (bf16
+    cannot be argmax-exact).  Written to ``train_{tag}_bf16.npz``."""
+    params = O.hash_init(n_channels, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, n_channels, h)
+    net = O.UNetOracle(params, gemm="bf16")
+    lg, cache, nb = net.forward(x)
+    loss, dl = O.weighted_ce(lg, tgt, wmap)
+    g = net.backward(dl, cache)
+    del cache
+    out = {"x_seed": np.array(seed), "n": np.array(n), "h": np.array(h), "c": np.array(n_channels),
+           "loss": np.array(loss), "logits_sample": lg[:, :, ::7, ::5].copy(),
+           "mask": np.packbits(lg[:, 1] > lg[:, 0], axis=-1)}
+    for name in g:
+        v = np.asarray(g[name], np.float64).ravel()
+        out[f"gbf16norm/{name}"] = np.array(np.linalg.norm(v))
+        out[f"gbf16val/{name}"] = v[F.sample_indices(name, v.size)]
+    for k, v in nb.items():
+        if "running" in k:
+            out[f"buf/{k}"] = np.asarray(v, np.float64)
+    path = os.path.join(HERE, f"train_{tag}_bf16.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes")
+
+
 def hela_stitch_1024():
     """configs[3]'s 1024^2 input: a 2x2 stitch of DIC-C2DH-HeLa 01 frames
     t000-t003 (the reference's 1024^2 demo, images/phase5 5.png, is such a
@@ -414,6 +445,11 @@ if __name__ == "__main__":
         full_size_train_case("n2_512", 2, 512, seed=5)
     if "t512b8" in which:  # the bench configuration (configs[1]): batch 8 x 512^2
         full_size_train_case("n8_512", 8, 512, seed=6)
+    if "t572c3" in which:  # configs[4]: 3-ch 572^2 train step (fwd + bwd), batch 2
+        full_size_train_case("n2_c3_572", 2, 572, n_channels=3, seed=7)
+    if "bf16" in which:  # the bf16 roundings' own floor for the bf16 tests at size
+        bf16_oracle_case("n8_512", 8, 512, seed=6)
+        bf16_oracle_case("n2_c3_572", 2, 572, n_channels=3, seed=7)
     if "farm" in which:
         tile_farm_case()
     if "hela_train" in which:

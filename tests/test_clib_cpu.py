@@ -164,3 +164,31 @@ def test_host_sanitizer_selftest():
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1", UBSAN_OPTIONS="halt_on_error=1"))
     assert r.returncode == 0, r.stdout + r.stderr
     assert "all checks passed" in r.stdout
+
+
+def test_plan_takes_reference_channel_and_class_counts():
+    """UNet(n_channels, n_classes) takes any counts in the reference
+    (models/unet_model.py:66-85); the plan takes 1..16 input channels and 1..32
+    classes (the first conv's direct kernel, the register-blocked head / loss)."""
+    from unet_amd import UNet
+    from unet_amd.plan import Plan
+    _lib()
+    for c, k in ((5, 5), (16, 32), (3, 9)):
+        p = Plan(1, c, 188, 188, k)
+        assert (p.out_h, p.out_w) == (4, 4)
+        m = UNet(c, k)
+        assert m.outc.conv.weight.shape == (k, 64, 1, 1) and m.inc.double_conv[0].weight.shape[1] == c
+    for c, k in ((17, 2), (1, 33)):
+        with pytest.raises(ValueError):
+            Plan(1, c, 188, 188, k)
+        with pytest.raises(ValueError):
+            UNet(c, k)
+
+
+def test_library_built_from_this_tree():
+    """unet_version() carries the hash of the sources the .so was built from
+    (csrc/Makefile SRC_HASH); it must equal the hash of the tree's sources."""
+    L = _lib()
+    ident = L.build_identity()
+    assert ident["src_match"], ident
+

@@ -147,7 +147,7 @@ def _bf16_worker(rank, world, port, q):
 
 @pytest.mark.timeout(300)
 def test_bf16_bucket_allreduce():
-    """comm_dtype=bf16 (the bf16 plans' default): each bucket goes over the wire
+    """comm_dtype=bf16 (opt-in): each bucket goes over the wire
     as bf16 and comes back widened; equals the bf16 sum of the bf16-rounded
     shards, identical on both ranks."""
     import torch

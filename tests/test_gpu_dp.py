@@ -118,7 +118,7 @@ def test_two_rank_trainer_matches_shard_average(tmp_path, overlap):
 
 
 def test_two_rank_trainer_bf16_gradient_allreduce(tmp_path):
-    """comm_dtype=bf16 (default of the bf16 plans): the buckets travel as bf16.
+    """comm_dtype=bf16 (opt-in): the buckets travel as bf16.
     Both ranks end identical; the first step's all-reduced gradient equals the
     fp32 shard sum to bf16 rounding (each shard and the sum rounded once:
     rel-L2 well under 2^-7)."""

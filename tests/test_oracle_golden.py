@@ -139,6 +139,35 @@ def test_whole_model_vs_reference(tag):
     np.testing.assert_allclose(le, z["logits_eval"], rtol=1e-9, atol=1e-10)
 
 
+def test_torch_cpu_restatement_fp64_vs_reference():
+    """oracle/torch_cpu_ref.py in float64 (the full-tensor oracle of the 512^2
+    GPU test and the CPU baseline's arithmetic) reproduces the reference's fp64
+    fixture: logits, loss and every gradient digest."""
+    import torch
+    from oracle import torch_cpu_ref as R
+    z = _load("model_n2_188.npz")
+    seed, n, h = int(z["x_seed"]), int(z["n"]), int(z["h"])
+    params = O.hash_init(1, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
+    net = R.TorchCpuUNet(params, dtype=torch.float64)
+    lg = net.forward(torch.from_numpy(x).double())
+    loss = R.weighted_ce(lg, torch.from_numpy(tgt), torch.from_numpy(wmap).double())
+    loss.backward()
+    np.testing.assert_allclose(lg.detach().numpy(), z["logits"], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(loss.item(), z["loss"], rtol=1e-12)
+    for name, p in net.p.items():
+        if not p.requires_grad:
+            continue
+        g = p.grad.numpy().ravel()
+        ref = float(z[f"gnorm/{name}"])
+        if O.bn_cancelled(name):  # analytically zero: fp64 noise on both sides
+            assert np.abs(g).max() < 1e-9 and ref < 1e-9, name
+            continue
+        assert abs(np.linalg.norm(g) - ref) <= 1e-9 * max(ref, 1e-30) + 1e-13, name
+        np.testing.assert_allclose(g[z[f"gidx/{name}"]], z[f"gval/{name}"], rtol=1e-8, atol=1e-12 * ref + 1e-14,
+                                   err_msg=name)
+
+
 def test_sgd_trajectory_vs_reference():
     z = _load("model_n2_188.npz")
     seed, n, h = int(z["x_seed"]), int(z["n"]), int(z["h"])

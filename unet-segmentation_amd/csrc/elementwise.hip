@@ -117,7 +117,7 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict_
 // bf16 (bf16 plans).
 template <int CI, int FUSED = 0, int Y16 = 0, int Z16 = 0>
 __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restrict__ x, int nimg, int h, int w,
-                                                          Src dy, float* __restrict__ dw,
+                                                          Src dy, float* __restrict__ dw, int ci_tot, int ci_off,
                                                           const float* __restrict__ yr = nullptr,
                                                           const float* __restrict__ coef = nullptr) {
   constexpr int RB = 4, PX = 64, TW = PX + 2;
@@ -147,7 +147,7 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restric
     for (int i = tid; i < CI * (RB + 2) * TW; i += 256) {
       const int ci = i / ((RB + 2) * TW), rem = i - ci * (RB + 2) * TW, r = rem / TW, cx = rem - r * TW;
       const int gx = min(x0 + cx, w - 1), gy = min(r0 + r, h - 1);
-      tile[ci][r][cx] = x[((size_t)(n * CI + ci) * h + gy) * w + gx];
+      tile[ci][r][cx] = x[((size_t)(n * ci_tot + ci_off + ci) * h + gy) * w + gx];
     }
     __syncthreads();
     // RB*PX = 256 pixels, 16 per slot, in two batches of 8 loads
@@ -220,8 +220,12 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restric
 // out[i] += sum_{b in chunk} slabs[b][i]: block (word group of 64, chunk of
 // 64 slabs); 4 waves each sum 16 slabs of the same 64 words (256-B coalesced
 // rows), then one atomic per word per block (out zeroed by the launcher).
+// Destination word of slab word w: (w / rowlen) * rowstride + rowoff + w % rowlen
+// (an input-channel group of a Ci > 4 first conv lands in its columns of
+// dW[co][ci][3][3]).
 __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ slabs, int nslab, int n,
-                                                      float* __restrict__ out) {
+                                                      float* __restrict__ out, int rowlen, int rowstride,
+                                                      int rowoff) {
   const int w = blockIdx.x * 64 + (threadIdx.x & 63);
   const int b0 = blockIdx.y * 64;
   const int b1 = min(nslab, b0 + 64);
@@ -231,13 +235,80 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ 
   __shared__ float red[4][64];
   red[threadIdx.x >> 6][threadIdx.x & 63] = s;
   __syncthreads();
-  if (threadIdx.x < 64 && w < n) atomicAdd(out + w, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                                        red[3][threadIdx.x]);
+  if (threadIdx.x < 64 && w < n)
+    atomicAdd(out + (w / rowlen) * rowstride + rowoff + w % rowlen,
+              red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] + red[3][threadIdx.x]);
+}
+
+// n_channels > 4 (models/unet_model.py:66 takes any count): the same direct
+// conv with the input-channel count at run time (<= kFirstMaxCi), the 64 x Ci
+// x 9 weights in LDS instead of registers.  Not on the benchmarked path.
+constexpr int kFirstMaxCi = 16;
+template <int H16>
+__global__ __launch_bounds__(256) void k_conv_first_fwd_gen(const float* __restrict__ x, int ci_n, int h, int w,
+                                                            const float* __restrict__ wt,
+                                                            const float* __restrict__ bias, float* __restrict__ y,
+                                                            double* __restrict__ stats) {
+  const int ho = h - 2, wo = w - 2;
+  const int x0 = blockIdx.x * 64, row = blockIdx.y, n = blockIdx.z;
+  __shared__ float tile[kFirstMaxCi][3][66];
+  __shared__ float wl[kFirstMaxCi * 9][64];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < ci_n * 3 * 66; i += 256) {
+    const int ci = i / 198, rem = i - ci * 198, r = rem / 66, cx = rem - r * 66;
+    const int gx = min(x0 + cx, w - 1);
+    tile[ci][r][cx] = x[((size_t)(n * ci_n + ci) * h + row + r) * w + gx];
+  }
+  for (int i = tid; i < ci_n * 9 * 64; i += 256) {
+    const int c = i / (ci_n * 9), k = i - c * (ci_n * 9);
+    wl[k][c] = wt[i];
+  }
+  const int c = tid & 63, q = tid >> 6;
+  const float b = bias[c];
+  __syncthreads();
+  float s1 = 0.f, s2 = 0.f;
+  for (int j = 0; j < 16; ++j) {
+    const int px = q + 4 * j;
+    const int gx = x0 + px;
+    float acc = b;
+    for (int ci = 0; ci < ci_n; ++ci)
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) acc = fmaf(tile[ci][ky][px + kx], wl[(ci * 3 + ky) * 3 + kx][c], acc);
+    if (gx < wo) {
+      const size_t yi = ((size_t)(n * ho + row) * wo + gx) * 64 + c;
+      if (H16) {
+        acc = round_bf(acc);
+        reinterpret_cast<uint16_t*>(y)[yi] = bf16_of(acc);
+      } else {
+        y[yi] = acc;
+      }
+      s1 += acc;
+      s2 += acc * acc;
+    }
+  }
+  if (stats == nullptr) return;
+  __shared__ float red[4][2][64];
+  red[q][0][c] = s1;
+  red[q][1][c] = s2;
+  __syncthreads();
+  if (tid < 64) {
+    const float a = red[0][0][tid] + red[1][0][tid] + red[2][0][tid] + red[3][0][tid];
+    const float bb = red[0][1][tid] + red[1][1][tid] + red[2][1][tid] + red[3][1][tid];
+    const int grp = (blockIdx.x + blockIdx.y * gridDim.x) % kStatGroups;
+    atomicAdd(stats + ((size_t)grp * 64 + tid) * 2 + 0, (double)a);
+    atomicAdd(stats + ((size_t)grp * 64 + tid) * 2 + 1, (double)bb);
+  }
 }
 
 template <int H16>
 static void conv_first_go(dim3 grid, int ci, const float* x, int h, int w, const float* wt, const float* bias, float* y,
                           double* stats, hipStream_t s) {
+  if (ci > 4) {
+    hipLaunchKernelGGL((k_conv_first_fwd_gen<H16>), grid, dim3(256), 0, s, x, ci, h, w, wt, bias, y, stats);
+    return;
+  }
   switch (ci) {
     case 1: hipLaunchKernelGGL((k_conv_first_fwd<1, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
     case 2: hipLaunchKernelGGL((k_conv_first_fwd<2, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
@@ -248,48 +319,51 @@ static void conv_first_go(dim3 grid, int ci, const float* x, int h, int w, const
 
 hipError_t launch_conv_first_fwd(const float* x, int n, int ci, int h, int w, const float* wt,
                                  const float* bias, int co, float* y, double* stats, hipStream_t s, int out_h16) {
-  if (co != 64 || ci < 1 || ci > 4 || h < 3 || w < 3) return hipErrorInvalidValue;
+  if (co != 64 || ci < 1 || ci > kFirstMaxCi || h < 3 || w < 3) return hipErrorInvalidValue;
   dim3 grid(cdiv(w - 2, 64), h - 2, n);
   if (out_h16) conv_first_go<1>(grid, ci, x, h, w, wt, bias, y, stats, s);
   else conv_first_go<0>(grid, ci, x, h, w, wt, bias, y, stats, s);
   return hipGetLastError();
 }
 
-hipError_t reduce_first_slabs(int ci, int grid, float* dw, const float* slabs, hipStream_t s);
+// slabs of one pass of <= 4 input channels (passes reuse the region in stream order)
+size_t conv_first_wgrad_ws_bytes(int ci) { return sizeof(float) * (size_t)kFirstWgradSlabs * (ci < 4 ? ci : 4) * 9 * 64; }
 
-size_t conv_first_wgrad_ws_bytes(int ci) { return sizeof(float) * (size_t)kFirstWgradSlabs * ci * 9 * 64; }
-
-hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, const Src& dy, int co,
-                                   float* dw, float* slabs, hipStream_t s) {
-  if (co != 64 || ci < 1 || ci > 4) return hipErrorInvalidValue;
-  const long long items = (long long)n * cdiv(h - 2, 4) * cdiv(w - 2, 64);
-  const int grid = (int)(items < kFirstWgradSlabs ? items : kFirstWgradSlabs);
-  switch (ci) {
-    case 1: hipLaunchKernelGGL(k_conv_first_wgrad<1>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
-    case 2: hipLaunchKernelGGL(k_conv_first_wgrad<2>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
-    case 3: hipLaunchKernelGGL(k_conv_first_wgrad<3>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
-    default: hipLaunchKernelGGL(k_conv_first_wgrad<4>, dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs); break;
-  }
-  return reduce_first_slabs(ci, grid, dw, slabs, s);
-}
-
-hipError_t reduce_first_slabs(int ci, int grid, float* dw, const float* slabs, hipStream_t s) {
-  const int nw = ci * 9 * 64;
-  hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * nw, s);
-  if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(nw, 64), cdiv(grid, 64)), dim3(256), 0, s, slabs, grid, nw, dw);
+// sum the pass's slabs into its columns [ci_off * 9, (ci_off + cp) * 9) of dW[64][ci_tot * 9]
+static hipError_t reduce_first_slabs(int cp, int ci_tot, int ci_off, int grid, float* dw, const float* slabs,
+                                     hipStream_t s) {
+  const int nw = cp * 9 * 64;
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(nw, 64), cdiv(grid, 64)), dim3(256), 0, s, slabs, grid, nw, dw, cp * 9,
+                     ci_tot * 9, ci_off * 9);
   return hipGetLastError();
 }
 
+// One launch per group of <= 4 input channels (models/unet_model.py:66 takes
+// any n_channels; the register accumulators hold 4 x 9 x 4 weights per thread).
 template <int FUSED, int Y16, int Z16 = 0>
-static void first_wgrad_go(int grid, int ci, const float* x, int n, int h, int w, const Src& dy, float* slabs,
-                           const float* y, const float* coef, hipStream_t s) {
-  switch (ci) {
-    case 1: hipLaunchKernelGGL((k_conv_first_wgrad<1, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
-    case 2: hipLaunchKernelGGL((k_conv_first_wgrad<2, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
-    case 3: hipLaunchKernelGGL((k_conv_first_wgrad<3, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
-    default: hipLaunchKernelGGL((k_conv_first_wgrad<4, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, y, coef); break;
+static hipError_t first_wgrad_run(int ci, const float* x, int n, int h, int w, const Src& dy, float* dw, float* slabs,
+                                  const float* y, const float* coef, hipStream_t s) {
+  const long long items = (long long)n * cdiv(h - 2, 4) * cdiv(w - 2, 64);
+  const int grid = (int)(items < kFirstWgradSlabs ? items : kFirstWgradSlabs);
+  hipError_t e = hipMemsetAsync(dw, 0, sizeof(float) * (size_t)ci * 9 * 64, s);
+  if (e != hipSuccess) return e;
+  for (int c0 = 0; c0 < ci; c0 += 4) {
+    const int cp = ci - c0 < 4 ? ci - c0 : 4;
+    switch (cp) {
+      case 1: hipLaunchKernelGGL((k_conv_first_wgrad<1, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, ci, c0, y, coef); break;
+      case 2: hipLaunchKernelGGL((k_conv_first_wgrad<2, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, ci, c0, y, coef); break;
+      case 3: hipLaunchKernelGGL((k_conv_first_wgrad<3, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, ci, c0, y, coef); break;
+      default: hipLaunchKernelGGL((k_conv_first_wgrad<4, FUSED, Y16, Z16>), dim3(grid), dim3(256), 0, s, x, n, h, w, dy, slabs, ci, c0, y, coef); break;
+    }
+    if ((e = reduce_first_slabs(cp, ci, c0, grid, dw, slabs, s)) != hipSuccess) return e;
   }
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, const Src& dy, int co,
+                                   float* dw, float* slabs, hipStream_t s) {
+  if (co != 64 || ci < 1 || ci > kFirstMaxCi) return hipErrorInvalidValue;
+  return first_wgrad_run<0, 0>(ci, x, n, h, w, dy, dw, slabs, nullptr, nullptr, s);
 }
 
 // inc.c0 weight gradient straight from the BN0 backward (dz, saved y, coef):
@@ -297,21 +371,15 @@ static void first_wgrad_go(int grid, int ci, const float* x, int n, int h, int w
 hipError_t launch_conv_first_wgrad_bn(const float* x, int n, int ci, int h, int w, const float* dz, const float* y,
                                       int y_h16, const float* coef, int co, float* dw, float* slabs, hipStream_t s,
                                       int dz_h16) {
-  if (co != 64 || ci < 1 || ci > 4) return hipErrorInvalidValue;
-  const long long items = (long long)n * cdiv(h - 2, 4) * cdiv(w - 2, 64);
-  const int grid = (int)(items < kFirstWgradSlabs ? items : kFirstWgradSlabs);
+  if (co != 64 || ci < 1 || ci > kFirstMaxCi) return hipErrorInvalidValue;
   Src d;
   d.ptr = dz;
   d.H = h - 2;
   d.W = w - 2;
   d.C = 64;
-  if (y_h16 && dz_h16)
-    first_wgrad_go<1, 1, 1>(grid, ci, x, n, h, w, d, slabs, y, coef, s);
-  else if (y_h16)
-    first_wgrad_go<1, 1>(grid, ci, x, n, h, w, d, slabs, y, coef, s);
-  else
-    first_wgrad_go<1, 0>(grid, ci, x, n, h, w, d, slabs, y, coef, s);
-  return reduce_first_slabs(ci, grid, dw, slabs, s);
+  if (y_h16 && dz_h16) return first_wgrad_run<1, 1, 1>(ci, x, n, h, w, d, dw, slabs, y, coef, s);
+  if (y_h16) return first_wgrad_run<1, 1>(ci, x, n, h, w, d, dw, slabs, y, coef, s);
+  return first_wgrad_run<1, 0>(ci, x, n, h, w, d, dw, slabs, y, coef, s);
 }
 
 // ---------------------------------------------------------------------------
@@ -676,15 +744,20 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
 // OutConv 1x1 head (models/unet_model.py:56-63): logits[n][k][y][x] =
 // b[k] + sum_c W[k][c] * relu(bn(y))[c].  16 lanes per pixel (C = 64).
 // ---------------------------------------------------------------------------
+// K: class capacity of the instantiation, kn <= K the model's classes (the
+// first 4 counts have their own instantiations; 5-8, 9-16 share one).  A pass
+// writes classes koff .. koff + kn - 1 of ktot (more than 16 classes: one pass
+// per 16, a lane per class in the 16-lane pixel group).
 template <int K>
 __global__ __launch_bounds__(256) void k_head_fwd(Src s, int n, int h, int w, const float* __restrict__ wt,
-                                                  const float* __restrict__ bias, float* __restrict__ logits) {
+                                                  const float* __restrict__ bias, float* __restrict__ logits, int kn,
+                                                  int koff, int ktot) {
   const int tid = threadIdx.x, sub = tid & 15;
   const long long pixels = (long long)n * h * w;
   const int c = sub * 4;
   float4 wk[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) wk[k] = ld4(wt + k * 64 + c);
+  for (int k = 0; k < K; ++k) wk[k] = k < kn ? ld4(wt + (koff + k) * 64 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   float4 sc = make_float4(1, 1, 1, 1), sf = make_float4(0, 0, 0, 0);
   if (s.scale) { sc = ld4(s.scale + c); sf = ld4(s.shift + c); }
   for (long long p = (long long)blockIdx.x * 16 + (tid >> 4); p < pixels; p += (long long)gridDim.x * 16) {
@@ -708,29 +781,29 @@ __global__ __launch_bounds__(256) void k_head_fwd(Src s, int n, int h, int w, co
 #pragma unroll
       for (int o = 8; o >= 1; o >>= 1) acc[k] += __shfl_xor(acc[k], o);
     }
-    if (sub < K) {
+    if (sub < kn) {
       float val = acc[0];
 #pragma unroll
       for (int k = 1; k < K; ++k)
         if (sub == k) val = acc[k];
-      logits[(((size_t)nn * K + sub) * h + yy) * w + xx] = val + bias[sub];
+      logits[(((size_t)nn * ktot + koff + sub) * h + yy) * w + xx] = val + bias[koff + sub];
     }
   }
 }
 
 // head backward: dz = W^T dl masked by ReLU'(bn(y)) (+ BN-bwd stats), dW, db.
-template <int K>
+template <int K>  // class capacity; kn <= K classes (as k_head_fwd)
 __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict__ dl, int n, int h, int w,
                                                   const float* __restrict__ wt, const float* __restrict__ mean,
                                                   const float* __restrict__ invstd, float* __restrict__ dz,
                                                   double* __restrict__ bstats, double* __restrict__ acc_out,
-                                                  int dz16) {
+                                                  int dz16, int kn) {
   const int tid = threadIdx.x, sub = tid & 15;
   const long long pixels = (long long)n * h * w;
   const int c = sub * 4;
   float4 wk[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) wk[k] = ld4(wt + k * 64 + c);
+  for (int k = 0; k < K; ++k) wk[k] = k < kn ? ld4(wt + k * 64 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
   const float4 sc = ld4(s.scale + c), sf = ld4(s.shift + c), mu = ld4(mean + c), is = ld4(invstd + c);
   float dwa[K][4], dba[K];
 #pragma unroll
@@ -749,7 +822,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
                             : ld4(s.ptr + ii);
     float g[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) g[k] = dl[((size_t)nn * K + k) * hw + r];
+    for (int k = 0; k < K; ++k) g[k] = k < kn ? dl[((size_t)nn * kn + k) * hw + r] : 0.f;
     const float zx = fmaf(yv.x, sc.x, sf.x), zy = fmaf(yv.y, sc.y, sf.y), zz = fmaf(yv.z, sc.z, sf.z),
                 zw = fmaf(yv.w, sc.w, sf.w);
     float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -790,6 +863,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
   __shared__ float red[256][4];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
+    if (k >= kn) continue;  // uniform
 #pragma unroll
     for (int j = 0; j < 4; ++j) red[tid][j] = dwa[k][j];
     __syncthreads();
@@ -807,7 +881,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
     if (tid == 0) {
       float t = 0.f;
       for (int rr = 0; rr < 256; rr += 16) t += red[rr][0];
-      atomicAdd(acc_out + K * 64 + k, (double)t);
+      atomicAdd(acc_out + kn * 64 + k, (double)t);
     }
     __syncthreads();
   }
@@ -818,17 +892,26 @@ __global__ void k_d2f(const double* __restrict__ a, int n, float* __restrict__ o
   if (i < n) o[i] = (float)a[i];
 }
 
+// largest class count (models/unet_model.py:66 takes any; the register-blocked
+// head backward and loss hold K values per thread)
+constexpr int kMaxClasses = 32;
+static int class_capacity(int k) { return k <= 4 ? k : k <= 8 ? 8 : k <= 16 ? 16 : 32; }
+
 hipError_t launch_head_fwd(const Src& s, int n, int h, int w, int c, const float* wt, const float* bias, int k,
                            float* logits, hipStream_t st) {
-  if (c != 64) return hipErrorInvalidValue;
+  if (c != 64 || k < 1 || k > kMaxClasses) return hipErrorInvalidValue;
   const long long pixels = (long long)n * h * w;
   dim3 grid(grid_cap(pixels, 16 * 4, 8192));
-  switch (k) {
-    case 1: hipLaunchKernelGGL(k_head_fwd<1>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits); break;
-    case 2: hipLaunchKernelGGL(k_head_fwd<2>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits); break;
-    case 3: hipLaunchKernelGGL(k_head_fwd<3>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits); break;
-    case 4: hipLaunchKernelGGL(k_head_fwd<4>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits); break;
-    default: return hipErrorInvalidValue;
+  for (int k0 = 0; k0 < k; k0 += 16) {
+    const int kn = k - k0 < 16 ? k - k0 : 16;
+    switch (class_capacity(kn)) {
+      case 1: hipLaunchKernelGGL(k_head_fwd<1>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits, kn, k0, k); break;
+      case 2: hipLaunchKernelGGL(k_head_fwd<2>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits, kn, k0, k); break;
+      case 3: hipLaunchKernelGGL(k_head_fwd<3>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits, kn, k0, k); break;
+      case 4: hipLaunchKernelGGL(k_head_fwd<4>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits, kn, k0, k); break;
+      case 8: hipLaunchKernelGGL(k_head_fwd<8>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits, kn, k0, k); break;
+      default: hipLaunchKernelGGL(k_head_fwd<16>, grid, dim3(256), 0, st, s, n, h, w, wt, bias, logits, kn, k0, k); break;
+    }
   }
   return hipGetLastError();
 }
@@ -837,19 +920,21 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
                            const float* yraw, const float* mean, const float* invstd, float* dz, double* bstats,
                            float* dw, float* db, double* acc, hipStream_t st, int dz_h16) {
   (void)yraw;
-  if (c != 64) return hipErrorInvalidValue;
+  if (c != 64 || k < 1 || k > kMaxClasses) return hipErrorInvalidValue;
   const long long pixels = (long long)n * h * w;
   // 512 blocks: the per-block fp64 atomics (BN statistics, dW, db) bound this
   // kernel at larger grids (measured: 256 blocks 199 us, 512 146 us, 2048 236 us)
   dim3 grid(grid_cap(pixels, 16 * 8, 512));
   hipError_t me = hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
   if (me != hipSuccess) return me;
-  switch (k) {
-    case 1: hipLaunchKernelGGL(k_head_bwd<1>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16); break;
-    case 2: hipLaunchKernelGGL(k_head_bwd<2>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16); break;
-    case 3: hipLaunchKernelGGL(k_head_bwd<3>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16); break;
-    case 4: hipLaunchKernelGGL(k_head_bwd<4>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16); break;
-    default: return hipErrorInvalidValue;
+  switch (class_capacity(k)) {
+    case 1: hipLaunchKernelGGL(k_head_bwd<1>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
+    case 2: hipLaunchKernelGGL(k_head_bwd<2>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
+    case 3: hipLaunchKernelGGL(k_head_bwd<3>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
+    case 4: hipLaunchKernelGGL(k_head_bwd<4>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
+    case 8: hipLaunchKernelGGL(k_head_bwd<8>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
+    case 16: hipLaunchKernelGGL(k_head_bwd<16>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
+    default: hipLaunchKernelGGL(k_head_bwd<32>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
   }
   hipLaunchKernelGGL(k_d2f, dim3(cdiv(k * 64, 256)), dim3(256), 0, st, acc, k * 64, dw);
   hipLaunchKernelGGL(k_d2f, dim3(1), dim3(64), 0, st, acc + k * 64, k, db);
@@ -861,11 +946,16 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
 // loss = mean(w * (logsumexp(l) - l[t]));  dl = w*(softmax - onehot)/count.
 // targets/weights through element strides (the caller's cropped views).
 // ---------------------------------------------------------------------------
+// K: class capacity, kn <= K classes.  A label outside [0, kn) other than
+// ignore_index (-100) contributes nothing and raises a flag: acc[1] = 1,
+// acc[2] = the label (torch's nn.CrossEntropyLoss raises "Target t is out of
+// bounds"; the host reads the flag at its next synchronisation point instead of
+// synchronising every step).
 template <int K>
 __global__ __launch_bounds__(256) void k_wce(const float* __restrict__ lg, const int64_t* __restrict__ t,
                                              const float* __restrict__ wm, int n, int h, int w, int64_t ts0,
                                              int64_t ts1, int64_t ts2, int64_t ws0, int64_t ws1, int64_t ws2,
-                                             float* __restrict__ dl, float gscale, double* __restrict__ acc) {
+                                             float* __restrict__ dl, float gscale, double* __restrict__ acc, int kn) {
   const long long hw = (long long)h * w, total = (long long)n * hw;
   const double inv = 1.0 / (double)total;
   float local = 0.f;
@@ -876,7 +966,7 @@ __global__ __launch_bounds__(256) void k_wce(const float* __restrict__ lg, const
     const int yy = (int)(r / w), xx = (int)(r % w);
     float l[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) l[k] = lg[((size_t)nn * K + k) * hw + r];
+    for (int k = 0; k < K; ++k) l[k] = k < kn ? lg[((size_t)nn * kn + k) * hw + r] : -INFINITY;
     const int64_t tg = t[nn * ts0 + yy * ts1 + xx * ts2];
     const float wt = wm[nn * ws0 + yy * ws1 + xx * ws2];
     float mx = l[0];
@@ -884,9 +974,13 @@ __global__ __launch_bounds__(256) void k_wce(const float* __restrict__ lg, const
     for (int k = 1; k < K; ++k) mx = fmaxf(mx, l[k]);
     float se = 0.f, e[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) { e[k] = __expf(l[k] - mx); se += e[k]; }
+    for (int k = 0; k < K; ++k) { e[k] = k < kn ? __expf(l[k] - mx) : 0.f; se += e[k]; }
     const float lse = mx + __logf(se);
-    const bool valid = (tg >= 0 && tg < K);   // ignore_index (-100) -> 0 loss, 0 grad
+    const bool valid = (tg >= 0 && tg < kn);   // ignore_index (-100) -> 0 loss, 0 grad
+    if (!valid && tg != -100) {
+      acc[1] = 1.0;
+      acc[2] = (double)tg;
+    }
     float lt = 0.f;
 #pragma unroll
     for (int k = 0; k < K; ++k)
@@ -895,7 +989,8 @@ __global__ __launch_bounds__(256) void k_wce(const float* __restrict__ lg, const
     const float sc = valid ? (float)((double)wt * inv) * gscale : 0.f;
     const float rs = 1.f / se;
 #pragma unroll
-    for (int k = 0; k < K; ++k) dl[((size_t)nn * K + k) * hw + r] = sc * (e[k] * rs - (k == tg ? 1.f : 0.f));
+    for (int k = 0; k < K; ++k)
+      if (k < kn) dl[((size_t)nn * kn + k) * hw + r] = sc * (e[k] * rs - (k == tg ? 1.f : 0.f));
   }
   for (int o = 32; o >= 1; o >>= 1) local += __shfl_xor(local, o);
   __shared__ float red[4];
@@ -909,16 +1004,19 @@ __global__ void k_wce_final(const double* acc, double count, float* loss) { *los
 hipError_t launch_wce(const float* logits, const int64_t* t, const float* wm, int n, int k, int h, int w,
                       const int64_t* ts, const int64_t* wsd, float* loss, float* dlogits, float gscale, double* acc,
                       hipStream_t s) {
+  if (k < 1 || k > kMaxClasses) return hipErrorInvalidValue;
   const long long total = (long long)n * h * w;
   dim3 grid(grid_cap(total, 256 * 4, 2048));
-  hipError_t me = hipMemsetAsync(acc, 0, sizeof(double), s);
+  hipError_t me = hipMemsetAsync(acc, 0, 3 * sizeof(double), s);  // sum, bad-label flag, bad label
   if (me != hipSuccess) return me;
-  switch (k) {
-    case 1: hipLaunchKernelGGL(k_wce<1>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
-    case 2: hipLaunchKernelGGL(k_wce<2>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
-    case 3: hipLaunchKernelGGL(k_wce<3>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
-    case 4: hipLaunchKernelGGL(k_wce<4>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc); break;
-    default: return hipErrorInvalidValue;
+  switch (class_capacity(k)) {
+    case 1: hipLaunchKernelGGL(k_wce<1>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;
+    case 2: hipLaunchKernelGGL(k_wce<2>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;
+    case 3: hipLaunchKernelGGL(k_wce<3>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;
+    case 4: hipLaunchKernelGGL(k_wce<4>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;
+    case 8: hipLaunchKernelGGL(k_wce<8>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;
+    case 16: hipLaunchKernelGGL(k_wce<16>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;
+    default: hipLaunchKernelGGL(k_wce<32>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;
   }
   hipLaunchKernelGGL(k_wce_final, dim3(1), dim3(1), 0, s, acc, (double)total, loss);
   return hipGetLastError();

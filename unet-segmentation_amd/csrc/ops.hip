@@ -336,7 +336,7 @@ int unet_bn_train_bwd(const float* x, const float* dy, int n, int h, int w, int 
 int unet_wce_fwd_bwd(const float* logits, const int64_t* t, const float* wm, int n, int k, int h, int w,
                      const int64_t* ts, const int64_t* wsd, float* loss, float* dl, float gscale, void* ws,
                      unet_stream_t st) {
-  if (!ts || !wsd || k < 1 || k > 4) return -EINVAL;
+  if (!ts || !wsd || k < 1 || k > 32) return -EINVAL;
   OPCK(launch_wce(logits, t, wm, n, k, h, w, ts, wsd, loss, dl, gscale, reinterpret_cast<double*>(ws),
                   reinterpret_cast<hipStream_t>(st)));
   return 0;

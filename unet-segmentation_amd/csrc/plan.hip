@@ -26,6 +26,7 @@
 using namespace unet;
 
 namespace unet {
+extern int g_wino_max, g_wino_dgrad_max, g_wino_wgrad_max;  // igemm.hip (Winograd tile caps)
 // unet_set_tuning("autotune", v) or UNET_AUTOTUNE (default on)
 int g_autotune = getenv("UNET_AUTOTUNE") ? atoi(getenv("UNET_AUTOTUNE")) : 1;
 // unet_set_tuning("concurrent", v) or UNET_CONCURRENT (default on): weight
@@ -98,6 +99,12 @@ struct unet_plan {
   // backward (joined at the end of every backward call)
   hipStream_t side = nullptr;
   hipEvent_t ev_dy[18] = {}, ev_du[4] = {}, ev_join = nullptr;
+  // per backward segment: recorded on the side stream after the segment's
+  // weight gradients (UNET_BWD_DEFER_JOIN calls), waited on by the caller's
+  // collective stream (unet_plan_wait_segment)
+  hipEvent_t ev_seg[9] = {};
+  bool seg_on_side[9] = {};
+  bool side_pending = false;  // side-stream work not yet joined into a caller stream
   int bwd_full = 0;  // completed whole backward passes (the first one tunes, serially)
   Buf slab;          // split-K partial tiles (igemm sites the tuner splits)
   Buf wino;          // Winograd F(2x2, 3x3) / F(4x4, 3x3) scratch (fp32 plans; U, M, V of one GEMM)
@@ -248,22 +255,31 @@ int env_autotune() { return unet::g_autotune; }
 
 constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 
+// Version of the GEMM variant tables (tile ids and their kernels): part of every
+// tuning key, so a database written by a build with another tile set is never
+// replayed (its lines simply miss).  Bump whenever a tile id changes meaning.
+constexpr int kTileTableVersion = 4;
+
 std::string igemm_key(const IgemmArgs& a) {
-  char b[200];
+  char b[240];
   const Epilogue& e = a.e;
   const int epi = (e.shuffle_co ? 1 : 0) | (e.stats ? 2 : 0) | (e.yref ? 4 : 0) | (e.colsum1 ? 8 : 0) |
                   (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0);
-  snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d",
+  // the Winograd caps decide which candidates exist: a choice tuned under other
+  // caps is a different key
+  snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d wino=%d/%d tt=%d",
            a.bl ? "_bf16x3" : a.bh ? "_bf16" : "", a.M,
-           a.N, a.K, a.a.Cg, a.a.taps_h, a.a.taps_w, a.a.stride, a.a.Hg, a.a.Wg, epi);
+           a.N, a.K, a.a.Cg, a.a.taps_h, a.a.taps_w, a.a.stride, a.a.Hg, a.a.Wg, epi, unet::g_wino_max,
+           unet::g_wino_dgrad_max, kTileTableVersion);
   return b;
 }
 
 std::string wgrad_key(const WgradArgs& a) {
-  char b[192];
-  snprintf(b, sizeof b, "wgrad%s Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d",
+  char b[240];
+  snprintf(b, sizeof b, "wgrad%s Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d wino=%d tt=%d",
            a.split ? "_bf16x3" : a.bf16 ? "_bf16" : "", a.Mo,
-           a.No, a.P, a.gb.Cg, a.gb.taps_h, a.gb.taps_w, a.gb.stride, a.gb.Hg, a.gb.Wg);
+           a.No, a.P, a.gb.Cg, a.gb.taps_h, a.gb.taps_w, a.gb.stride, a.gb.Hg, a.gb.Wg, unet::g_wino_wgrad_max,
+           kTileTableVersion);
   return b;
 }
 
@@ -358,7 +374,16 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   tune_db_load_once();
   auto it = g_tuned.find(key);
-  if (it != g_tuned.end()) return it->second;
+  if (it != g_tuned.end()) {
+    // a cached / database choice must still apply to this build and plan (a
+    // database from another tile set, or a split whose partials no longer fit
+    // the slab): otherwise it is dropped and the shape re-tuned
+    const GemmChoice g = it->second;
+    const bool slab_ok = g.tile >= 70 || igemm_slab_bytes(a, g.split) <= c.p->slab.bytes;  // Winograd: split = inner tile
+    if (g.tile < 0 || (igemm_tile_fits(a, g.tile) && slab_ok)) return g;
+    g_tuned.erase(it);
+    g_tune_log.erase(key);
+  }
   if (capturing(c.s)) return GemmChoice{};  // hipGraph capture: replay the tuned choice, never time
   IgemmArgs t = a;
   double* scr = c.d(c.p->tune_scratch);
@@ -395,7 +420,12 @@ GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
   std::lock_guard<std::mutex> lk(g_tune_mu);
   tune_db_load_once();
   auto it = g_tuned.find(key);
-  if (it != g_tuned.end()) return it->second;
+  if (it != g_tuned.end()) {
+    const GemmChoice g = it->second;
+    if (g.tile < 0 || wgrad_tile_fits(a, g.tile)) return g;
+    g_tuned.erase(it);  // not applicable to this build: re-tune
+    g_tune_log.erase(key);
+  }
   if (capturing(c.s)) return GemmChoice{};
   WgradArgs t = a;
   t.out = c.f(c.p->tune_scratch);
@@ -635,11 +665,13 @@ hipError_t ensure_side_stream(unet_plan* p) {
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
   for (auto& ev : p->ev_du)
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+  for (auto& ev : p->ev_seg)
+    if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
   return hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming);
 }
 
 int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* x, const float* dlogits, char* ws,
-                 int seg_b, int seg_e, hipStream_t s) {
+                 int seg_b, int seg_e, hipStream_t s, int flags) {
   Ctx c{p, ws, s};
   const int n = p->n;
   // bf16 plans store the activation gradients between GEMMs in bf16 (as
@@ -854,9 +886,19 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       CK(run_igemm(c, b));
     }
   }
+  for (int sg = seg_b; sg < seg_e; ++sg) p->seg_on_side[sg] = conc;
   if (conc) {
-    CK(hipEventRecord(p->ev_join, sw));
-    CK(hipStreamWaitEvent(s, p->ev_join, 0));
+    if (flags & UNET_BWD_DEFER_JOIN) {
+      // data-parallel schedule: the caller's next segment (dgrad chain) does not
+      // wait for this segment's weight gradients; its all-reduce waits on this
+      // event (unet_plan_wait_segment) and unet_plan_join() ends the backward
+      for (int sg = seg_b; sg < seg_e; ++sg) CK(hipEventRecord(p->ev_seg[sg], sw));
+      p->side_pending = true;
+    } else {
+      CK(hipEventRecord(p->ev_join, sw));
+      CK(hipStreamWaitEvent(s, p->ev_join, 0));
+      p->side_pending = false;
+    }
   }
   if (seg_e == 9) ++p->bwd_full;
   return 0;
@@ -867,7 +909,13 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
 // =========================== C-ABI =======================================
 extern "C" {
 
-const char* unet_version(void) { return "unet_hip 0.3 gfx950 fp32/bf16/bf16x3-mfma"; }
+#ifndef UNET_SRC_HASH
+#define UNET_SRC_HASH "unknown"
+#endif
+// the hash of the sources this library was built from (csrc/Makefile: sha256
+// over $(SRCS), the internal headers and include/unet_hip.h, first 16 hex
+// digits), so a run's record names the code it ran
+const char* unet_version(void) { return "unet_hip 0.4 gfx950 fp32/bf16/bf16x3-mfma src " UNET_SRC_HASH; }
 const char* unet_last_error(void) { return g_err.c_str(); }
 
 unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
@@ -877,8 +925,8 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
 int unet_plan_precision(const unet_plan* p) { return p ? p->prec : -EINVAL; }
 
 unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int prec) {
-  if (n < 1 || c_in < 1 || c_in > 4 || n_classes < 1 || n_classes > 4) {
-    set_err("unet_plan_create: need n>=1, 1<=c_in<=4, 1<=n_classes<=4");
+  if (n < 1 || c_in < 1 || c_in > 16 || n_classes < 1 || n_classes > 32) {
+    set_err("unet_plan_create: need n>=1, 1<=c_in<=16, 1<=n_classes<=32");
     return nullptr;
   }
   if (prec != UNET_PREC_FP32 && prec != UNET_PREC_BF16 && prec != UNET_PREC_BF16X3) {
@@ -985,7 +1033,7 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
   }
   for (int k = 0; k < 4; ++k)  // colsum groups + (tail) expanded bias table
     p->T[k].colsum = al.take(sizeof(double) * kStatGroups * p->T[k].co);
-  p->head_acc = al.take(sizeof(double) * (64 * 4 + 4));
+  p->head_acc = al.take(sizeof(double) * (64 * 32 + 32));  // dW, db of up to 32 classes
   p->wce_acc = al.take(64);
   p->first_slabs = al.take(conv_first_wgrad_ws_bytes(c_in));
   p->stat_region.off = stat_start;
@@ -1098,6 +1146,7 @@ void unet_plan_destroy(unet_plan* p) {
     (void)hipStreamSynchronize(p->side);
     for (auto ev : p->ev_dy) (void)hipEventDestroy(ev);
     for (auto ev : p->ev_du) (void)hipEventDestroy(ev);
+    for (auto ev : p->ev_seg) (void)hipEventDestroy(ev);
     (void)hipEventDestroy(p->ev_join);
     (void)hipStreamDestroy(p->side);
   }
@@ -1151,7 +1200,41 @@ int unet_plan_backward(unet_plan* p, void* const* prm, void* const* grd, const f
     return -EINVAL;
   }
   return run_backward(p, prm, grd, x, dlogits, reinterpret_cast<char*>(ws), sb, se,
-                      reinterpret_cast<hipStream_t>(stream));
+                      reinterpret_cast<hipStream_t>(stream), 0);
+}
+
+int unet_plan_backward_ex(unet_plan* p, void* const* prm, void* const* grd, const float* x, const float* dlogits,
+                          void* ws, int sb, int se, int flags, unet_stream_t stream) {
+  if (!p || !prm || !grd || !x || !dlogits || !ws || sb < 0 || se > 9 || sb >= se || (flags & ~UNET_BWD_DEFER_JOIN)) {
+    set_err("unet_plan_backward_ex: bad argument");
+    return -EINVAL;
+  }
+  return run_backward(p, prm, grd, x, dlogits, reinterpret_cast<char*>(ws), sb, se,
+                      reinterpret_cast<hipStream_t>(stream), flags);
+}
+
+int unet_plan_wait_segment(unet_plan* p, int seg, unet_stream_t stream) {
+  if (!p || seg < 0 || seg >= 9) {
+    set_err("unet_plan_wait_segment: bad argument");
+    return -EINVAL;
+  }
+  // the segment ran without the side stream (tuning pass, timing, serial mode):
+  // its weight gradients are on the caller's stream already
+  if (!p->seg_on_side[seg] || !p->side) return 0;
+  CK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->ev_seg[seg], 0));
+  return 0;
+}
+
+int unet_plan_join(unet_plan* p, unet_stream_t stream) {
+  if (!p) {
+    set_err("unet_plan_join: null plan");
+    return -EINVAL;
+  }
+  if (!p->side || !p->side_pending) return 0;
+  CK(hipEventRecord(p->ev_join, p->side));
+  CK(hipStreamWaitEvent(reinterpret_cast<hipStream_t>(stream), p->ev_join, 0));
+  p->side_pending = false;
+  return 0;
 }
 
 size_t unet_tuning_report(char* buf, size_t len) {

@@ -138,7 +138,7 @@ hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s);
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c);
 double wgrad_exec_flops(const WgradArgs& a, GemmChoice c);
 hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int mt);
-// bf16 halo conv with LDS-DMA weights (conv3_dma.hip), tile ids 61-66
+// bf16 halo conv with LDS-DMA weights (conv3_dma.hip), tile ids 63 and 65-68
 bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch);
 hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);
 int num_cus();

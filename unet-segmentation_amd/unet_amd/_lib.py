@@ -34,6 +34,9 @@ SIGNATURES = {
     "unet_plan_num_segments": (_i, [_vp]),
     "unet_plan_segment_grads": (_i, [_vp, _i, ctypes.POINTER(_i), ctypes.POINTER(_i)]),
     "unet_plan_backward": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
+    "unet_plan_backward_ex": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp]),
+    "unet_plan_wait_segment": (_i, [_vp, _i, _vp]),
+    "unet_plan_join": (_i, [_vp, _vp]),
     "unet_plan_set_timing": (_i, [_vp, _i]),
     "unet_plan_timing": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "unet_plan_timing_mfma_flops": (_i, [_vp, _vp]),
@@ -130,6 +133,33 @@ def ptr_array(tensors):
 def stream_of(device=None):
     import torch
     return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+# csrc/Makefile SRC_HASH: sha256 over these files, in this order
+_HASHED = ["igemm.hip", "igemm_bf16.hip", "conv3_dma.hip", "winograd.hip", "elementwise.hip", "elastic.hip",
+           "tiling.hip", "weightmap.hip", "postproc.hip", "track.hip", "ops.hip", "plan.hip", "unet_internal.h",
+           "gemm_common.h", os.path.join("..", "..", "include", "unet_hip.h")]
+
+
+def source_hash() -> str:
+    """The hash csrc/Makefile compiles into unet_version(), recomputed from the
+    sources in this tree (first 16 hex digits of sha256)."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(_HERE, "..", "csrc")
+    for f in _HASHED:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
+def build_identity() -> dict:
+    """unet_version() of the loaded library, the hash of the tree's sources and
+    whether the two agree (a stale .so shows up as src_match False)."""
+    v = load().unet_version().decode()
+    built = v.rsplit(" src ", 1)[-1] if " src " in v else "unknown"
+    tree = source_hash()
+    return {"version": v, "lib_src": built, "tree_src": tree, "src_match": built == tree}
 
 
 def tuning_report() -> str:

@@ -78,13 +78,23 @@ class GradBucketReducer:
     ``comm_dtype=torch.bfloat16`` sends the buckets as bf16 (half the bytes on
     xGMI: 62 instead of 124 MB per step for the U-Net): each bucket is rounded
     into a bf16 shadow, reduced there and widened back into ``flat`` on
-    ``wait()``.  The bf16 GEMM plans use it by default (Trainer)."""
+    ``wait()``.  Opt-in (Trainer(comm_dtype=torch.bfloat16)): the ranks' values
+    are then summed in bf16 by the collective, so the summation error grows with
+    the world size; the default keeps fp32 DDP semantics.
 
-    def __init__(self, flat, buckets, group=None, comm_dtype=None):
+    ``ready(b, stream)``, when given, makes the collective's issuing stream wait
+    for everything bucket b depends on beyond the current stream (the plan's
+    side-stream weight gradients, unet_plan_wait_segment); the collective is
+    then issued from that stream, so later work on the current stream (the
+    next backward segment) does not wait for it."""
+
+    def __init__(self, flat, buckets, group=None, comm_dtype=None, ready=None):
         self.flat = flat
         self.buckets = list(buckets)
         self.group = group
         self.works = []
+        self.ready = ready
+        self.stream = None
         comm_dtype = flat.dtype if comm_dtype is None else comm_dtype  # None: the buffer's own dtype
         self.comm_dtype = comm_dtype
         self.shadow = None if comm_dtype == flat.dtype else torch.empty(flat.numel(), dtype=comm_dtype,
@@ -107,6 +117,18 @@ class GradBucketReducer:
         if self.world == 1:
             return
         a, z = self.buckets[b]
+        if self.ready is None or not self.flat.is_cuda:
+            self._issue(a, z)
+            return
+        if self.stream is None:
+            self.stream = torch.cuda.Stream(device=self.flat.device)
+        cur = torch.cuda.current_stream(self.flat.device)
+        self.stream.wait_stream(cur)       # the segment's input-gradient chain and bucket writes
+        self.ready(b, self.stream)         # + its side-stream weight gradients
+        with torch.cuda.stream(self.stream):
+            self._issue(a, z)
+
+    def _issue(self, a, z):
         if self.shadow is None:
             self.works.append((dist.all_reduce(self.flat[a:z], group=self.group, async_op=True), a, z))
             return
@@ -119,10 +141,14 @@ class GradBucketReducer:
             self.reduce(b)
 
     def wait(self):
+        """Make the current stream wait for every issued collective (and widen
+        bf16 buckets back into the flat buffer)."""
         for w, a, z in self.works:
             w.wait()
             if self.shadow is not None:
                 self.flat[a:z].copy_(self.shadow[a:z])
+        if self.stream is not None:
+            torch.cuda.current_stream(self.flat.device).wait_stream(self.stream)
         self.works.clear()
 
 

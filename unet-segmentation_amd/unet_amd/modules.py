@@ -179,10 +179,12 @@ class UNet(nn.Module):
         super().__init__()
         if bilinear:
             raise NotImplementedError("bilinear=True is outside the MI355X hot path (reference default False)")
-        if not 1 <= n_channels <= 4:
-            raise ValueError("n_channels must be in 1..4 (first conv is the Ci<=4 direct kernel)")
-        if not 1 <= n_classes <= 4:
-            raise ValueError("n_classes must be in 1..4")
+        # models/unet_model.py:66-85 takes any counts; the first conv's direct
+        # kernel holds up to 16 input channels, the head / loss up to 32 classes
+        if not 1 <= n_channels <= 16:
+            raise ValueError("n_channels must be in 1..16")
+        if not 1 <= n_classes <= 32:
+            raise ValueError("n_classes must be in 1..32")
         self.n_channels = n_channels
         self.n_classes = n_classes
         self.bilinear = bilinear
@@ -231,13 +233,43 @@ class UNet(nn.Module):
         return "fp32"
 
 
+class LabelCheck:
+    """torch's nn.CrossEntropyLoss (utils/losses.py:27) raises for a target
+    outside [0, K) other than ignore_index -100.  The fused loss kernel flags
+    such a target on the device (it contributes nothing); the flag is copied to
+    pinned host memory behind the loss and read at the caller's next
+    synchronisation point -- the next loss call whose predecessor has finished,
+    or check(wait=True) -- instead of synchronising every step."""
+
+    def __init__(self):
+        self.pending = []
+
+    def record(self, acc):
+        host = torch.empty(2, dtype=torch.float64, pin_memory=True)
+        host.copy_(acc[1:3], non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(torch.cuda.current_stream(acc.device))
+        self.pending.append((host, ev))
+
+    def check(self, wait=False):
+        keep = []
+        for host, ev in self.pending:
+            if wait:
+                ev.synchronize()
+            elif not ev.query():
+                keep.append((host, ev))
+                continue
+            if host[0] != 0:
+                self.pending = []
+                raise IndexError(f"Target {int(host[1])} is out of bounds.")
+        self.pending = keep
+
+
 def _check_loss_operands(logits, targets, weights):
     """The checks torch's CrossEntropyLoss / the reference's elementwise product
     make before touching memory (utils/losses.py:49-57): targets int64 and the
     weight map floating point, both (N, H, W) of the logits and on their device.
-    Labels outside [0, K) are treated as ignore_index (contribute 0) instead of
-    raising as torch does for values other than -100: validating them would
-    need a device synchronisation per step."""
+    Target values are checked on the device (LabelCheck)."""
     n, k, h, w = logits.shape
     if targets.dtype != torch.int64:
         raise RuntimeError(f"targets must be int64 class indices, got {targets.dtype}")
@@ -251,11 +283,15 @@ def _check_loss_operands(logits, targets, weights):
                          f"{tuple(weights.shape)}")
 
 
+_LABELS = LabelCheck()
+
+
 class _WCEFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, logits, targets, weights):
         _check_tensor(logits, "inputs")
         _check_loss_operands(logits, targets, weights)
+        _LABELS.check()
         if weights.dtype != torch.float32:
             weights = weights.float()
         n, k, h, w = logits.shape
@@ -268,6 +304,7 @@ class _WCEFunction(torch.autograd.Function):
         _lib.check(lib.unet_wce_fwd_bwd(logits.data_ptr(), targets.data_ptr(), weights.data_ptr(), n, k, h, w,
                                         ts, wsd, loss.data_ptr(), dl.data_ptr(), ctypes.c_float(1.0),
                                         acc.data_ptr(), _lib.stream_of(logits.device)), "unet_wce_fwd_bwd")
+        _LABELS.record(acc)
         ctx.save_for_backward(dl)
         return loss
 
@@ -291,3 +328,10 @@ class WeightedCrossEntropyLoss(nn.Module):
 
     def forward(self, inputs, targets, weight_maps):
         return _WCEFunction.apply(inputs, targets, weight_maps)
+
+    @staticmethod
+    def check_targets():
+        """Synchronise and raise IndexError if any loss computed so far saw a
+        target outside [0, n_classes) other than -100 (later loss calls raise it
+        anyway once the offending call has finished)."""
+        _LABELS.check(wait=True)

@@ -52,10 +52,23 @@ class Plan:
                                               ws.data_ptr(), int(bool(train)), _lib.stream_of(x.device)),
                    "unet_plan_forward")
 
-    def backward(self, param_tab, grad_tab, x, dlogits, ws, seg_begin=0, seg_end=N_SEGMENTS):
-        _lib.check(self.lib.unet_plan_backward(self.handle, param_tab, grad_tab, x.data_ptr(), dlogits.data_ptr(),
-                                               ws.data_ptr(), seg_begin, seg_end, _lib.stream_of(x.device)),
-                   "unet_plan_backward")
+    def backward(self, param_tab, grad_tab, x, dlogits, ws, seg_begin=0, seg_end=N_SEGMENTS, defer_join=False):
+        """defer_join: leave the segments' side-stream weight gradients running
+        (UNET_BWD_DEFER_JOIN); wait_segment() before reducing a segment's
+        gradients and join() before the optimizer."""
+        _lib.check(self.lib.unet_plan_backward_ex(self.handle, param_tab, grad_tab, x.data_ptr(), dlogits.data_ptr(),
+                                                  ws.data_ptr(), seg_begin, seg_end, 1 if defer_join else 0,
+                                                  _lib.stream_of(x.device)),
+                   "unet_plan_backward_ex")
+
+    def wait_segment(self, seg, stream):
+        """Make `stream` (a torch stream) wait for segment seg's weight gradients."""
+        _lib.check(self.lib.unet_plan_wait_segment(self.handle, seg, ctypes.c_void_p(stream.cuda_stream)),
+                   "unet_plan_wait_segment")
+
+    def join(self, device):
+        """Join the side stream into the current stream of `device`."""
+        _lib.check(self.lib.unet_plan_join(self.handle, _lib.stream_of(device)), "unet_plan_join")
 
     timing_on = False
 

@@ -46,6 +46,12 @@ class Tracker:
             raise ValueError("Tracker.add_frame runs on the HIP device only (no CPU fallback)")
         if tuple(labels.shape) != (self.h, self.w):
             raise ValueError(f"labels must be ({self.h}, {self.w}), got {tuple(labels.shape)}")
+        if labels.dtype != torch.uint16 and labels.numel():
+            # the device tables index labels as uint16: a wider label would wrap
+            # (e.g. 65536 -> 0 = background, or merge with another object)
+            lo, hi = torch.aminmax(labels)
+            if int(lo) < 0 or int(hi) >= 65536:
+                raise ValueError(f"labels must lie in [0, 65535], got [{int(lo)}, {int(hi)}]")
         lab = _u16(labels)
         if self.ws is None:
             self.ws = torch.empty(self.lib.unet_tracker_ws_bytes(self.h, self.w), dtype=torch.uint8,

@@ -14,9 +14,13 @@ SGD(lr, momentum=0.99).step() -- with the same arithmetic as the drop-in
   bf16 matrix cores (operands split into bf16 hi/lo pairs, three products);
   weights, gradients and the optimizer stay fp32 in every mode;
 * with a process group, the backward runs in 9 segments and each segment's
-  gradient bucket is all-reduced (RCCL over xGMI) while later segments compute
-  (bf16 on the wire for bf16 plans), and every step starts by broadcasting rank
-  0's BatchNorm running statistics (one flat buffer), as DDP does.
+  gradient bucket is all-reduced (RCCL over xGMI) while later segments compute:
+  the plan leaves each segment's weight gradients running on its side stream
+  (UNET_BWD_DEFER_JOIN), the bucket's collective is issued from a stream that
+  waits for them, and the side stream is joined once, before the optimizer;
+  gradients are summed in fp32 (``comm_dtype=torch.bfloat16`` halves the xGMI
+  bytes, opt-in); every step starts by broadcasting rank 0's BatchNorm running
+  statistics (one flat buffer), as DDP does.
 """
 from __future__ import annotations
 
@@ -107,6 +111,9 @@ class Trainer:
         self.dlogits = torch.empty_like(self.logits)
         self.loss = torch.empty((), dtype=torch.float32, device=dev)
         self.acc = torch.empty(8, dtype=torch.float64, device=dev)
+        from .modules import LabelCheck
+        self.labels = LabelCheck()
+        self._capturing = False
         self.first_step = True
         self.use_graph = bool(graph)
         self._graph = None
@@ -115,12 +122,12 @@ class Trainer:
         self.graph_error = None
         self.lib = _lib.load()
         buckets = [self.flat.range_for(*self.plan.segment_grads(s)) for s in range(N_SEGMENTS)]
-        # gradient all-reduce dtype: bf16 for the bf16 GEMM plans (half the xGMI
-        # bytes), fp32 otherwise
-        if comm_dtype is None:
-            comm_dtype = torch.bfloat16 if precision == "bf16" else torch.float32
-        self.comm_dtype = comm_dtype
-        self.reducer = GradBucketReducer(self.flat.grad, buckets, process_group, comm_dtype)
+        # gradient all-reduce dtype: fp32 (DDP semantics) unless the caller asks
+        # for bf16 on the wire (half the xGMI bytes; summed in bf16)
+        self.comm_dtype = torch.float32 if comm_dtype is None else comm_dtype
+        comm_dtype = self.comm_dtype
+        self.reducer = GradBucketReducer(self.flat.grad, buckets, process_group, comm_dtype,
+                                         ready=lambda b, st: self.plan.wait_segment(b, st))
         self.reducer_whole = GradBucketReducer(self.flat.grad, [(0, self.flat.numel)], process_group, comm_dtype)
 
     @property
@@ -142,6 +149,8 @@ class Trainer:
 
     def forward_loss(self, x, targets, weights):
         self._check_batch(x, targets, weights)
+        if not self._capturing:
+            self.labels.check()  # an earlier step's out-of-range target (raises IndexError)
         self.plan.forward(self.param_tab, x, self.logits, self.ws, True)
         n, k, h, w = self.logits.shape
         ts = (ctypes.c_int64 * 3)(*targets.stride())
@@ -150,6 +159,8 @@ class Trainer:
                                              w, ts, wsd, self.loss.data_ptr(), self.dlogits.data_ptr(),
                                              ctypes.c_float(1.0), self.acc.data_ptr(), _lib.stream_of(x.device)),
                    "unet_wce_fwd_bwd")
+        if not self._capturing:
+            self.labels.record(self.acc)
         return self.loss
 
     def backward_and_reduce(self, x):
@@ -160,8 +171,11 @@ class Trainer:
                 self.reducer_whole.wait()
             return
         for s in range(N_SEGMENTS):
-            self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, s, s + 1)
-            self.reducer.reduce(s)  # bucket s is final: all-reduce it while segment s+1 computes
+            # segment s's weight gradients stay on the plan's side stream (no join):
+            # segment s+1's input gradients start at once
+            self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, s, s + 1, defer_join=True)
+            self.reducer.reduce(s)  # bucket s is final once its side-stream work is: all-reduce it meanwhile
+        self.plan.join(x.device)
         self.reducer.wait()
 
     def optimizer_step(self):
@@ -183,6 +197,9 @@ class Trainer:
                 self._graph_key == self._key(x, targets, weights)):
             self._graph.replay()
             return self.loss
+        if self._graph is not None and self._graph_key[1:] != (self.lr, self.mom):
+            self._graph = None  # stale hyper-parameters: capture again after this eager step
+            self._eager_steps = 1
         if self.broadcast_buffers and self.flat_buffers.flat is not None:
             torch.distributed.broadcast(self.flat_buffers.flat, 0, group=self.pg)
         loss = self.forward_loss(x, targets, weights)
@@ -194,9 +211,10 @@ class Trainer:
             self._capture(x, targets, weights)
         return loss
 
-    @staticmethod
-    def _key(x, targets, weights):
-        return tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride())) for t in (x, targets, weights))
+    def _key(self, x, targets, weights):
+        # lr / momentum are baked into the captured SGD launch: a change re-captures
+        return (tuple((t.data_ptr(), tuple(t.shape), tuple(t.stride())) for t in (x, targets, weights)),
+                self.lr, self.mom)
 
     def _capture(self, x, targets, weights):
         """Capture one eager-equivalent step (first_step is already False, so
@@ -204,6 +222,7 @@ class Trainer:
         the trainer eager."""
         torch.cuda.synchronize()
         g = torch.cuda.CUDAGraph()
+        self._capturing = True
         try:
             with torch.cuda.graph(g):
                 self.forward_loss(x, targets, weights)
@@ -214,6 +233,8 @@ class Trainer:
             self.graph_error = repr(e)
             torch.cuda.synchronize()
             return
+        finally:
+            self._capturing = False
         # (capture launches nothing: the step that triggered it has already run eagerly)
         self._graph, self._graph_key = g, self._key(x, targets, weights)
 
