@@ -307,11 +307,21 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *  "concurrent"    1 (default, or env UNET_CONCURRENT) = a plan's backward
  *                  runs the weight-gradient GEMMs on a side stream beside the
  *                  dX chain (joined before the call returns); 0 = one stream.
+ *  "bf16_norm"     1 (or env UNET_BF16_NORM=1; default 0) = UNET_PREC_BF16 plans
+ *                  created afterwards write relu(bn(y)) of every layer once
+ *                  as a bf16 tensor, the plain operand of its GEMM consumers
+ *                  (LDS-DMA staging; tiles 81-84 need it); 0 = consumers apply
+ *                  BatchNorm + ReLU while staging.
+ *  "bn_fold"       1 (default, or env UNET_BN_FOLD) = eval forwards fold each
+ *                  BatchNorm into its conv (weights x gamma / sqrt(var + eps),
+ *                  bias x that + beta - mean x that) and store relu(conv') in
+ *                  the GEMM epilogue; 0 = consumers apply BN + ReLU on load.
  *  "force_split"   k > 1: every plan igemm runs split-K k (tests), 0 = off.
  *  "force_tile"    id > 0: every plan igemm whose shape admits tile id runs
  *                  it (tests; 1-4, 6-9 register-staged, 11-14 LDS-DMA, 51-54
  *                  fp32 halo, 70-72 / 74 fp32 Winograd, 21-26 / 31-36 / 63-67
- *                  bf16 operands -- only in UNET_PREC_BF16 / _BF16X3 plans).
+ *                  / 81-84 bf16 operands -- only in UNET_PREC_BF16 / _BF16X3
+ *                  plans).
  *  "op_precision"  UNET_PREC_* of the per-op GEMM entry points below
  *                  (unet_conv3x3_*, unet_convT2_*); default fp32.
  *  "op_a16"        1 = with op_precision UNET_PREC_BF16, unet_conv3x3_fwd /

@@ -321,11 +321,14 @@ def gemm_mode(request, lib):
     for part in mode.split("+"):
         if part == "heuristic":
             lib.unet_set_tuning(b"autotune", 0)
+        elif part == "norm":  # normalised bf16 operand copies (the ring tiles 81-84 need them)
+            lib.unet_set_tuning(b"bf16_norm", 1)
         elif part.startswith("split"):
             lib.unet_set_tuning(b"force_split", int(part[5:]))
         elif part.startswith("tile"):
             lib.unet_set_tuning(b"force_tile", int(part[4:]))
     yield mode
+    lib.unet_set_tuning(b"bf16_norm", 0)
     lib.unet_set_tuning(b"autotune", 1)
     lib.unet_set_tuning(b"force_split", 0)
     lib.unet_set_tuning(b"force_tile", 0)
@@ -336,12 +339,15 @@ def gemm_mode(request, lib):
                                        "tile22+split3", "tile24+split8", "tile31", "tile32", "tile33", "tile34",
                                        "tile35", "tile36", "tile31+split2", "tile34+split3", "tile41", "tile42",
                                        "tile43", "tile44", "tile41+split3", "tile63", "tile65", "tile66",
-                                       "tile67", "tile67+split3", "tile63+split2"],
+                                       "tile67", "tile67+split3", "tile63+split2", "norm+tile81", "norm+tile82",
+                                       "norm+tile83", "norm+tile84", "norm+tile81+split3", "norm+tile83+split2",
+                                       "norm+tile31", "norm+heuristic"],
                          indirect=True)
 def test_bf16_gemm_variants_vs_bf16_oracle(gemm_mode):
-    """Every bf16 tile (21-26 row gather, 31-36 halo-tiled 3x3 -- the convT GEMMs
-    fall back to the built-in tile there) and split-K on every conv / convT /
-    dgrad GEMM of a train step; the weight gradients run the bf16 wgrad tiles."""
+    """Every bf16 tile (21-26 row gather, 31-36 halo-tiled 3x3, 63-67 LDS-DMA
+    halo, 81-84 LDS-DMA halo / weight rings -- the convT GEMMs fall back to the
+    built-in tile there) and split-K on every conv / convT / dgrad GEMM of a
+    train step; the weight gradients run the bf16 wgrad tiles."""
     params = O.hash_init(1, 2, seed=21, bn_random=True)
     x, tgt, wmap = F.make_inputs(21, 2, 1, 188)
     check_vs_bf16_oracle(make_model(params), params, x, tgt, wmap, gemm_mode)

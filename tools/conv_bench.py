@@ -27,6 +27,9 @@ SHAPES = [
     ("down3.c1", 8, 58, 58, 512, 512),
     ("down4.c1", 8, 26, 26, 1024, 1024),
     ("up1.c0", 8, 48, 48, 1024, 512),
+    ("up2.c0", 8, 88, 88, 512, 256),
+    ("up3.c0", 8, 168, 168, 256, 128),
+    ("up4.c0", 8, 328, 328, 128, 64),
     ("up4.c1", 8, 326, 326, 64, 64),
 ]
 VARIANTS = [-1, 21, 22, 23, 24, 31, 32, 33, 34, 35, 36, 41, 42, 43, 44]
@@ -42,6 +45,8 @@ def main():
     ap.add_argument("--a16", action="store_true", help="bf16-stored A as in a bf16 plan (op_a16; tiles 61-66)")
     ap.add_argument("--variants", default=None, help="comma-separated variant ids")
     ap.add_argument("--shapes", default=None, help="comma-separated shape names")
+    ap.add_argument("--no-tf", action="store_true",
+                    help="forward without the consumer BN+ReLU (the bf16 plan's normalised-copy operand; ring tiles)")
     args = ap.parse_args()
     lib = _lib.load()
     lib.unet_set_tuning(b"op_precision", args.prec)
@@ -83,8 +88,9 @@ def main():
                 rc = lib.unet_conv3x3_dgrad(dy.data_ptr(), n, h, w, ci, wt.data_ptr(), co, dx.data_ptr(),
                                             ws.data_ptr(), st)
             else:
-                rc = lib.unet_conv3x3_fwd(x.data_ptr(), n, h, w, ci, wt.data_ptr(), b.data_ptr(), co, sc.data_ptr(),
-                                          sh.data_ptr(), y.data_ptr(), ws.data_ptr(), st)
+                rc = lib.unet_conv3x3_fwd(x.data_ptr(), n, h, w, ci, wt.data_ptr(), b.data_ptr(), co,
+                                          None if args.no_tf else sc.data_ptr(), None if args.no_tf else sh.data_ptr(),
+                                          y.data_ptr(), ws.data_ptr(), st)
             return rc
 
         times = {v: [] for v in variants}

@@ -47,7 +47,7 @@ template <int CI, int H16>  // H16: y stored bf16 (statistics of the rounded val
 __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict__ x, int h, int w,
                                                         const float* __restrict__ wt,
                                                         const float* __restrict__ bias, float* __restrict__ y,
-                                                        double* __restrict__ stats) {
+                                                        double* __restrict__ stats, int relu) {
   const int ho = h - 2, wo = w - 2;
   const int x0 = blockIdx.x * 64, row = blockIdx.y, n = blockIdx.z;
   __shared__ float tile[CI][3][66];
@@ -75,6 +75,7 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd(const float* __restrict_
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) acc = fmaf(tile[ci][ky][px + kx], wr[(ci * 3 + ky) * 3 + kx], acc);
+    if (relu) acc = fmaxf(acc, 0.f);  // eval with BatchNorm folded into wt / bias
     if (gx < wo) {
       const size_t yi = ((size_t)(n * ho + row) * wo + gx) * 64 + c;
       if (H16) {
@@ -248,7 +249,7 @@ template <int H16>
 __global__ __launch_bounds__(256) void k_conv_first_fwd_gen(const float* __restrict__ x, int ci_n, int h, int w,
                                                             const float* __restrict__ wt,
                                                             const float* __restrict__ bias, float* __restrict__ y,
-                                                            double* __restrict__ stats) {
+                                                            double* __restrict__ stats, int relu) {
   const int ho = h - 2, wo = w - 2;
   const int x0 = blockIdx.x * 64, row = blockIdx.y, n = blockIdx.z;
   __shared__ float tile[kFirstMaxCi][3][66];
@@ -276,6 +277,7 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd_gen(const float* __restr
       for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) acc = fmaf(tile[ci][ky][px + kx], wl[(ci * 3 + ky) * 3 + kx][c], acc);
+    if (relu) acc = fmaxf(acc, 0.f);  // eval with BatchNorm folded into wt / bias
     if (gx < wo) {
       const size_t yi = ((size_t)(n * ho + row) * wo + gx) * 64 + c;
       if (H16) {
@@ -304,25 +306,49 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd_gen(const float* __restr
 
 template <int H16>
 static void conv_first_go(dim3 grid, int ci, const float* x, int h, int w, const float* wt, const float* bias, float* y,
-                          double* stats, hipStream_t s) {
+                          double* stats, int relu, hipStream_t s) {
   if (ci > 4) {
-    hipLaunchKernelGGL((k_conv_first_fwd_gen<H16>), grid, dim3(256), 0, s, x, ci, h, w, wt, bias, y, stats);
+    hipLaunchKernelGGL((k_conv_first_fwd_gen<H16>), grid, dim3(256), 0, s, x, ci, h, w, wt, bias, y, stats, relu);
     return;
   }
   switch (ci) {
-    case 1: hipLaunchKernelGGL((k_conv_first_fwd<1, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
-    case 2: hipLaunchKernelGGL((k_conv_first_fwd<2, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
-    case 3: hipLaunchKernelGGL((k_conv_first_fwd<3, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
-    default: hipLaunchKernelGGL((k_conv_first_fwd<4, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats); break;
+    case 1: hipLaunchKernelGGL((k_conv_first_fwd<1, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats, relu); break;
+    case 2: hipLaunchKernelGGL((k_conv_first_fwd<2, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats, relu); break;
+    case 3: hipLaunchKernelGGL((k_conv_first_fwd<3, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats, relu); break;
+    default: hipLaunchKernelGGL((k_conv_first_fwd<4, H16>), grid, dim3(256), 0, s, x, h, w, wt, bias, y, stats, relu); break;
   }
 }
 
 hipError_t launch_conv_first_fwd(const float* x, int n, int ci, int h, int w, const float* wt,
-                                 const float* bias, int co, float* y, double* stats, hipStream_t s, int out_h16) {
+                                 const float* bias, int co, float* y, double* stats, hipStream_t s, int out_h16,
+                                 int relu) {
   if (co != 64 || ci < 1 || ci > kFirstMaxCi || h < 3 || w < 3) return hipErrorInvalidValue;
   dim3 grid(cdiv(w - 2, 64), h - 2, n);
-  if (out_h16) conv_first_go<1>(grid, ci, x, h, w, wt, bias, y, stats, s);
-  else conv_first_go<0>(grid, ci, x, h, w, wt, bias, y, stats, s);
+  if (out_h16) conv_first_go<1>(grid, ci, x, h, w, wt, bias, y, stats, relu, s);
+  else conv_first_go<0>(grid, ci, x, h, w, wt, bias, y, stats, relu, s);
+  return hipGetLastError();
+}
+
+// BatchNorm folded into a conv for eval (scripts/predict.py:70 model.eval()):
+// row r of the weight matrix w[rows][K] times scale[r] (into wout, may alias w)
+// and bias_out[r] = scale[r] * bias[r] + shift[r], scale / shift from the
+// running statistics (k_bn_eval_prepare): bn(conv(x)) = conv'(x).
+__global__ void k_fold_bn(const float* __restrict__ w, long long K, int rows, const float* __restrict__ scale,
+                          const float* __restrict__ shift, const float* __restrict__ bias, float* __restrict__ wout,
+                          float* __restrict__ bias_out) {
+  const long long n = (long long)rows * K;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const int r = (int)(i / K);
+    wout[i] = w[i] * scale[r];
+    if (i - (long long)r * K == 0) bias_out[r] = fmaf(scale[r], bias[r], shift[r]);
+  }
+}
+
+hipError_t launch_fold_bn(const float* w, long long K, int rows, const float* scale, const float* shift,
+                          const float* bias, float* wout, float* bias_out, hipStream_t s) {
+  const long long n = (long long)rows * K;
+  hipLaunchKernelGGL(k_fold_bn, dim3(grid_cap(n, 256, 8192)), dim3(256), 0, s, w, K, rows, scale, shift, bias, wout,
+                     bias_out);
   return hipGetLastError();
 }
 
@@ -552,8 +578,13 @@ hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, 
 // MaxPool2d(2) forward (models/unet_model.py:28) of relu(bn(y)): floor mode,
 // scan order (0,0),(0,1),(1,0),(1,1) with strict '>' so the FIRST max wins.
 // ---------------------------------------------------------------------------
+// anorm (optional, bf16 plans): the normalised input relu(bn(y)) of every
+// window element, bf16 at its NHWC position -- the encoder output's skip view
+// for the up block's concat (a row / column that floor mode drops is never
+// inside that center crop).
 template <int H16, int Y16>  // H16: pooled map stored bf16 (a GEMM operand only); Y16: input y stored bf16
-__global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y, uint8_t* __restrict__ arg) {
+__global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y, uint8_t* __restrict__ arg,
+                              uint16_t* __restrict__ anorm) {
   const int C = s.C, C4 = C / 4, ho = h / 2, wo = w / 2;
   const long long total = (long long)n * ho * wo * C4;
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
@@ -579,6 +610,8 @@ __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y,
         t.w = fmaxf(fmaf(t.w, a.w, b.w), 0.f);
       }
       v[k] = t;
+      if (anorm)
+        *reinterpret_cast<uint2*>(anorm + si) = make_uint2(bf16pack(t.x, t.y), bf16pack(t.z, t.w));
     }
     float4 best = v[0];
     uchar4 a = make_uchar4(0, 0, 0, 0);
@@ -598,16 +631,41 @@ __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y,
 }
 
 hipError_t launch_maxpool_fwd(const Src& s, int n, int h, int w, float* y, uint8_t* arg, hipStream_t st,
-                              int out_h16) {
-  if (s.C % 4) return hipErrorInvalidValue;
+                              int out_h16, uint16_t* anorm) {
+  if (s.C % 4 || (anorm && (s.oy || s.ox))) return hipErrorInvalidValue;
   const long long work = (long long)n * (h / 2) * (w / 2) * (s.C / 4);
   const dim3 grid(grid_cap(work, 256, 8192));
   switch (out_h16 * 2 + (s.h16 ? 1 : 0)) {
-    case 0: hipLaunchKernelGGL((k_maxpool_fwd<0, 0>), grid, dim3(256), 0, st, s, n, h, w, y, arg); break;
-    case 1: hipLaunchKernelGGL((k_maxpool_fwd<0, 1>), grid, dim3(256), 0, st, s, n, h, w, y, arg); break;
-    case 2: hipLaunchKernelGGL((k_maxpool_fwd<1, 0>), grid, dim3(256), 0, st, s, n, h, w, y, arg); break;
-    default: hipLaunchKernelGGL((k_maxpool_fwd<1, 1>), grid, dim3(256), 0, st, s, n, h, w, y, arg); break;
+    case 0: hipLaunchKernelGGL((k_maxpool_fwd<0, 0>), grid, dim3(256), 0, st, s, n, h, w, y, arg, anorm); break;
+    case 1: hipLaunchKernelGGL((k_maxpool_fwd<0, 1>), grid, dim3(256), 0, st, s, n, h, w, y, arg, anorm); break;
+    case 2: hipLaunchKernelGGL((k_maxpool_fwd<1, 0>), grid, dim3(256), 0, st, s, n, h, w, y, arg, anorm); break;
+    default: hipLaunchKernelGGL((k_maxpool_fwd<1, 1>), grid, dim3(256), 0, st, s, n, h, w, y, arg, anorm); break;
   }
+  return hipGetLastError();
+}
+
+// a = bf16(relu(y * scale + shift)) over an NHWC bf16 tensor (8 channels = 16 B
+// per lane-step): the normalised copy a bf16 plan's GEMMs read as a plain
+// operand (BatchNorm + ReLU of the producer applied once per element instead
+// of in every consumer's staging path; the same fmaf / max / RNE, so the
+// operand bits are those of the on-load transform).
+__global__ __launch_bounds__(256) void k_bn_relu_bf(const uint16_t* __restrict__ y, const float* __restrict__ scale,
+                                                    const float* __restrict__ shift, long long n8, int c8,
+                                                    uint16_t* __restrict__ a) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n8; i += (long long)gridDim.x * blockDim.x) {
+    const int c = (int)(i % c8) * 8;
+    const uint4 u = reinterpret_cast<const uint4*>(y)[i];
+    const float4 r0 = affine_relu4(bf16x4_to_f4(make_uint2(u.x, u.y)), ld4(scale + c), ld4(shift + c));
+    const float4 r1 = affine_relu4(bf16x4_to_f4(make_uint2(u.z, u.w)), ld4(scale + c + 4), ld4(shift + c + 4));
+    reinterpret_cast<uint4*>(a)[i] = bf16pack8(r0, r1);
+  }
+}
+
+hipError_t launch_bn_relu_bf(const uint16_t* y, const float* scale, const float* shift, long long pixels, int c,
+                             uint16_t* a, hipStream_t s) {
+  if (c % 8) return hipErrorInvalidValue;
+  const long long n8 = pixels * (c / 8);
+  hipLaunchKernelGGL(k_bn_relu_bf, dim3(grid_cap(n8, 256, 8192)), dim3(256), 0, s, y, scale, shift, n8, c / 8, a);
   return hipGetLastError();
 }
 

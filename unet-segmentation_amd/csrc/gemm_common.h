@@ -119,6 +119,7 @@ struct LinearRows {
     mb = m0 + fr * 32 + 4 * h;
     lim = M - mb;
   }
+  __device__ __forceinline__ bool full(int fr) const { return M - (m0 + fr * 32) >= 32; }
 };
 // Tile pixel of GEMM row p (32 rows per MFMA fragment).  Row-major, except in
 // 16 x 16 tiles read from 80-B LDS rows: there fragment f holds tile rows f and
@@ -153,6 +154,8 @@ struct HaloRows {
     mb = (n * Hg + y) * Wg + x0 + 4 * h;
     lim = y < Hg ? Wg - x0 - 4 * h : 0;
   }
+  // every row of fragment block fr lies inside the grid (wave-uniform)
+  __device__ __forceinline__ bool full(int fr) const { return y0 + fr < Hg && Wg - x0 >= 32; }
 };
 
 template <class R>
@@ -209,6 +212,93 @@ __device__ __forceinline__ void igemm_finish_stats(const Epilogue& e, float (&s1
 }
 
 
+// Fast-path epilogue, specialised at compile time on what the GEMM's epilogue
+// does -- KIND 0: plain store (+ concat column sums of the second destination),
+// 1: forward BatchNorm statistics, 2: ReLU mask of the producer + BN-backward
+// statistics, 3: ReLU (eval with BatchNorm folded in) -- and on the storage (H16: bf16 destination, YH16: bf16 yref).
+// Row bases per fragment block; fragments whose 32 rows all lie inside the grid
+// (the wave-uniform common case) store without per-element guards.  A bf16
+// value is converted once: its bits are stored and its rounded value feeds the
+// statistics (the values the consumers read).
+template <int TM, int TN, int KIND, int H16, int YH16, class RowMap>
+__device__ __forceinline__ void epi_fast(const Epilogue& e, const floatx16 (&acc)[TM][TN], const RowMap& rows,
+                                         const Gather& g, int n0, int wm, int wn, int h, int li, float (&s1)[TN],
+                                         float (&s2)[TN], float (&t1)[TN]) {
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * TN * 32 + j * 32 + li;
+    const float bias = e.bias ? e.bias[col] : 0.f;
+    const bool second = col >= e.n_split;  // uniform per 32-column block (n_split % 32 == 0)
+    float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
+    const int dC = second ? e.d[1].C : e.d[0].C;
+    const int dcol = second ? col - e.n_split : col;
+    const bool csum = second && e.colsum1 != nullptr;
+    float bsc = 0.f, bsh = 0.f, bmu = 0.f, bis = 0.f;
+    if constexpr (KIND == 2) {
+      bsc = e.bn_scale[col];
+      bsh = e.bn_shift[col];
+      bmu = e.bn_mean[col];
+      bis = e.bn_invstd[col];
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      int mb, lim;
+      rows.block(wm * TM + i, h, mb, lim);
+      const unsigned ib = (unsigned)mb * (unsigned)dC + (unsigned)dcol;
+      float yv[KIND == 2 ? 16 : 1];
+      if constexpr (KIND == 2) {
+        // the mask operand of all 16 rows before the first store (the
+        // destination may alias yref as far as the compiler knows); rows past
+        // the grid re-load the last valid row
+        if (lim > 0) {
+          const int kmax = lim - 1;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const unsigned idx = ib + (unsigned)(min((r & 3) + 8 * (r >> 2), kmax) * dC);
+            yv[r] = YH16 ? __uint_as_float((unsigned)reinterpret_cast<const uint16_t*>(e.yref)[idx] << 16)
+                         : e.yref[idx];
+          }
+        }
+      }
+      auto one = [&](int r) {
+        const int k = (r & 3) + 8 * (r >> 2);
+        const unsigned idx = ib + (unsigned)(k * dC);
+        float v = acc[i][j][r] + bias;
+        if constexpr (KIND == 3) v = fmaxf(v, 0.f);
+        unsigned bits = 0;
+        if constexpr (H16) {
+          bits = bf16_of(v);
+          if constexpr (KIND == 1 || KIND == 2) v = __uint_as_float(bits << 16);  // statistics of the stored value
+        }
+        if constexpr (KIND == 2) {
+          const bool on = fmaf(yv[r], bsc, bsh) > 0.f;
+          v = on ? v : 0.f;
+          if constexpr (H16) bits = on ? bits : 0u;
+          s1[j] += v;
+          s2[j] += v * ((yv[r] - bmu) * bis);
+        } else if constexpr (KIND == 1) {
+          s1[j] += v;
+          s2[j] += v * v;
+        } else {
+          if (csum) t1[j] += v;
+        }
+        if constexpr (H16)
+          reinterpret_cast<uint16_t*>(dptr)[idx] = (uint16_t)bits;
+        else
+          dptr[idx] = v;
+      };
+      if (rows.full(wm * TM + i)) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) one(r);
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if ((r & 3) + 8 * (r >> 2) < lim) one(r);
+      }
+    }
+  }
+}
+
 // Split-K partial store or the full epilogue of an implicit-GEMM tile: bias,
 // destination mapping (linear / pixel shuffle / cropped), ReLU mask + BN-bwd
 // statistics, BN statistics, concat column sums.  `red` is WM*3*BN floats of
@@ -256,6 +346,27 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
   // epilogue is a large share of the small-K (64 / 128-channel) GEMMs.
   if constexpr (fast_rows<RowMap>::value) {
     auto lin = [&](const Dst& d) { return d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg; };
+    const bool two = e.n_split < N;
+    if (!e.shuffle_co && lin(e.d[0]) && (!two || (lin(e.d[1]) && e.d[1].h16 == e.d[0].h16)) &&
+        !(e.stats && (two || e.yref)) && !(e.yref && two) && !(e.relu && (two || e.stats || e.yref))) {
+      const int kind = e.yref ? 2 : e.stats ? 1 : e.relu ? 3 : 0;
+      const int h16 = e.d[0].h16, yh16 = e.yref_h16;
+      const int sel = kind * 4 + h16 * 2 + (kind == 2 ? yh16 : 0);
+      switch (sel) {
+        case 0: epi_fast<TM, TN, 0, 0, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        case 2: epi_fast<TM, TN, 0, 1, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        case 4: epi_fast<TM, TN, 1, 0, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        case 6: epi_fast<TM, TN, 1, 1, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        case 8: epi_fast<TM, TN, 2, 0, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        case 9: epi_fast<TM, TN, 2, 0, 1>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        case 10: epi_fast<TM, TN, 2, 1, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        case 11: epi_fast<TM, TN, 2, 1, 1>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        case 12: epi_fast<TM, TN, 3, 0, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+        default: epi_fast<TM, TN, 3, 1, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;
+      }
+      igemm_finish_stats<BN, WM, WN, NT>(e, s1, s2, t1, n0, wn, N, tid, red);
+      return;
+    }
     if (!e.shuffle_co && lin(e.d[0]) && (e.n_split >= N || lin(e.d[1]))) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -309,6 +420,7 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
             } else if (second && e.colsum1) {
               t1[j] += v;
             }
+            if (e.relu) v = fmaxf(v, 0.f);
             if (dh16)
               reinterpret_cast<uint16_t*>(dptr)[idx] = bf16_of(v);
             else
@@ -367,6 +479,7 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
         } else if (second && e.colsum1) {
           t1[j] += v;
         }
+        if (e.relu) v = fmaxf(v, 0.f);
         dst_store(d, idx, v);
       }
     }

@@ -875,6 +875,10 @@ __global__ __launch_bounds__(256) void k_splitk_epi(const IgemmArgs args) {
         s2[q] += vv[q] * vv[q];
       }
     }
+    if (e.relu) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) vv[q] = fmaxf(vv[q], 0.f);
+    }
     if (d.h16)
       *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(d.ptr) + idx) =
           make_uint2(bf16pack(vv[0], vv[1]), bf16pack(vv[2], vv[3]));
@@ -1131,6 +1135,12 @@ static TileInfo tile_info(int id) {
     case 66: return {512, 64, 288, 1};
     case 67: return {256, 64, 144, 2};
     case 68: return {256, 128, 144, 1};
+    // bf16 3x3 with LDS-DMA halo and weight rings (k_conv3_ring, conv3_ring.hip):
+    // bk = one 64- or 32-channel chunk x 9 taps (the split-K unit)
+    case 81: return {256, 128, 576, 1};
+    case 82: return {256, 64, 288, 2};
+    case 83: return {128, 128, 288, 3};
+    case 84: return {256, 64, 576, 1};
     // Winograd F(2x2, 3x3) (winograd.hip): no K split
     case 70: case 71: case 74: return {256, 64, 9, 2};
     case 72: return {32, 32, 16, 1};
@@ -1145,7 +1155,10 @@ static TileInfo tile_info(int id) {
 
 static bool is_halo_tile(int tile) { return (tile >= 31 && tile <= 36) || (tile >= 41 && tile <= 44); }
 static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 68); }
-static bool is_bf16_tile(int tile) { return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile); }
+static bool is_ring_tile(int tile) { return tile >= 81 && tile <= 84; }
+static bool is_bf16_tile(int tile) {
+  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile);
+}
 static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 
 // A tile applies when the shape divides and the packed B operand is in the
@@ -1159,6 +1172,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   if (is_halo_tile(tile))  // 3x3 stride-1 gathers only (conv fwd / dgrad), K = 9 x Cg
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
+  if (is_ring_tile(tile)) return conv3_ring_fits(a, tile);
   if (tile == 70 || tile == 71 || tile == 74) return wino_applies(a, tile == 70 ? 2 : tile == 71 ? 4 : 6);
   if (tile == 72) return wino_fused_applies(a);
   if (is_dma_tile(tile)) {  // bf16-stored A sources, no split operands
@@ -1180,7 +1194,7 @@ long long igemm_tile_count(const IgemmArgs& a, int tile) {
   int th, tw, bn, ch;
   if (halo_tile_shape(tile, th, tw, bn))
     return (long long)a.a.nimg * ((a.a.Hg + th - 1) / th) * ((a.a.Wg + tw - 1) / tw) * (a.N / bn);
-  if (conv3_dma_tile_shape(tile, th, bn, ch))
+  if (conv3_dma_tile_shape(tile, th, bn, ch) || conv3_ring_tile_shape(tile, th, bn, ch))
     return (long long)a.a.nimg * ((a.a.Hg + th - 1) / th) * ((a.a.Wg + 31) / 32) * (a.N / bn);
   return (long long)((a.M + t.bm - 1) / t.bm) * (a.N / t.bn);
 }
@@ -1259,6 +1273,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 31: case 32: case 33: case 34: case 35: case 36:
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
     case 63: case 65: case 66: case 67: case 68: return go_conv3_dma_tile(a, s, tile);
+    case 81: case 82: case 83: case 84: return go_conv3_ring_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);
     case 71: return launch_wino(a, s, 4);
     case 74: return launch_wino(a, s, 6);

@@ -12,7 +12,7 @@ using namespace unet;
 
 namespace unet {
 extern int g_tune_igemm, g_tune_wgrad, g_autotune, g_force_split, g_force_tile, g_concurrent, g_wino_max,
-    g_wino_dgrad_max, g_wino_wgrad_max;
+    g_wino_dgrad_max, g_wino_wgrad_max, g_bf16_norm, g_bn_fold;
 hipError_t launch_fill(float* p, size_t n, float v, hipStream_t s);
 hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream_t s);
 }  // namespace unet
@@ -373,6 +373,8 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "force_tile") g_force_tile = value;
   else if (k == "concurrent") g_concurrent = value;
   else if (k == "wino_max") g_wino_max = value;
+  else if (k == "bf16_norm") g_bf16_norm = value != 0;
+  else if (k == "bn_fold") g_bn_fold = value != 0;
   else if (k == "wino_dgrad_max") g_wino_dgrad_max = value;
   else if (k == "wino_wgrad_max") g_wino_wgrad_max = value;
   else if (k == "op_a16") g_op_a16 = value != 0;

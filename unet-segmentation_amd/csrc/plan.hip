@@ -32,6 +32,16 @@ int g_autotune = getenv("UNET_AUTOTUNE") ? atoi(getenv("UNET_AUTOTUNE")) : 1;
 // unet_set_tuning("concurrent", v) or UNET_CONCURRENT (default on): weight
 // gradients on a side stream
 int g_concurrent = getenv("UNET_CONCURRENT") ? atoi(getenv("UNET_CONCURRENT")) : 1;
+// unet_set_tuning("bf16_norm", v) or UNET_BF16_NORM (default off): bf16 plans
+// materialise relu(bn(y)) once per element (the normalised copy every GEMM
+// consumer stages as a plain operand); off: consumers transform on load.
+// Read at plan creation (workspace layout).
+int g_bf16_norm = getenv("UNET_BF16_NORM") ? atoi(getenv("UNET_BF16_NORM")) : 0;
+// unet_set_tuning("bn_fold", v) or UNET_BN_FOLD (default on): eval forwards
+// fold each BatchNorm into its conv (scale into the packed weights, scale *
+// bias + shift as the bias) and store relu(conv') in the epilogue, so every
+// consumer reads a plain operand
+int g_bn_fold = getenv("UNET_BN_FOLD") ? atoi(getenv("UNET_BN_FOLD")) : 1;
 // unet_set_tuning("force_split", k) / ("force_tile", id): every igemm site
 // runs split-K k and/or tile id where they apply (tests)
 int g_force_split = 0;
@@ -64,6 +74,7 @@ struct Conv {
   int ci = 0, co = 0, hi = 0, wi = 0, ho = 0, wo = 0;
   int pw = 0, gw = 0;  // param / grad table base (conv w, b, bn w, bn b, rm, rv, nbt)
   Buf y, mean, invstd, scale, shift, wf, wd, dwp, dz, dyp, coef, stats, bstats;
+  Buf a;  // bf16 plans: relu(bn(y)) in bf16, the operand its GEMM consumers read
 };
 struct ConvT {
   int ci = 0, co = 0, h = 0, w = 0;  // input grid (h, w) -> output (2h, 2w)
@@ -95,6 +106,8 @@ struct unet_plan {
   Pool P[4];
   Skip S[4];
   Buf stat_region, dwp_region, head_acc, wce_acc, first_slabs;
+  Buf fold0w;         // inc.c0 weights with its BatchNorm folded in (eval)
+  bool fold = false;  // this forward folds BatchNorm into the convs (eval + g_bn_fold)
   // weight-gradient GEMMs run on a side stream beside the dY -> dX chain of the
   // backward (joined at the end of every backward call)
   hipStream_t side = nullptr;
@@ -264,7 +277,7 @@ std::string igemm_key(const IgemmArgs& a) {
   char b[240];
   const Epilogue& e = a.e;
   const int epi = (e.shuffle_co ? 1 : 0) | (e.stats ? 2 : 0) | (e.yref ? 4 : 0) | (e.colsum1 ? 8 : 0) |
-                  (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0);
+                  (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0) | (e.relu ? 64 : 0);
   // the Winograd caps decide which candidates exist: a choice tuned under other
   // caps is a different key
   snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d wino=%d/%d tt=%d",
@@ -287,7 +300,8 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
-                36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 70, 71, 72, 74}) {  // fits() filters by precision and gather
+                36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 81, 82, 83, 84, 70, 71, 72,
+                74}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t)) continue;
     v.push_back({t, 1});
     if (t == 70 || t == 71 || t == 74)  // Winograd: no K split; the tile of its batched point GEMMs
@@ -491,10 +505,26 @@ Src src_of(const Ctx& c, const Conv& L, bool transform) {
   s.W = L.wo;
   s.C = L.co;
   s.h16 = c.p->prec == UNET_PREC_BF16;  // raw conv outputs of a bf16 plan are stored bf16
-  if (transform) {
+  if (transform && !c.p->fold) {  // folded eval: y is already relu(bn(conv))
     s.scale = c.f(L.scale);
     s.shift = c.f(L.shift);
   }
+  return s;
+}
+
+// Layer l's output as its GEMM consumers read it: relu(bn(y)).  bf16 plans
+// read the normalised bf16 copy (written once per element after the layer's
+// statistics are final: k_bn_relu_bf, or the max-pool for encoder outputs), so
+// their staging is a plain copy; fp32 plans apply BN+ReLU on load.
+Src src_in(const Ctx& c, int l) {
+  const Conv& L = c.p->L[l];
+  if (!L.a.bytes || c.p->fold) return src_of(c, L, true);
+  Src s;
+  s.ptr = c.f(L.a);
+  s.H = L.ho;
+  s.W = L.wo;
+  s.C = L.co;
+  s.h16 = 1;
   return s;
 }
 
@@ -510,7 +540,7 @@ Gather input_gather(const Ctx& c, int l) {
   g.Wg = L.wo;
   g.nimg = p->n;
   if (l % 2 == 1) {  // second conv of a DoubleConv: input = relu(bn(y[l-1]))
-    g.s[0] = src_of(c, p->L[l - 1], true);
+    g.s[0] = src_in(c, l - 1);
     g.Cg = g.c_split = L.ci;
   } else if (l <= 8) {  // first conv of down block: pooled tensor
     const Pool& pl = p->P[l / 2 - 1];
@@ -526,7 +556,7 @@ Gather input_gather(const Ctx& c, int l) {
     const int k = (l - 10) / 2;
     const Skip& sk = p->S[k];
     const int enc = 7 - 2 * k;
-    Src a = src_of(c, p->L[enc], true);
+    Src a = src_in(c, enc);
     a.oy = sk.oy;
     a.ox = sk.ox;
     Src b;
@@ -551,6 +581,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
   // follows it (BN stats, BN-bwd stats, convT bias sums, head/loss sums, and in
   // train mode the packed weight-gradient region, laid out right after).
   CK(hipMemsetAsync(ws + p->stat_region.off, 0, p->stat_region.bytes + (train ? p->dwp_region.bytes : 0), s));
+  p->fold = !train && unet::g_bn_fold;
   // ---- repack weights (per call: the optimizer moves them every step) ----
   {
     Timer t(p, s, UNET_KC_ELEMWISE, 0, 0);
@@ -562,17 +593,27 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       ConvT& T = p->T[k];
       CK(launch_pack_convT(P<float>(prm, T.pw), T.ci, T.co, c.f(T.wf), c.f(T.wd), s));
     }
+    if (!train) {  // BatchNorm from the running statistics (scripts/predict.py:70 model.eval())
+      for (int l = 0; l < 18; ++l) {
+        Conv& L = p->L[l];
+        CK(launch_bn_eval_prepare(L.co, P<float>(prm, L.pw + 2), P<float>(prm, L.pw + 3), P<float>(prm, L.pw + 4),
+                                  P<float>(prm, L.pw + 5), c.f(L.scale), c.f(L.shift), kEps, s));
+      }
+    }
+    if (p->fold) {  // bn(conv(x)) = conv'(x): scale into the weights, folded bias into L.coef
+      const Conv& L0 = p->L[0];
+      CK(launch_fold_bn(P<float>(prm, L0.pw), 9LL * L0.ci, L0.co, c.f(L0.scale), c.f(L0.shift),
+                        P<float>(prm, L0.pw + 1), c.f(p->fold0w), c.f(L0.coef), s));
+      for (int l = 1; l < 18; ++l) {
+        Conv& L = p->L[l];
+        CK(launch_fold_bn(c.f(L.wf), 9LL * L.ci, L.co, c.f(L.scale), c.f(L.shift), P<float>(prm, L.pw + 1),
+                          c.f(L.wf), c.f(L.coef), s));
+      }
+    }
     if (p->prec != UNET_PREC_FP32) {
       uint16_t* hi = reinterpret_cast<uint16_t*>(c.u8(p->pack16));
       const size_t ne = p->pack_region.bytes / 4;
       CK(launch_f2bf(c.f(p->pack_region), hi, ne, s, p->prec == UNET_PREC_BF16X3 ? hi + ne : nullptr));
-    }
-  }
-  if (!train) {
-    for (int l = 0; l < 18; ++l) {
-      Conv& L = p->L[l];
-      CK(launch_bn_eval_prepare(L.co, P<float>(prm, L.pw + 2), P<float>(prm, L.pw + 3), P<float>(prm, L.pw + 4),
-                                P<float>(prm, L.pw + 5), c.f(L.scale), c.f(L.shift), kEps, s));
     }
   }
   auto finalize = [&](int l) -> int {
@@ -584,23 +625,35 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
                           kEps, s));
     return 0;
   };
+  // bf16 plans: the normalised copy of layer l's output (encoder outputs get it
+  // from their max-pool, which reads every element with the transform anyway)
+  auto normalise = [&](int l) -> int {
+    Conv& L = p->L[l];
+    if (!L.a.bytes || p->fold || (l <= 7 && l % 2 == 1)) return 0;
+    Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * L.ho * L.wo * L.co);
+    CK(launch_bn_relu_bf(reinterpret_cast<const uint16_t*>(c.f(L.y)), c.f(L.scale), c.f(L.shift),
+                         (long long)n * L.ho * L.wo, L.co, reinterpret_cast<uint16_t*>(c.f(L.a)), s));
+    return 0;
+  };
   // ---- inc.c0 ----
   {
     Conv& L = p->L[0];
     Timer t(p, s, UNET_KC_STAGE1, conv_flops(L, n),
             4.0 * n * (double)p->cin * p->h * p->w +
                 (p->prec == UNET_PREC_BF16 ? 2.0 : 4.0) * n * (double)L.ho * L.wo * L.co);
-    CK(launch_conv_first_fwd(x, n, p->cin, p->h, p->w, P<float>(prm, L.pw), P<float>(prm, L.pw + 1), L.co,
-                             c.f(L.y), train ? c.d(L.stats) : nullptr, s, p->prec == UNET_PREC_BF16));
+    CK(launch_conv_first_fwd(x, n, p->cin, p->h, p->w, p->fold ? c.f(p->fold0w) : P<float>(prm, L.pw),
+                             p->fold ? c.f(L.coef) : P<float>(prm, L.pw + 1), L.co, c.f(L.y),
+                             train ? c.d(L.stats) : nullptr, s, p->prec == UNET_PREC_BF16, p->fold));
   }
   if (int r = finalize(0)) return r;
+  if (int r = normalise(0)) return r;
   for (int l = 1; l < 18; ++l) {
     Conv& L = p->L[l];
     if (l >= 10 && l % 2 == 0) {  // ConvTranspose2d of up block k, input = y[l-1]
       const int k = (l - 10) / 2;
       ConvT& T = p->T[k];
       IgemmArgs a;
-      a.a.s[0] = src_of(c, p->L[l - 1], true);
+      a.a.s[0] = src_in(c, l - 1);
       a.a.s[1] = a.a.s[0];
       a.a.Cg = a.a.c_split = T.ci;
       a.a.Hg = T.h;
@@ -623,7 +676,8 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
     a.M = n * L.ho * L.wo;
     a.N = L.co;
     a.K = 9 * L.ci;
-    a.e.bias = P<float>(prm, L.pw + 1);
+    a.e.bias = p->fold ? c.f(L.coef) : P<float>(prm, L.pw + 1);
+    a.e.relu = p->fold;
     a.e.d[0] = Dst{c.f(L.y), L.ho, L.wo, L.co, 0, 0, p->prec == UNET_PREC_BF16};
     a.e.stats = train ? c.d(L.stats) : nullptr;
     {
@@ -632,10 +686,12 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       CK(run_igemm(c, a));
     }
     if (int r = finalize(l)) return r;
+    if (int r = normalise(l)) return r;
     if (l <= 7 && l % 2 == 1) {  // encoder output -> MaxPool2d(2)
       Pool& pl = p->P[l / 2];
       Timer t(p, s, UNET_KC_ELEMWISE, 0, 4.0 * n * pl.h * pl.w * pl.c * 1.25);
-      CK(launch_maxpool_fwd(src_of(c, L, true), n, pl.h, pl.w, c.f(pl.p), c.u8(pl.arg), s, p->prec == UNET_PREC_BF16));
+      CK(launch_maxpool_fwd(src_of(c, L, true), n, pl.h, pl.w, c.f(pl.p), c.u8(pl.arg), s, p->prec == UNET_PREC_BF16,
+                            L.a.bytes && !p->fold ? reinterpret_cast<uint16_t*>(c.f(L.a)) : nullptr));
     }
   }
   {
@@ -824,7 +880,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       Conv& Q = p->L[l - 1];
       {
         WgradArgs w;
-        w.ga.s[0] = src_of(c, Q, true);
+        w.ga.s[0] = src_in(c, l - 1);
         w.ga.s[1] = w.ga.s[0];
         w.ga.Cg = w.ga.c_split = T.ci;
         w.ga.Hg = T.h;
@@ -1085,6 +1141,7 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
       p->pack16 = al.take(p->pack_region.bytes / 2 * (prec == UNET_PREC_BF16X3 ? 2 : 1));
   }
   // everything a forward touches (train or eval) ...
+  p->fold0w = al.take(fsz(64LL * c_in * 9));
   for (int l = 0; l < 18; ++l) {
     Conv& L = p->L[l];
     const long long pix = (long long)n * L.ho * L.wo;
@@ -1094,6 +1151,8 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     L.scale = al.take(fsz(L.co));
     L.shift = al.take(fsz(L.co));
     L.coef = al.take(fsz(4LL * L.co));
+    if (prec == UNET_PREC_BF16 && unet::g_bf16_norm && l < 17)
+      L.a = al.take((size_t)pix * L.co * 2);  // head reads y17 itself
   }
   for (int k = 0; k < 4; ++k) {
     ConvT& T = p->T[k];

@@ -54,6 +54,9 @@ struct Epilogue {
   int shuffle_co = 0;            // >0: ConvTranspose2d k2s2 pixel shuffle
   Dst d[2];
   int n_split = 1 << 30;         // columns < n_split -> d[0], else d[1]
+  // eval with BatchNorm folded into the weights (scripts/predict.py's
+  // model.eval()): the stored value is relu(conv + folded bias), no statistics
+  int relu = 0;
   // forward BN statistics of the stored values: stats[g][col][2] (sum, sumsq)
   double* stats = nullptr;
   // backward: mask the d[0] values with ReLU'(yref*scale+shift) and collect
@@ -141,6 +144,10 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
 // bf16 halo conv with LDS-DMA weights (conv3_dma.hip), tile ids 63 and 65-68
 bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch);
 hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);
+// bf16 3x3 conv with LDS-DMA halo / weight rings (conv3_ring.hip), tile ids 81-84
+bool conv3_ring_tile_shape(int tile, int& th, int& bn, int& ck);
+bool conv3_ring_fits(const IgemmArgs& a, int tile);
+hipError_t go_conv3_ring_tile(const IgemmArgs& a, hipStream_t s, int tile);
 int num_cus();
 hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s);  // heuristic
 hipError_t launch_igemm_v(const IgemmArgs& a, hipStream_t s, GemmChoice c);
@@ -194,7 +201,10 @@ hipError_t launch_elastic(const uint8_t* img, const uint16_t* lab, int n, int h,
 // inc.c0: Ci in {1,2,3,4} direct conv from an NCHW input; y NHWC (Co = 64 multiple).
 hipError_t launch_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w,
                                  const float* wt_oihw, const float* bias, int co, float* y,
-                                 double* stats, hipStream_t s, int out_h16 = 0);
+                                 double* stats, hipStream_t s, int out_h16 = 0, int relu = 0);
+// eval BatchNorm fold: wout[r][:] = w[r][:] * scale[r], bias_out[r] = scale[r] * bias[r] + shift[r]
+hipError_t launch_fold_bn(const float* w, long long K, int rows, const float* scale, const float* shift,
+                          const float* bias, float* wout, float* bias_out, hipStream_t s);
 // Written per workgroup into `slabs` (conv_first_wgrad_ws_bytes) then reduced
 // into dw_oihw (overwritten, not accumulated).
 constexpr int kFirstWgradSlabs = 2048;
@@ -225,9 +235,13 @@ hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const 
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h,
                             int w, int c, float* dypad, int pad, hipStream_t s, int out_h16 = 0,
                             int y_h16 = 0, int dz_h16 = 0);
-// MaxPool2d(2) fwd with BN+ReLU transform on load (src grid H x W, pooled H/2 x W/2).
+// MaxPool2d(2) fwd with BN+ReLU transform on load (src grid H x W, pooled H/2 x W/2);
+// anorm (bf16 plans): also writes every window element's relu(bn(.)) in bf16.
 hipError_t launch_maxpool_fwd(const Src& src, int n, int h, int w, float* y, uint8_t* arg,
-                              hipStream_t s, int out_h16 = 0);
+                              hipStream_t s, int out_h16 = 0, uint16_t* anorm = nullptr);
+// a = bf16(relu(y * scale + shift)), y bf16 NHWC (pixels x c, c % 8 == 0)
+hipError_t launch_bn_relu_bf(const uint16_t* y, const float* scale, const float* shift, long long pixels, int c,
+                             uint16_t* a, hipStream_t s);
 // Maxpool bwd fused: dz = route(dpool) + crop-embedded dskip (may be null), then
 // ReLU mask + BN-bwd stats (if scale != null).  Writes dz' (n,h,w,c).
 hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, const float* dskip,

@@ -174,6 +174,7 @@ __global__ __launch_bounds__(256) void k_wino_out(const float* __restrict__ m, l
           } else if (second && e.colsum1) {
             s1 = s1 + v;
           }
+          if (e.relu) v = make_float4(fmaxf(v.x, 0.f), fmaxf(v.y, 0.f), fmaxf(v.z, 0.f), fmaxf(v.w, 0.f));
           st4(dptr + idx, v);
         }
     }
@@ -421,7 +422,8 @@ __global__ __launch_bounds__(256) void k_wino4_out(const float* __restrict__ m, 
           } else if (second && e.colsum1) {
             s1 += v;
           }
-          dptr[idx] = v;
+          if (e.relu) v = fmaxf(v, 0.f);
+        dptr[idx] = v;
         }
       }
     }
@@ -662,6 +664,7 @@ __global__ __launch_bounds__(256) void k_wino6_out(const float* __restrict__ m, 
           } else if (second && e.colsum1) {
             s1 += v;
           }
+          if (e.relu) v = fmaxf(v, 0.f);
           dptr[idx] = v;
         }
       }
@@ -905,6 +908,7 @@ __device__ __forceinline__ void wf_output(float* lds, int tid, long long t0, int
         } else if (second && e.colsum1) {
           s1 += v;
         }
+        if (e.relu) v = fmaxf(v, 0.f);
         dptr[idx] = v;
       }
     }
