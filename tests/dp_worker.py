@@ -43,9 +43,11 @@ def main():
     m = m.cuda().train()
     tr = Trainer(m, BATCH, SIZE, SIZE, lr=1e-4, momentum=0.99, process_group=dist.group.WORLD, overlap=overlap,
                  comm_dtype=comm)
+    tr.defer_join = os.environ.get("UNET_DP_DEFER", "1") != "0"
     x, t, w = (torch.from_numpy(a).cuda() for a in shard(rank))
     res = {}
     for s in range(steps):
+        res[f"w{s}"] = tr.flat.flat.cpu().numpy().copy()         # weights this step starts from
         loss = tr.forward_loss(x, t, w)
         tr.backward_and_reduce(x)
         torch.cuda.synchronize()

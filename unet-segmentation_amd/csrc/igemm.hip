@@ -1090,7 +1090,9 @@ int g_tune_wgrad = env_int("UNET_WGRAD_VARIANT", -1);
 int g_wino_max = env_int("UNET_WINO_MAX", 4);
 int g_wino_dgrad_max = env_int("UNET_WINO_DGRAD_MAX", 4);  // input gradients (no forward BN statistics)
 int g_wino_wgrad_max = env_int("UNET_WINO_WGRAD_MAX", 6);
-static int wino_tile_m(int tile) { return tile == 70 ? 2 : tile == 71 || tile == 72 ? 4 : tile == 74 ? 6 : 0; }
+static int wino_tile_m(int tile) {
+  return tile == 70 ? 2 : tile == 71 || tile == 72 || tile == 73 ? 4 : tile == 74 ? 6 : 0;
+}
 
 // igemm tile table: id -> (BM, BN, waves M x N, BK), resident workgroups per CU
 // (min of the LDS and VGPR limits of the built kernels).
@@ -1144,6 +1146,7 @@ static TileInfo tile_info(int id) {
     // Winograd F(2x2, 3x3) (winograd.hip): no K split
     case 70: case 71: case 74: return {256, 64, 9, 2};
     case 72: return {32, 32, 16, 1};
+    case 73: return {32, 64, 8, 1};
     // fp32 halo-tiled 3x3 (k_conv3_f32): bk = one 16-channel chunk x 9 taps
     case 51: return {256, 64, 144, 2};
     case 52: return {256, 64, 144, 2};
@@ -1175,6 +1178,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   if (is_ring_tile(tile)) return conv3_ring_fits(a, tile);
   if (tile == 70 || tile == 71 || tile == 74) return wino_applies(a, tile == 70 ? 2 : tile == 71 ? 4 : 6);
   if (tile == 72) return wino_fused_applies(a);
+  if (tile == 73) return wino_fused64_applies(a);
   if (is_dma_tile(tile)) {  // bf16-stored A sources, no split operands
     const int ch = tile_info(tile).bk / 9;
     const bool two = a.a.c_split < a.a.Cg;
@@ -1278,6 +1282,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 71: return launch_wino(a, s, 4);
     case 74: return launch_wino(a, s, 6);
     case 72: return launch_wino_fused(a, s);
+    case 73: return launch_wino_fused64(a, s);
     case 51: return go_halo32<8, 32, 64, 8, 1, 4>(a, s);
     case 52: return go_halo32<16, 16, 64, 8, 1, 4>(a, s);
     case 53: return go_halo32<8, 32, 64, 4, 1, 2>(a, s);
@@ -1427,7 +1432,7 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c) {
   int t = c.tile;
   if (t < 0 && g_tune_igemm >= 70 && g_tune_igemm <= 74 && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;
-  if ((t >= 70 && t <= 72) || t == 74) {
+  if (t >= 70 && t <= 74) {
     const int mt = t == 70 ? 2 : t == 74 ? 6 : 4;
     const Gather& g = a.a;
     const double T = (double)g.nimg * ((g.Hg + mt - 1) / mt) * ((g.Wg + mt - 1) / mt);

@@ -1149,8 +1149,8 @@ __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
   __syncthreads();
   for (; t < tiles; t += gridDim.z) {
     const bool more = t + (int)gridDim.z < tiles;
-    if (more) issue(t + gridDim.z);
-    compute();
+    if (more && !(args.abl & 4)) issue(t + gridDim.z);
+    if (!(args.abl & 2)) compute();
     __syncthreads();
     if (more) {
       commit();
@@ -1166,7 +1166,8 @@ __global__ __launch_bounds__(512, 2) void k_wgrad3_bf(const WgradArgs args) {
       for (int r = 0; r < 16; ++r) {
         const int row = i0 + ct * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = (tap0 + j) * Ci + cb + it_ * 32 + li;
-        atomicAdd(args.out + (size_t)row * args.No + col, acc[j][r]);
+        if (args.abl & 1) args.out[(size_t)row * args.No + col] = acc[j][r];
+        else atomicAdd(args.out + (size_t)row * args.No + col, acc[j][r]);
       }
     }
   }
@@ -1192,7 +1193,10 @@ static hipError_t go_wgrad3(const WgradArgs& a, hipStream_t s, int per_cu) {
   int splits = (per_cu * num_cus() + blocks - 1) / blocks;
   splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
   dim3 grid(a.Mo / 64, a.gb.Cg / 64, splits);
-  hipLaunchKernelGGL((k_wgrad3_bf<TH, TW, D16, SPLIT>), grid, dim3(512), smem, s, a);
+  static const int abl = getenv("UNET_WG_ABL") ? atoi(getenv("UNET_WG_ABL")) : 0;
+  WgradArgs b = a;
+  b.abl = abl;
+  hipLaunchKernelGGL((k_wgrad3_bf<TH, TW, D16, SPLIT>), grid, dim3(512), smem, s, b);
   return hipGetLastError();
 }
 

@@ -116,6 +116,10 @@ struct WgradArgs {
   // Winograd F(4x4, 3x3) weight gradient (wgrad tile 71, winograd.hip): scratch
   float* wino_ws = nullptr;
   size_t wino_ws_bytes = 0;
+  // timing ablations of k_wgrad3_bf (UNET_WG_ABL; results wrong with any bit):
+  // 1 = plain stores instead of the output atomics, 2 = no MFMA, 4 = no operand
+  // loads after the first tile
+  int abl = 0;
 };
 
 // ---------------- launchers (kernels.hip) ----------------
@@ -135,7 +139,9 @@ bool wino_applies(const IgemmArgs& a, int mt);           // mt = 2: F(2x2, 3x3),
 hipError_t launch_wino(const IgemmArgs& a, hipStream_t s, int mt);
 bool wino_wgrad_applies(const WgradArgs& a, int mt);  // weight gradient, mt = 4 (wgrad tile 71) / 6 (74)
 bool wino_fused_applies(const IgemmArgs& a);  // tile 72: fused F(4x4, 3x3)
+bool wino_fused64_applies(const IgemmArgs& a);  // tile 73: fused F(4x4, 3x3), 64 output channels
 hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s);
+hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s);
 // MFMA flops a GEMM launch executes with variant c (Winograd: 2 * points *
 // tiles * Cg * N; otherwise the direct 2 * M * N * K)
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c);

@@ -1151,6 +1151,239 @@ hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s) {
   return hipGetLastError();
 }
 
+// ---------------------------------------------------------------------------
+// Fused F(4x4, 3x3), 64 output channels (tile 73).  k_wino4f's input transform
+// (and the loads + BatchNorm in front of it) is done once per 32 tiles x 32
+// output channels; f32 MFMA and that VALU work share the SIMD, so the kernel
+// runs at their sum.  Here a workgroup owns 32 tiles x 64 output channels and
+// walks the input channels in chunks of 8, which halves the transform work per
+// MFMA at the same LDS (U 32 tiles x 8 + V 64 outputs x 8 per point) and the
+// same 72 MFMAs per wave and chunk:
+//   * 256 patches (32 tiles x 8 channels) per chunk, two threads per patch:
+//     lanes of 16-lane row 2r take the patch's columns 0..2, row 2r + 1 its
+//     columns 3..5 (same tile / channel by lane & 15).  Each transforms its
+//     three columns (B^T d), then v_permlane16_swap exchanges the halves so
+//     that the even row holds rows 0..2 and the odd row rows 3..5 of all six
+//     columns (no lane-dependent selects), and each applies the row transform
+//     to its three rows: 18 loads, 6 bt6 and 9 swaps per thread and chunk;
+//   * V (k_wino4f_w8, layout [Cg/8][36][N][8], 8-float rows pre-swizzled) is
+//     copied row for row: 9 float4 per thread;
+//   * LDS rows are 8 floats; slot s (2 floats) of row r holds channels (q, q+4)
+//     with s = q ^ (2 ((r >> 3) & 1)), so the ds_read_b64 of a 16x16x4 operand
+//     (lane quarter q: k = q in step 0, q + 4 in step 1) hits 64 banks;
+//   * wave w: tile half w & 1, points 9 (w >> 1) .. +8, the four 16-channel
+//     output blocks: per point one U read, four V reads, eight MFMAs;
+//   * the accumulators leave in two 32-channel passes through wf_output.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int wf8_slot(int row, int q) { return (q ^ (((row >> 3) & 1) << 1)) << 1; }
+
+__global__ void k_wino4f_w8(const float* __restrict__ b, int N, int Cg, float* __restrict__ v) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)N * Cg) return;
+  const int n = (int)(i / Cg), c = (int)(i - (long long)n * Cg);
+  float tg[6][3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    float col[3] = {b[((size_t)n * 9 + 0 + k) * Cg + c], b[((size_t)n * 9 + 3 + k) * Cg + c],
+                    b[((size_t)n * 9 + 6 + k) * Cg + c]};
+    float r[6];
+    g6(col, r);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) tg[a][k] = r[a];
+  }
+  const size_t base = (size_t)(c >> 3) * 36 * N;
+  const int pos = wf8_slot(n, c & 3) + ((c >> 2) & 1);  // n & 63 and n agree on bit 3
+#pragma unroll
+  for (int a = 0; a < 6; ++a) {
+    float r[6];
+    g6(tg[a], r);
+#pragma unroll
+    for (int bb = 0; bb < 6; ++bb) v[(base + (size_t)(a * 6 + bb) * N + n) * 8 + pos] = r[bb];
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __restrict__ V, int N, long long T,
+                                                     int Th, int Tw, int NB, Epilogue e) {
+  constexpr int PU = 32 * 8 + 8;  // U point plane (+8: the two lane rows of a patch store 18 planes apart)
+  constexpr int PV = 64 * 8;      // V point plane
+  __shared__ __attribute__((aligned(16))) float lds[36 * 1024];  // U + V, then X [36][32][32]
+  float* Us = lds;
+  float* Vs = lds + 36 * PU;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  long long bid = blockIdx.x;
+  const long long G = gridDim.x;
+  if ((G & 7) == 0) bid = (bid & 7) * (G >> 3) + (bid >> 3);  // an XCD's workgroups share tiles
+  const int nb = (int)(bid % NB);
+  const long long t0 = (bid / NB) * 32;
+  const int n0 = nb * 64;
+
+  // ---- loader role: patch (tile lt, channel lc), column half hf ----
+  const int hf = (lane >> 4) & 1;
+  const int pt = wave * 32 + (lane & 15) + ((lane >> 5) << 4);
+  const int lt = pt >> 3, lc = pt & 7;
+  const long long t = t0 + lt;
+  int img = 0, ty = 0, tx = 0;
+  if (t < T) {
+    tx = (int)(t % Tw);
+    const long long r = t / Tw;
+    ty = (int)(r % Th);
+    img = (int)(r / Th);
+  }
+  const int vrows = t < T ? min(6, g.Hg + 2 - 4 * ty) : 0;
+  const int vcols = t < T ? min(6, g.Wg + 2 - 4 * tx) : 0;
+  const bool wfull = __all(vrows == 6 && vcols == 6);
+  // this thread's three output rows 3 hf .. 3 hf + 2 of the transformed patch
+  float* const ubase = Us + (3 * hf) * 6 * PU + lt * 8 + wf8_slot(lt, lc & 3) + (lc >> 2);
+  float raw[18];  // [row 0..5][column 3 hf + 0..2]
+  float4 vr[9];
+  const int nk = g.Cg >> 3;
+  auto load = [&](int kc) {
+    const bool second = kc * 8 >= g.c_split;  // c_split % 8 == 0: uniform source
+    const float* sp = second ? g.s[1].ptr : g.s[0].ptr;
+    const int sH = second ? g.s[1].H : g.s[0].H, sW = second ? g.s[1].W : g.s[0].W;
+    const int sC = second ? g.s[1].C : g.s[0].C;
+    const int soy = second ? g.s[1].oy : g.s[0].oy, sox = second ? g.s[1].ox : g.s[0].ox;
+    const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    const char* sb = reinterpret_cast<const char*>(sp);
+    const unsigned o0 = ((unsigned)((img * sH + 4 * ty + soy) * sW + 4 * tx + sox) * sC + cl) * 4u;
+    const unsigned rs = (unsigned)sW * sC * 4u, cs = (unsigned)sC * 4u;
+    if (wfull) {
+      const unsigned oh = o0 + 3u * hf * cs;
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 3; ++xx)
+          raw[yy * 3 + xx] = *reinterpret_cast<const float*>(sb + (oh + (yy * rs + xx * cs)));
+    } else {  // clamp to the last in-window row / column (zeroed in commit)
+      const unsigned lr = (unsigned)max(vrows - 1, 0), lcn = (unsigned)max(vcols - 1, 0);
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 3; ++xx)
+          raw[yy * 3 + xx] = *reinterpret_cast<const float*>(
+              sb + (o0 + (min((unsigned)yy, lr) * rs + min((unsigned)(3 * hf + xx), lcn) * cs)));
+    }
+    const char* vb = reinterpret_cast<const char*>(V + ((size_t)kc * 36 * N + n0) * 8);
+    const unsigned vo = ((unsigned)(tid >> 7) * N * 8u + (tid & 127) * 4u) * 4u;
+    const unsigned vstep = 4u * N * 8u * 4u;  // 4 points per 512 float4
+#pragma unroll
+    for (int j = 0; j < 9; ++j) vr[j] = *reinterpret_cast<const float4*>(vb + (vo + j * vstep));
+  };
+  auto commit = [&](int kc) {
+    const bool second = kc * 8 >= g.c_split;
+    const float* scp = second ? g.s[1].scale : g.s[0].scale;
+    const float* shp = second ? g.s[1].shift : g.s[0].shift;
+    const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    if (scp) {
+      const float sc = scp[cl], sh = shp[cl];
+#pragma unroll
+      for (int q = 0; q < 18; ++q) raw[q] = fmaxf(fmaf(raw[q], sc, sh), 0.f);
+    }
+    if (!wfull) {
+#pragma unroll
+      for (int q = 0; q < 18; ++q) raw[q] = (q / 3 < vrows && 3 * hf + q % 3 < vcols) ? raw[q] : 0.f;
+    }
+#pragma unroll
+    for (int xx = 0; xx < 3; ++xx) {  // columns in place: raw[a][xx] = (B^T d)[a][3 hf + xx]
+      float d[6];
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy) d[yy] = raw[yy * 3 + xx];
+      float rr[6];
+      bt6(d, rr);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) raw[a * 3 + xx] = rr[a];
+    }
+    // X = rows 0..2, Y = rows 3..5 of this thread's columns; the swap trades
+    // the odd lane row's X for the even lane row's Y: the even row then holds
+    // rows 0..2 x columns (0..2 in X, 3..5 in Y), the odd row rows 3..5 alike
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(raw[k]), __float_as_uint(raw[9 + k]),
+                                                       false, false);
+      raw[k] = __uint_as_float(sw[0]);
+      raw[9 + k] = __uint_as_float(sw[1]);
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float d[6] = {raw[a * 3 + 0], raw[a * 3 + 1], raw[a * 3 + 2],
+                          raw[9 + a * 3 + 0], raw[9 + a * 3 + 1], raw[9 + a * 3 + 2]};
+      float rr[6];
+      bt6(d, rr);
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) ubase[(a * 6 + bb) * PU] = rr[bb];
+    }
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int q = tid + 512 * j;
+      st4(Vs + (q >> 7) * PV + (q & 127) * 4, vr[j]);
+    }
+  };
+
+  // ---- MFMA role: tile half th, points 9 pg .. 9 pg + 8, four channel blocks ----
+  const int th = wave & 1, pg = wave >> 1;
+  const int mi = lane & 15, mq = lane >> 4;
+  const int aoff = (16 * th + mi) * 8 + wf8_slot(16 * th + mi, mq);
+  const int boff = mi * 8 + wf8_slot(mi, mq);  // + 128 per 16-channel block (bit 3 of the row unchanged)
+  floatx4 acc[9][4];
+#pragma unroll
+  for (int j = 0; j < 9; ++j)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) acc[j][c] = (floatx4){0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int kc = 0; kc < nk; ++kc) {
+    commit(kc);
+    __syncthreads();
+    if (kc + 1 < nk) load(kc + 1);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int p = pg * 9 + j;
+      const float2 a = *reinterpret_cast<const float2*>(Us + p * PU + aoff);
+      float2 b[4];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) b[c] = *reinterpret_cast<const float2*>(Vs + p * PV + boff + 128 * c);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[j][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[c].x, acc[j][c], 0, 0, 0);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) acc[j][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[c].y, acc[j][c], 0, 0, 0);
+    }
+    __syncthreads();
+  }
+
+  // ---- two 32-channel passes: accumulators -> X[36][32][32] -> wf_output ----
+  float* X = lds;
+#pragma unroll
+  for (int hh = 0; hh < 2; ++hh) {
+    if (hh) __syncthreads();  // pass 0's wf_output has finished reading X / red
+#pragma unroll
+    for (int j = 0; j < 9; ++j)
+#pragma unroll
+      for (int c = 0; c < 2; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          X[(pg * 9 + j) * 1024 + (16 * th + 4 * mq + r) * 32 + 16 * c + mi] = acc[j][2 * hh + c][r];
+    __syncthreads();
+    wf_output(lds, tid, t0, n0 + 32 * hh, T, Th, Tw, N, g, e);
+  }
+}
+
+bool wino_fused64_applies(const IgemmArgs& a) {
+  return wino_fused_applies(a) && a.N % 64 == 0;  // Cg, c_split % 16 == 0 imply % 8
+}
+
+hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s) {
+  if (!wino_fused64_applies(a)) return hipErrorInvalidValue;
+  const Gather& g = a.a;
+  const int Th = (g.Hg + 3) / 4, Tw = (g.Wg + 3) / 4;
+  const long long T = (long long)g.nimg * Th * Tw;
+  float* V = reinterpret_cast<float*>(a.wino_ws);
+  const long long nw = (long long)a.N * g.Cg;
+  const int NB = a.N / 64;
+  const long long G = (T + 31) / 32 * NB;
+  hipLaunchKernelGGL(k_wino4f_w8, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
+  hipLaunchKernelGGL(k_wino4f64, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  return hipGetLastError();
+}
+
 
 
 // ---------------------------------------------------------------------------

@@ -115,6 +115,9 @@ class Trainer:
         self.labels = LabelCheck()
         self._capturing = False
         self.first_step = True
+        # segment s+1's input gradients do not wait for segment s's weight
+        # gradients (False: join the side stream at every segment end)
+        self.defer_join = True
         self.use_graph = bool(graph)
         self._graph = None
         self._graph_key = None
@@ -173,7 +176,8 @@ class Trainer:
         for s in range(N_SEGMENTS):
             # segment s's weight gradients stay on the plan's side stream (no join):
             # segment s+1's input gradients start at once
-            self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, s, s + 1, defer_join=True)
+            self.plan.backward(self.param_tab, self.grad_tab, x, self.dlogits, self.ws, s, s + 1,
+                               defer_join=self.defer_join)
             self.reducer.reduce(s)  # bucket s is final once its side-stream work is: all-reduce it meanwhile
         self.plan.join(x.device)
         self.reducer.wait()
