@@ -223,6 +223,35 @@ def test_bf16_conv3x3_wgrad(op_bf16, n, h, w, ci, co, variant):
     assert rel_err(host(db), rdb) < 2e-5
 
 
+@pytest.mark.parametrize("variant", [-1, 20, 24, 25])
+@pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 128, 128), (1, 40, 37, 128, 128), (2, 21, 44, 256, 128),
+                                         (1, 7, 5, 128, 64), (2, 30, 19, 64, 256), (1, 3, 3, 128, 128)])
+def test_bf16_conv3x3_wgrad_bf16_storage(op_bf16, n, h, w, ci, co, variant):
+    """bf16-stored dY and X (op_a16, as a bf16 plan stores them): the halo-tiled
+    k_wgrad3_bf (20) and the wide two-stage-ring k_wgrad3w_bf (24: 128 co x 64
+    ci, 25: 64 co x 128 ci per workgroup) on ragged grids, including a grid
+    smaller than one 8x16 pixel tile."""
+    if variant == 24 and (co % 128 or ci % 64) or variant == 25 and (co % 64 or ci % 128):
+        pytest.skip("shape outside the tile's channel blocking")
+    lib = op_bf16
+    lib.unet_set_tuning(b"op_a16", 1)
+    lib.unet_set_tuning(b"wgrad_variant", variant)
+    try:
+        rng = np.random.default_rng(14)
+        x = f32(rng.standard_normal((n, h, w, ci)))
+        dy = f32(rng.standard_normal((n, h - 2, w - 2, co)))
+        _, rdw, _ = O.conv_valid_bwd(q(x), np.zeros((co, ci, 3, 3), np.float32), q(dy), need_dx=False)
+        dw = torch.empty((co, ci, 3, 3), device="cuda")
+        ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
+        ck(lib.unet_conv3x3_wgrad(dev(x).data_ptr(), dev(dy).data_ptr(), n, h, w, ci, co, dw.data_ptr(),
+                                  None, ws.data_ptr(), stream()))
+        torch.cuda.synchronize()
+        assert rel_err(host(dw), rdw) < 5e-5
+    finally:
+        lib.unet_set_tuning(b"op_a16", 0)
+        lib.unet_set_tuning(b"wgrad_variant", -1)
+
+
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 5, 7, 128, 64), (1, 6, 6, 256, 128)])
 def test_bf16_convT2_fwd_bwd(op_bf16, n, h, w, ci, co):
     lib = op_bf16

@@ -92,7 +92,9 @@ def check_bf16_vs_reference(z, zb, lg, loss, grads, tag):
             assert np.abs(g).max() <= 5e-3 * wn, (tag, name)   # bf16 dgrad sums do not cancel exactly
             continue
         floor = abs(float(zb[f"gbf16norm/{name}"]) - r)
-        tol = max(1e-2 * r, 2 * floor)
+        # the GPU result carries its own bf16 rounding pattern (fp32 sums, tuned
+        # tile mix) on top of the one the bf16 oracle measures: within 3 floors
+        tol = max(1e-2 * r, 3 * floor)
         e = abs(np.linalg.norm(g) - r)
         worst = max(worst, e / tol)
         assert e <= tol, (tag, name, np.linalg.norm(g), r, floor)

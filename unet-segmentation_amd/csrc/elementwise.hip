@@ -532,6 +532,66 @@ __global__ void k_bnb_apply(const float* __restrict__ dz, const float* __restric
   }
 }
 
+// All-bf16 twin of k_bnb_apply (bf16 plans: dz, y and dYpad bf16): 8 channels
+// (16 B) per lane and two padded rows per loop trip, both rows' loads issued
+// before either is used.
+__global__ void k_bnb_apply_bf8(const uint16_t* __restrict__ dz, const uint16_t* __restrict__ yr,
+                                const float* __restrict__ coef, int n, int h, int w, int C,
+                                uint16_t* __restrict__ dyp, int pad) {
+  const int C8 = C / 8;
+  const int hp = h + 2 * pad, wp = w + 2 * pad, rowlen = wp * C8;
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= rowlen) return;
+  const int xp = j / C8, c8 = j - xp * C8, xx = xp - pad;
+  const bool colin = xx >= 0 && xx < w;
+  float4 k0[2], k1[2], k2[2], mu[2];
+  if (colin) {
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int c = c8 * 8 + 4 * hh;
+      k0[hh] = ld4(coef + c); k1[hh] = ld4(coef + C + c); k2[hh] = ld4(coef + 2 * C + c);
+      mu[hh] = ld4(coef + 3 * C + c);
+    }
+  }
+  const int rows = n * hp;
+  for (int r0 = blockIdx.y; r0 < rows; r0 += 2 * gridDim.y) {
+    uint4 d[2], yv[2];
+    bool in[2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * gridDim.y;
+      const int nn = r / hp, yy = r - nn * hp - pad;
+      in[u] = r < rows && colin && yy >= 0 && yy < h;
+      d[u] = yv[u] = make_uint4(0u, 0u, 0u, 0u);
+      if (in[u]) {
+        const size_t src = ((((size_t)nn * h + yy) * w + xx) * C + c8 * 8) / 8;
+        d[u] = reinterpret_cast<const uint4*>(dz)[src];
+        yv[u] = reinterpret_cast<const uint4*>(yr)[src];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int r = r0 + u * gridDim.y;
+      if (r >= rows) continue;
+      uint4 o = make_uint4(0u, 0u, 0u, 0u);
+      if (in[u]) {
+        float4 res[2];
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const float4 dd = bf16x4_to_f4(hh ? make_uint2(d[u].z, d[u].w) : make_uint2(d[u].x, d[u].y));
+          const float4 y4 = bf16x4_to_f4(hh ? make_uint2(yv[u].z, yv[u].w) : make_uint2(yv[u].x, yv[u].y));
+          res[hh].x = fmaf(k0[hh].x, dd.x, fmaf(k1[hh].x, y4.x - mu[hh].x, k2[hh].x));
+          res[hh].y = fmaf(k0[hh].y, dd.y, fmaf(k1[hh].y, y4.y - mu[hh].y, k2[hh].y));
+          res[hh].z = fmaf(k0[hh].z, dd.z, fmaf(k1[hh].z, y4.z - mu[hh].z, k2[hh].z));
+          res[hh].w = fmaf(k0[hh].w, dd.w, fmaf(k1[hh].w, y4.w - mu[hh].w, k2[hh].w));
+        }
+        o = bf16pack8(res[0], res[1]);
+      }
+      reinterpret_cast<uint4*>(dyp)[(size_t)r * rowlen + j] = o;
+    }
+  }
+}
+
 hipError_t launch_bn_finalize(const double* stats, int c, double count, const float* gamma, const float* beta,
                               float* rmean, float* rvar, int64_t* nbt, float* mean, float* invstd, float* scale,
                               float* shift, float momentum, float eps, hipStream_t s) {
@@ -562,6 +622,14 @@ hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, 
   const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max<long long>(1, 32768 / gx))));
   if (dz_h16) {  // bf16 plans: dz, y and dYpad all bf16
     if (!out_h16 || !y_h16) return hipErrorInvalidValue;
+    if (c % 8 == 0) {
+      const long long rl8 = (long long)(w + 2 * pad) * (c / 8);
+      const int gx8 = (int)((rl8 + 255) / 256);
+      const dim3 g8(gx8, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max<long long>(1, 32768 / gx8))));
+      hipLaunchKernelGGL(k_bnb_apply_bf8, g8, dim3(256), 0, s, reinterpret_cast<const uint16_t*>(dz),
+                         reinterpret_cast<const uint16_t*>(y), coef, n, h, w, c, reinterpret_cast<uint16_t*>(dypad), pad);
+      return hipGetLastError();
+    }
     hipLaunchKernelGGL((k_bnb_apply<1, 1, 1>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad);
     return hipGetLastError();
   }
@@ -587,46 +655,68 @@ __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y,
                               uint16_t* __restrict__ anorm) {
   const int C = s.C, C4 = C / 4, ho = h / 2, wo = w / 2;
   const long long total = (long long)n * ho * wo * C4;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const int c4 = (int)(i % C4);
-    long long p = i / C4;
-    const int xo = (int)(p % wo);
-    p /= wo;
-    const int yo = (int)(p % ho);
-    const int nn = (int)(p / ho);
-    float4 v[4];
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  // U items per loop trip, every window load issued before any use
+  // (latency-bound otherwise: one HBM round trip per trip)
+  constexpr int U = 4;
+  for (long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x; i0 < total; i0 += U * stride) {
+    float4 v[U][4];
+    size_t sb0[U];  // window corner; element k at + ((k >> 1) W + (k & 1)) C
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int yy = 2 * yo + (k >> 1), xx = 2 * xo + (k & 1);
-      const size_t si = ((size_t)(nn * s.H + yy + s.oy) * s.W + xx + s.ox) * C + c4 * 4;
-      float4 t = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + si))
-                     : ld4(s.ptr + si);
+    for (int u = 0; u < U; ++u) {
+      const long long i = min(i0 + u * stride, total - 1);  // tail items recompute the last one (not stored)
+      const int c4 = (int)(i % C4);
+      long long p = i / C4;
+      const int xo = (int)(p % wo);
+      p /= wo;
+      const int yo = (int)(p % ho);
+      const int nn = (int)(p / ho);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int yy = 2 * yo + (k >> 1), xx = 2 * xo + (k & 1);
+        const size_t si = ((size_t)(nn * s.H + yy + s.oy) * s.W + xx + s.ox) * C + c4 * 4;
+        if (k == 0) sb0[u] = si;
+        v[u][k] = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + si))
+                      : ld4(s.ptr + si);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * stride;
+      if (i >= total) continue;
+      const int c4 = (int)(i % C4);
       if (s.scale) {
         const float4 a = ld4(s.scale + c4 * 4), b = ld4(s.shift + c4 * 4);
-        t.x = fmaxf(fmaf(t.x, a.x, b.x), 0.f);
-        t.y = fmaxf(fmaf(t.y, a.y, b.y), 0.f);
-        t.z = fmaxf(fmaf(t.z, a.z, b.z), 0.f);
-        t.w = fmaxf(fmaf(t.w, a.w, b.w), 0.f);
-      }
-      v[k] = t;
-      if (anorm)
-        *reinterpret_cast<uint2*>(anorm + si) = make_uint2(bf16pack(t.x, t.y), bf16pack(t.z, t.w));
-    }
-    float4 best = v[0];
-    uchar4 a = make_uchar4(0, 0, 0, 0);
 #pragma unroll
-    for (int k = 1; k < 4; ++k) {
-      if (v[k].x > best.x) { best.x = v[k].x; a.x = k; }
-      if (v[k].y > best.y) { best.y = v[k].y; a.y = k; }
-      if (v[k].z > best.z) { best.z = v[k].z; a.z = k; }
-      if (v[k].w > best.w) { best.w = v[k].w; a.w = k; }
+        for (int k = 0; k < 4; ++k) {
+          float4& t = v[u][k];
+          t.x = fmaxf(fmaf(t.x, a.x, b.x), 0.f);
+          t.y = fmaxf(fmaf(t.y, a.y, b.y), 0.f);
+          t.z = fmaxf(fmaf(t.z, a.z, b.z), 0.f);
+          t.w = fmaxf(fmaf(t.w, a.w, b.w), 0.f);
+        }
+      }
+      if (anorm) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          *reinterpret_cast<uint2*>(anorm + sb0[u] + ((size_t)(k >> 1) * s.W + (k & 1)) * C) =
+              make_uint2(bf16pack(v[u][k].x, v[u][k].y), bf16pack(v[u][k].z, v[u][k].w));
+      }
+      float4 best = v[u][0];
+      uchar4 am = make_uchar4(0, 0, 0, 0);
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        if (v[u][k].x > best.x) { best.x = v[u][k].x; am.x = k; }
+        if (v[u][k].y > best.y) { best.y = v[u][k].y; am.y = k; }
+        if (v[u][k].z > best.z) { best.z = v[u][k].z; am.z = k; }
+        if (v[u][k].w > best.w) { best.w = v[u][k].w; am.w = k; }
+      }
+      if (H16)
+        reinterpret_cast<uint2*>(y)[i] = make_uint2(bf16pack(best.x, best.y), bf16pack(best.z, best.w));
+      else
+        st4(y + i * 4, best);
+      *reinterpret_cast<uchar4*>(arg + i * 4) = am;
     }
-    if (H16)
-      reinterpret_cast<uint2*>(y)[i] = make_uint2(bf16pack(best.x, best.y), bf16pack(best.z, best.w));
-    else
-      st4(y + i * 4, best);
-    *reinterpret_cast<uchar4*>(arg + i * 4) = a;
   }
 }
 
@@ -682,7 +772,7 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
                                                            const float* scale, const float* shift,
                                                            const float* mean, const float* invstd, int n, int h,
                                                            int w, int C, float* __restrict__ dz,
-                                                           double* __restrict__ bstats) {
+                                                           double* __restrict__ bstats, int contig) {
   const int C4 = C / 4;            // channel groups; C4 divides 256 (C <= 1024, power of 2)
   const int tid = threadIdx.x;
   const int cg = tid % C4;
@@ -698,70 +788,88 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
   // together.  The row-pair index is the only division.
   const int xx = blockIdx.x * ppb + tid / C4;
   const int hq = (h + 1) / 2;
+  // U row pairs per loop trip, all their loads issued before any use: the
+  // kernel is latency-bound (one HBM round trip per trip), not bandwidth-bound
+  constexpr int U = 4;
   if (xx < w) {
     const int xo = xx >> 1;
     const bool in_skip_x = dskip && xx >= sox && xx < sox + sw;
-    for (int q = blockIdx.y; q < n * hq; q += gridDim.y) {
-      const int nn = q / hq, yo = q - nn * hq;
-      uchar4 a = make_uchar4(255, 255, 255, 255);
-      float4 g = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (yo < ho && xo < wo) {
-        const size_t pi = (((size_t)nn * ho + yo) * wo + xo) * C + c;
-        a = *reinterpret_cast<const uchar4*>(arg + pi);
-        g = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dpool) + pi))
-                : ld4(dpool + pi);
-      }
-      float4 d[2], yv[2];
+    const int nq = n * hq;
+    // contig: block y owns one run of consecutive row pairs; else strided by gridDim.y
+    const int per = (nq + gridDim.y - 1) / gridDim.y;
+    const int qb = contig ? blockIdx.y * per : blockIdx.y, qe = contig ? min(nq, qb + per) : nq;
+    const int qs = contig ? 1 : gridDim.y;
+    for (int q0 = qb; q0 < qe; q0 += U * qs) {
+      uchar4 a[U];
+      float4 g[U], d[U][2], yv[U][2];
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int yy = 2 * yo + k;
-        d[k] = make_float4(0.f, 0.f, 0.f, 0.f);
-        yv[k] = d[k];
-        if (yy >= h) continue;
-        if (in_skip_x && yy >= soy && yy < soy + sh)
-        {
-          const size_t si = (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c;
-          d[k] = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dskip) + si))
-                     : ld4(dskip + si);
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u * qs;
+        a[u] = make_uchar4(255, 255, 255, 255);
+        g[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+        d[u][0] = d[u][1] = yv[u][0] = yv[u][1] = g[u];
+        if (q >= qe) continue;
+        const int nn = q / hq, yo = q - nn * hq;
+        if (yo < ho && xo < wo) {
+          const size_t pi = (((size_t)nn * ho + yo) * wo + xo) * C + c;
+          a[u] = *reinterpret_cast<const uchar4*>(arg + pi);
+          g[u] = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dpool) + pi))
+                     : ld4(dpool + pi);
         }
-        const size_t oi = (((size_t)nn * h + yy) * w + xx) * C + c;
-        if (scale)
-          yv[k] = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
-                      : ld4(yr + oi);
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int yy = 2 * yo + k;
+          if (yy >= h) continue;
+          if (in_skip_x && yy >= soy && yy < soy + sh) {
+            const size_t si = (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c;
+            d[u][k] = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dskip) + si))
+                          : ld4(dskip + si);
+          }
+          const size_t oi = (((size_t)nn * h + yy) * w + xx) * C + c;
+          if (scale)
+            yv[u][k] = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
+                           : ld4(yr + oi);
+        }
       }
 #pragma unroll
-      for (int k = 0; k < 2; ++k) {
-        const int yy = 2 * yo + k;
-        if (yy >= h) continue;
-        const int sel = k * 2 + (xx & 1);  // window position of this pixel (argmax byte 255: not pooled)
-        float4 dd = d[k];
-        dd.x += (a.x == sel) ? g.x : 0.f;
-        dd.y += (a.y == sel) ? g.y : 0.f;
-        dd.z += (a.z == sel) ? g.z : 0.f;
-        dd.w += (a.w == sel) ? g.w : 0.f;
-        if (G16) {
-          dd.x = round_bf(dd.x);
-          dd.y = round_bf(dd.y);
-          dd.z = round_bf(dd.z);
-          dd.w = round_bf(dd.w);
+      for (int u = 0; u < U; ++u) {
+        const int q = q0 + u * qs;
+        if (q >= qe) continue;
+        const int nn = q / hq, yo = q - nn * hq;
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+          const int yy = 2 * yo + k;
+          if (yy >= h) continue;
+          const int sel = k * 2 + (xx & 1);  // window position of this pixel (argmax byte 255: not pooled)
+          float4 dd = d[u][k];
+          dd.x += (a[u].x == sel) ? g[u].x : 0.f;
+          dd.y += (a[u].y == sel) ? g[u].y : 0.f;
+          dd.z += (a[u].z == sel) ? g[u].z : 0.f;
+          dd.w += (a[u].w == sel) ? g[u].w : 0.f;
+          if (G16) {
+            dd.x = round_bf(dd.x);
+            dd.y = round_bf(dd.y);
+            dd.z = round_bf(dd.z);
+            dd.w = round_bf(dd.w);
+          }
+          if (scale) {
+            const float4 y4 = yv[u][k];
+            dd.x = (fmaf(y4.x, sc.x, sf.x) > 0.f) ? dd.x : 0.f;
+            dd.y = (fmaf(y4.y, sc.y, sf.y) > 0.f) ? dd.y : 0.f;
+            dd.z = (fmaf(y4.z, sc.z, sf.z) > 0.f) ? dd.z : 0.f;
+            dd.w = (fmaf(y4.w, sc.w, sf.w) > 0.f) ? dd.w : 0.f;
+            sa[0] += dd.x; sa[1] += dd.y; sa[2] += dd.z; sa[3] += dd.w;
+            sb[0] += dd.x * (y4.x - mu.x) * is.x;
+            sb[1] += dd.y * (y4.y - mu.y) * is.y;
+            sb[2] += dd.z * (y4.z - mu.z) * is.z;
+            sb[3] += dd.w * (y4.w - mu.w) * is.w;
+          }
+          const size_t oi = (((size_t)nn * h + yy) * w + xx) * C + c;
+          if (G16)
+            reinterpret_cast<uint2*>(dz)[oi / 4] = make_uint2(bf16pack(dd.x, dd.y), bf16pack(dd.z, dd.w));
+          else
+            st4(dz + oi, dd);
         }
-        if (scale) {
-          const float4 y4 = yv[k];
-          dd.x = (fmaf(y4.x, sc.x, sf.x) > 0.f) ? dd.x : 0.f;
-          dd.y = (fmaf(y4.y, sc.y, sf.y) > 0.f) ? dd.y : 0.f;
-          dd.z = (fmaf(y4.z, sc.z, sf.z) > 0.f) ? dd.z : 0.f;
-          dd.w = (fmaf(y4.w, sc.w, sf.w) > 0.f) ? dd.w : 0.f;
-          sa[0] += dd.x; sa[1] += dd.y; sa[2] += dd.z; sa[3] += dd.w;
-          sb[0] += dd.x * (y4.x - mu.x) * is.x;
-          sb[1] += dd.y * (y4.y - mu.y) * is.y;
-          sb[2] += dd.z * (y4.z - mu.z) * is.z;
-          sb[3] += dd.w * (y4.w - mu.w) * is.w;
-        }
-        const size_t oi = (((size_t)nn * h + yy) * w + xx) * C + c;
-        if (G16)
-          reinterpret_cast<uint2*>(dz)[oi / 4] = make_uint2(bf16pack(dd.x, dd.y), bf16pack(dd.z, dd.w));
-        else
-          st4(dz + oi, dd);
       }
     }
   }
@@ -784,17 +892,19 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
   // those, not the HBM streams, set this kernel's time at larger grids (measured
   // per step at 512^2 x 8: 256 blocks 1.14 ms, 512 0.73, 1024 0.54, 2048 0.71,
   // 4096 0.80, 16384 1.28)
-  const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max(1, 1024 / gx))));
+  static const int target = getenv("UNET_MPB_BLOCKS") ? atoi(getenv("UNET_MPB_BLOCKS")) : 1024;
+  static const int contig = getenv("UNET_MPB_CONTIG") ? atoi(getenv("UNET_MPB_CONTIG")) : 0;
+  const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max(1, target / gx))));
   if (g_h16) {
     if (!y_h16) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_maxpool_bwd_fused<1, 1>), grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
-                       shift, mean, invstd, n, h, w, c, dz, bstats);
+                       shift, mean, invstd, n, h, w, c, dz, bstats, contig);
   } else if (y_h16)
     hipLaunchKernelGGL(k_maxpool_bwd_fused<1>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
-                       shift, mean, invstd, n, h, w, c, dz, bstats);
+                       shift, mean, invstd, n, h, w, c, dz, bstats, contig);
   else
     hipLaunchKernelGGL(k_maxpool_bwd_fused<0>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
-                       shift, mean, invstd, n, h, w, c, dz, bstats);
+                       shift, mean, invstd, n, h, w, c, dz, bstats, contig);
   return hipGetLastError();
 }
 

@@ -299,6 +299,63 @@ __device__ __forceinline__ void epi_fast(const Epilogue& e, const floatx16 (&acc
   }
 }
 
+// Pixel-shuffle epilogue of the ConvTranspose2d(k2, s2) GEMM (rows = input
+// pixels of the linear grid, column ab * Co + co -> output pixel (2y + a, 2x + b),
+// channel co): the destination base of each accumulator row is computed once
+// per fragment row (one pixel decomposition per block, then increments) and a
+// 32-column block is one (a, b) sub-pixel, so an element costs an add and its
+// store.  (The generic path decomposes every element's pixel: two integer
+// divisions per element dominated the convT forward.)
+template <int TM, int TN, int H16>
+__device__ __forceinline__ void epi_shuffle(const Epilogue& e, const floatx16 (&acc)[TM][TN], const LinearRows& rows,
+                                            const Gather& g, int n0, int wm, int wn, int h, int li) {
+  const Dst& d = e.d[0];
+  const unsigned Co = (unsigned)e.shuffle_co, W2 = (unsigned)d.W, H2 = (unsigned)d.H;
+  const int Wg = g.Wg, Hg = g.Hg;
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int mb, lim;
+    rows.block(wm * TM + i, h, mb, lim);
+    if (lim <= 0) continue;
+    int nn = mb / (Hg * Wg);
+    const int rr = mb - nn * Hg * Wg;
+    int y = rr / Wg, x = rr - y * Wg;
+    unsigned base[16];
+    int kprev = 0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int k = (r & 3) + 8 * (r >> 2);
+      x += k - kprev;
+      kprev = k;
+      while (x >= Wg) {  // at most (27 / Wg) + 1 wraps
+        x -= Wg;
+        if (++y == Hg) {
+          y = 0;
+          ++nn;
+        }
+      }
+      base[r] = (((unsigned)nn * H2 + 2u * y) * W2 + 2u * x) * Co;
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = n0 + wn * TN * 32 + j * 32 + li;
+      const unsigned ab = (unsigned)col / Co, co = (unsigned)col - ab * Co;  // ab uniform per 32 columns
+      const unsigned off = ((ab >> 1) * W2 + (ab & 1)) * Co + co;
+      const float bias = e.bias ? e.bias[co] : 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        if ((r & 3) + 8 * (r >> 2) >= lim) continue;
+        float v = acc[i][j][r] + bias;
+        if (e.relu) v = fmaxf(v, 0.f);
+        if constexpr (H16)
+          reinterpret_cast<uint16_t*>(d.ptr)[base[r] + off] = (uint16_t)bf16_of(v);
+        else
+          d.ptr[base[r] + off] = v;
+      }
+    }
+  }
+}
+
 // Split-K partial store or the full epilogue of an implicit-GEMM tile: bias,
 // destination mapping (linear / pixel shuffle / cropped), ReLU mask + BN-bwd
 // statistics, BN statistics, concat column sums.  `red` is WM*3*BN floats of
@@ -344,6 +401,16 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
   // plus a compile-time multiple of the (uniform) channel count: a handful of
   // VALU per element instead of a per-element pixel decomposition -- the
   // epilogue is a large share of the small-K (64 / 128-channel) GEMMs.
+  if constexpr (std::is_same<RowMap, LinearRows>::value) {
+    const Dst& d = e.d[0];
+    if (e.shuffle_co && e.shuffle_co % 32 == 0 && e.n_split >= N && !e.stats && !e.yref && !e.colsum1 &&
+        d.C == e.shuffle_co && d.oy == 0 && d.ox == 0 && d.H == 2 * g.Hg && d.W == 2 * g.Wg &&
+        (size_t)args.M * 4 * d.C < (1ull << 32)) {
+      if (d.h16) epi_shuffle<TM, TN, 1>(e, acc, rows, g, n0, wm, wn, h, li);
+      else epi_shuffle<TM, TN, 0>(e, acc, rows, g, n0, wm, wn, h, li);
+      return;
+    }
+  }
   if constexpr (fast_rows<RowMap>::value) {
     auto lin = [&](const Dst& d) { return d.oy == 0 && d.ox == 0 && d.H == g.Hg && d.W == g.Wg; };
     const bool two = e.n_split < N;

@@ -1229,6 +1229,232 @@ hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_c
 }
 
 // ---------------------------------------------------------------------------
+// k_wgrad3w_bf: k_wgrad3_bf with a wider workgroup tile and a two-stage ring
+// (wgrad tiles 24: 128 co x 64 ci, 25: 64 co x 128 ci; bf16-stored dY and X).
+// k_wgrad3_bf's waves hold 32 co x 32 ci x 5 taps: per 16-pixel k step 12
+// transposed LDS reads feed 5 MFMAs, which saturates the LDS (~150 B/clk per CU
+// at full MFMA rate against 128) -- and with one staging buffer the next
+// tile's loads land before a ~1 us compute phase is over, so the barrier-bound
+// loop exposes their latency (measured: without its MFMAs the kernel still
+// takes ~70 % of its time).  Here a wave holds 64 co x 32 ci x 5 taps (160
+// accumulator registers, one workgroup of 8 waves per CU): 14 transposed reads
+// feed 10 MFMAs (~90 B/clk), and tile t+1 is loaded while tile t is multiplied
+// and committed into the other buffer: one barrier per tile.
+// LDS rows: [pixel][channels] bf16, 128 B (64 channels; 16-B chunk c stored at
+// c ^ (((row >> 1) & 1) << 2), as k_wgrad3_bf) or 256 B (128 channels; the
+// 64-B segment s of row r at s ^ (r & 3)): the 4 rows x 64 B a 32-lane half of
+// a transposed read covers fall in 4 distinct 64-B bank groups either way.
+// ---------------------------------------------------------------------------
+template <int RB>  // row bytes 128 or 256
+__device__ __forceinline__ int wgw_chunk(int row, int c) {
+  if constexpr (RB == 128) return c ^ (((row >> 1) & 1) << 2);
+  else return (((c >> 2) ^ (row & 3)) << 2) | (c & 3);
+}
+
+template <int BCO, int BCI>
+constexpr size_t wgrad3w_smem() {
+  return 2 * (size_t)(128 * BCO + 180 * BCI) * 2 + 2 * BCI * 4;  // 2 stages of (dY 8x16 px, X 10x18 halo) + scale/shift
+}
+
+template <int BCO, int BCI>
+__global__ __launch_bounds__(512, 1) void k_wgrad3w_bf(const WgradArgs args, int gx, int gy) {
+  constexpr int NT = 512, TH = 8, TW = 16, NTAP = 5;
+  constexpr int PT = TH * TW, HW2 = TW + 2, PH = (TH + 2) * HW2;
+  constexpr int RA = BCO * 2, RBX = BCI * 2;                // LDS row bytes
+  constexpr int CA = BCO / 8, CB = BCI / 8;                 // 16-B chunks per row
+  constexpr int UA = PT * CA, UB = PH * CB;                 // 16-B staging units per tile
+  constexpr int NA = UA / NT, NB = (UB + NT - 1) / NT;
+  constexpr int WCO = BCO / 64, WCI = BCI / 32;
+  static_assert(UA % NT == 0 && WCO * WCI * 2 == 8, "8 waves: co groups x ci groups x 2 tap groups");
+  constexpr int STAGE = PT * RA + PH * RBX;
+  extern __shared__ __attribute__((aligned(16))) unsigned char wsm[];
+  float* ssc = reinterpret_cast<float*>(wsm + 2 * STAGE);  // [2][BCI]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // workgroups of one pixel-tile set (same z) share the dY / X tiles: keep
+  // them on one XCD (consecutive dispatch ids go round-robin over the 8 XCDs)
+  long long bid = blockIdx.x;
+  const long long G = gridDim.x;
+  if ((G & 7) == 0) bid = (bid & 7) * (G >> 3) + (bid >> 3);
+  const int bx = (int)(bid % gx), by = (int)((bid / gx) % gy), bz = (int)(bid / ((long long)gx * gy));
+  const int splits = (int)(G / ((long long)gx * gy));
+  const Gather& gb = args.gb;
+  const Src& ds = args.ga.s[0];
+  const int i0 = bx * BCO, cb = by * BCI;
+  const int Hg = gb.Hg, Wg = gb.Wg, Ci = gb.Cg;
+  const bool second = cb >= gb.c_split;  // a BCI-channel block never straddles the concat split
+  const Src& xs = second ? gb.s[1] : gb.s[0];
+  const int xc = second ? cb - gb.c_split : cb;
+  const bool xtf = xs.scale != nullptr;
+  if (xtf)
+    for (int c = tid; c < BCI; c += NT) {
+      ssc[c] = xs.scale[xc + c];
+      ssc[BCI + c] = xs.shift[xc + c];
+    }
+  const int tiles_x = (Wg + TW - 1) / TW, tiles_y = (Hg + TH - 1) / TH;
+  const int tiles = gb.nimg * tiles_x * tiles_y;
+
+  uint4 ra[NA], rx[NB];
+  unsigned dvalid = 0;
+  auto issue = [&](int t) {
+    const int x0 = (t % tiles_x) * TW;
+    const int r = t / tiles_x;
+    const int y0 = (r % tiles_y) * TH, n = r / tiles_y;
+    dvalid = 0;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      const int p = u / CA, ch = u % CA;
+      const int y = y0 + p / TW, x = x0 + p % TW;
+      dvalid |= (y < Hg && x < Wg) ? (1u << k) : 0u;
+      const int yy = min(y, Hg - 1), xx = min(x, Wg - 1);
+      const size_t e = (size_t)((n * ds.H + yy + ds.oy) * ds.W + xx + ds.ox) * ds.C + i0 + ch * 8;
+      ra[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(ds.ptr) + e);
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int u = min(tid + k * NT, UB - 1);
+      const int hp = u / CB, ch = u % CB;
+      const int yy = min(y0 + hp / HW2, Hg + 1), xx = min(x0 + hp % HW2, Wg + 1);
+      const size_t e = (size_t)((n * xs.H + yy + xs.oy) * xs.W + xx + xs.ox) * xs.C + xc + ch * 8;
+      rx[k] = *reinterpret_cast<const uint4*>(reinterpret_cast<const uint16_t*>(xs.ptr) + e);
+    }
+  };
+  auto commit = [&](int b) {
+    unsigned char* Ad = wsm + b * STAGE;
+    unsigned char* Bx = Ad + PT * RA;
+#pragma unroll
+    for (int k = 0; k < NA; ++k) {
+      const int u = tid + k * NT;
+      const int p = u / CA, ch = u % CA;
+      const uint4 o = ((dvalid >> k) & 1) ? ra[k] : make_uint4(0u, 0u, 0u, 0u);  // pixels past the grid add nothing
+      *reinterpret_cast<uint4*>(Ad + p * RA + wgw_chunk<RA>(p, ch) * 16) = o;
+    }
+#pragma unroll
+    for (int k = 0; k < NB; ++k) {
+      const int u = tid + k * NT;
+      if (u < UB) {
+        const int hp = u / CB, ch = u % CB;
+        uint4 o = rx[k];
+        if (xtf) {
+          const float4 r0 = affine_relu4(bf16x4_to_f4(make_uint2(o.x, o.y)), ld4(ssc + ch * 8), ld4(ssc + BCI + ch * 8));
+          const float4 r1 =
+              affine_relu4(bf16x4_to_f4(make_uint2(o.z, o.w)), ld4(ssc + ch * 8 + 4), ld4(ssc + BCI + ch * 8 + 4));
+          o = bf16pack8(r0, r1);
+        }
+        *reinterpret_cast<uint4*>(Bx + hp * RBX + wgw_chunk<RBX>(hp, ch) * 16) = o;
+      }
+    }
+  };
+
+  floatx16 acc[2][NTAP];
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int t = 0; t < NTAP; ++t)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[f][t][r] = 0.f;
+
+  // transposed-read lane roles (k_wgrad3_bf): group g16 = lane >> 4 reads channel
+  // half (g16 & 1) of k half (g16 >> 1); lane 4q + p of the group addresses
+  // pixel row q, channels 4p .. 4p+3
+  const int g16 = lane >> 4, q = (lane & 15) >> 2, pp = lane & 3;
+  const int hk = g16 >> 1;
+  const int wco = wave % WCO, wci = (wave / WCO) % WCI, tg = wave / (WCO * WCI);
+  const int tap0 = tg * NTAP, ntap = tg ? 9 - NTAP : NTAP;  // wave-uniform
+  const int colA = wco * 64 + (g16 & 1) * 16 + pp * 4, colB = wci * 32 + (g16 & 1) * 16 + pp * 4;
+  auto compute = [&](int b) {
+    const unsigned char* Ad = wsm + b * STAGE;
+    const unsigned char* Bx = Ad + PT * RA;
+#pragma unroll 2
+    for (int ks = 0; ks < PT / 16; ++ks) {
+      auto frag = [&](const unsigned char* base, int rb, int r, int col) {
+        const int c = col >> 3, bo = (col & 7) * 2;
+        const bf16x4_t lo = tr_read(base + r * rb + (rb == 128 ? wgw_chunk<128>(r, c) : wgw_chunk<256>(r, c)) * 16 + bo);
+        const bf16x4_t hi =
+            tr_read(base + (r + 4) * rb + (rb == 128 ? wgw_chunk<128>(r + 4, c) : wgw_chunk<256>(r + 4, c)) * 16 + bo);
+        return (bf16x8_t)__builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7);
+      };
+      const int pa = ks * 16 + 8 * hk + q;
+      const bf16x8_t fa0 = frag(Ad, RA, pa, colA), fa1 = frag(Ad, RA, pa, colA + 32);
+      const int prow = ks, px0 = 0;  // TW = 16: one tile row per k step
+#pragma unroll
+      for (int j = 0; j < NTAP; ++j) {
+        if (j < ntap) {
+          const int tap = tap0 + j;
+          const int hb = (prow + tap / 3) * HW2 + px0 + tap % 3 + 8 * hk + q;
+          const bf16x8_t fb = frag(Bx, RBX, hb, colB);
+          acc[0][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa0, fb, acc[0][j], 0, 0, 0);
+          acc[1][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa1, fb, acc[1][j], 0, 0, 0);
+        }
+      }
+    }
+  };
+
+  if (xtf) __syncthreads();  // scale/shift table before the first commit
+  int t = bz, b = 0;
+  if (t < tiles) {
+    issue(t);
+    commit(0);
+  }
+  __syncthreads();
+  for (; t < tiles; t += splits) {
+    const bool more = t + splits < tiles;
+    if (more && !(args.abl & 4)) issue(t + splits);
+    if (!(args.abl & 2)) compute(b);
+    if (more) commit(b ^ 1);  // its last reader (compute of the previous tile) passed the last barrier
+    __syncthreads();
+    b ^= 1;
+  }
+  // accumulate into out[co][tap * Ci + ci] (fp32 atomics, one per element per workgroup)
+  const int h = lane >> 5, li = lane & 31;
+#pragma unroll
+  for (int f = 0; f < 2; ++f)
+#pragma unroll
+    for (int j = 0; j < NTAP; ++j) {
+      if (j < ntap) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int row = i0 + wco * 64 + 32 * f + (r & 3) + 8 * (r >> 2) + 4 * h;
+          const int col = (tap0 + j) * Ci + cb + wci * 32 + li;
+          if (args.abl & 1) args.out[(size_t)row * args.No + col] = acc[f][j][r];
+          else atomicAdd(args.out + (size_t)row * args.No + col, acc[f][j][r]);
+        }
+      }
+    }
+}
+
+bool wgrad3w_fits(const WgradArgs& a, int tile) {
+  const int bco = tile == 24 ? 128 : 64, bci = tile == 24 ? 64 : 128;
+  const Gather& g = a.gb;
+  const bool two = g.c_split < g.Cg;
+  return (tile == 24 || tile == 25) && wgrad3_fits(a) && !a.split && a.ga.s[0].h16 && g.s[0].h16 &&
+         (!two || g.s[1].h16) && a.Mo % bco == 0 && g.Cg % bci == 0 && (!two || g.c_split % bci == 0);
+}
+
+template <int BCO, int BCI>
+static hipError_t go_wgrad3w(const WgradArgs& a, hipStream_t s, int per_cu) {
+  static bool attr = false;
+  const size_t smem = wgrad3w_smem<BCO, BCI>();
+  hipError_t e = allow_smem(reinterpret_cast<const void*>(&k_wgrad3w_bf<BCO, BCI>), smem, attr);
+  if (e != hipSuccess) return e;
+  const int tiles = a.gb.nimg * ((a.gb.Hg + 7) / 8) * ((a.gb.Wg + 15) / 16);
+  const int gx = a.Mo / BCO, gy = a.gb.Cg / BCI, blocks = gx * gy;
+  int splits = (per_cu * num_cus() + blocks - 1) / blocks;
+  splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
+  static const int abl = getenv("UNET_WG_ABL") ? atoi(getenv("UNET_WG_ABL")) : 0;
+  WgradArgs b = a;
+  b.abl = abl;
+  hipLaunchKernelGGL((k_wgrad3w_bf<BCO, BCI>), dim3((unsigned)(blocks * splits)), dim3(512), smem, s, b, gx, gy);
+  return hipGetLastError();
+}
+
+hipError_t go_wgrad3w_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu) {
+  if (!wgrad3w_fits(a, tile)) return hipErrorInvalidValue;
+  return tile == 24 ? go_wgrad3w<128, 64>(a, s, per_cu) : go_wgrad3w<64, 128>(a, s, per_cu);
+}
+
+// ---------------------------------------------------------------------------
 // fp32 -> bf16 (RNE) of the packed weight region, 4 elements per lane-step;
 // with `lo` also the residual plane bf16(v - bf16(v)) of split operands
 // ---------------------------------------------------------------------------

@@ -179,6 +179,18 @@ int unet_conv3x3_wgrad(const float* x, const float* dy, int n, int h, int w, int
   a.out = dwp;
   a.bf16 = g_op_prec != UNET_PREC_FP32;
   a.split = g_op_prec == UNET_PREC_BF16X3;
+  if (g_op_prec == UNET_PREC_BF16 && g_op_a16) {  // bf16-stored dY and X, as in a bf16 plan
+    uint16_t* dy16 = reinterpret_cast<uint16_t*>(p + 2 * wb);  // the (unused) padded-dY region
+    uint16_t* x16 = reinterpret_cast<uint16_t*>(p + 2 * wb + al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co) +
+                                                al256(sizeof(float) * 4 * co) +
+                                                al256(sizeof(double) * kStatGroups * 2 * co));
+    OPCK(launch_f2bf(dy, dy16, (size_t)n * (h - 2) * (w - 2) * co, s));
+    OPCK(launch_f2bf(x, x16, (size_t)n * h * w * ci, s));
+    a.ga.s[0].ptr = a.ga.s[1].ptr = reinterpret_cast<const float*>(dy16);
+    a.ga.s[0].h16 = a.ga.s[1].h16 = 1;
+    a.gb.s[0].ptr = a.gb.s[1].ptr = reinterpret_cast<const float*>(x16);
+    a.gb.s[0].h16 = a.gb.s[1].h16 = 1;
+  }
   OPCK(launch_wgrad(a, s));
   OPCK(launch_permute_last2(dwp, co, 9, ci, dw, s));
   if (db) {

@@ -173,6 +173,9 @@ hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid)
 // halo-tiled 3x3 weight gradient (wgrad tiles 20, 21): all 9 taps per workgroup
 bool wgrad3_fits(const WgradArgs& a);
 hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
+// wide halo-tiled 3x3 weight gradient with a two-stage ring (wgrad tiles 24, 25)
+bool wgrad3w_fits(const WgradArgs& a, int tile);
+hipError_t go_wgrad3w_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
 // tiles 21-26 / 31-36 / 41-44 that have a split-operand kernel
 bool bf16_tile_splits(int tile);
 // out[i] = bf16(in[i]) (RNE), n a multiple of 4, in 16-B / out 8-B aligned;

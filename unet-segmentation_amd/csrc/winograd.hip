@@ -1202,6 +1202,10 @@ __global__ void k_wino4f_w8(const float* __restrict__ b, int N, int Cg, float* _
   }
 }
 
+// ABL: timing ablations (UNET_WF64_ABL; results wrong with any bit set): 1 = no
+// BatchNorm / transform arithmetic, 2 = no MFMA, 4 = no operand loads after the
+// first chunk, 8 = no output stage
+template <int ABL>
 __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __restrict__ V, int N, long long T,
                                                      int Th, int Tw, int NB, Epilogue e) {
   constexpr int PU = 32 * 8 + 8;  // U point plane (+8: the two lane rows of a patch store 18 planes apart)
@@ -1274,6 +1278,12 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
     const float* scp = second ? g.s[1].scale : g.s[0].scale;
     const float* shp = second ? g.s[1].shift : g.s[0].shift;
     const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    if constexpr (ABL & 1) {
+#pragma unroll
+      for (int a = 0; a < 3; ++a)
+#pragma unroll
+        for (int bb = 0; bb < 6; ++bb) ubase[(a * 6 + bb) * PU] = raw[a * 6 + bb];
+    } else {
     if (scp) {
       const float sc = scp[cl], sh = shp[cl];
 #pragma unroll
@@ -1312,6 +1322,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
 #pragma unroll
       for (int bb = 0; bb < 6; ++bb) ubase[(a * 6 + bb) * PU] = rr[bb];
     }
+    }
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       const int q = tid + 512 * j;
@@ -1333,7 +1344,8 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
   for (int kc = 0; kc < nk; ++kc) {
     commit(kc);
     __syncthreads();
-    if (kc + 1 < nk) load(kc + 1);
+    if (!(ABL & 4) && kc + 1 < nk) load(kc + 1);
+    if constexpr (!(ABL & 2))
 #pragma unroll
     for (int j = 0; j < 9; ++j) {
       const int p = pg * 9 + j;
@@ -1350,6 +1362,10 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
   }
 
   // ---- two 32-channel passes: accumulators -> X[36][32][32] -> wf_output ----
+  if constexpr (ABL & 8) {
+    if (acc[0][0][0] == 1.2345f) e.d[0].ptr[tid] = acc[8][3][3];  // keep the accumulators live
+    return;
+  }
   float* X = lds;
 #pragma unroll
   for (int hh = 0; hh < 2; ++hh) {
@@ -1380,7 +1396,14 @@ hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s) {
   const int NB = a.N / 64;
   const long long G = (T + 31) / 32 * NB;
   hipLaunchKernelGGL(k_wino4f_w8, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
-  hipLaunchKernelGGL(k_wino4f64, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  static const int abl = getenv("UNET_WF64_ABL") ? atoi(getenv("UNET_WF64_ABL")) : 0;
+  switch (abl) {
+#define WF64(A) \
+  case A: hipLaunchKernelGGL(k_wino4f64<A>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;
+    WF64(1) WF64(2) WF64(4) WF64(8) WF64(6) WF64(3)
+#undef WF64
+    default: hipLaunchKernelGGL(k_wino4f64<0>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  }
   return hipGetLastError();
 }
 
