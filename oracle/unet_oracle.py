@@ -97,6 +97,12 @@ def bn_cancelled(name: str) -> bool:
     return name.endswith(("double_conv.0.bias", "double_conv.3.bias", ".up.bias"))
 
 
+def is_bn_param(name: str) -> bool:
+    """BatchNorm2d affine parameters (weight / bias of double_conv.1 and .4)."""
+    return name.endswith(("double_conv.1.weight", "double_conv.1.bias", "double_conv.4.weight",
+                          "double_conv.4.bias"))
+
+
 def is_buffer(name: str) -> bool:
     return name.endswith(("running_mean", "running_var", "num_batches_tracked"))
 

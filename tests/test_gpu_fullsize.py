@@ -93,8 +93,13 @@ def check_bf16_vs_reference(z, zb, lg, loss, grads, tag):
             continue
         floor = abs(float(zb[f"gbf16norm/{name}"]) - r)
         # the GPU result carries its own bf16 rounding pattern (fp32 sums, tuned
-        # tile mix) on top of the one the bf16 oracle measures: within 3 floors
-        tol = max(1e-2 * r, 3 * floor)
+        # tile mix) on top of the one the bf16 oracle measures: within 3 floors.
+        # BatchNorm affine gradients are sums over 0.1-2 M bf16-stored BN-input
+        # gradients with heavy cancellation: two fp32-summing bf16 runs with
+        # different (timing-tuned) kernel mixes differed by up to 1.7 % on them
+        # (GPUTEST runs g9 / g10 of round 3), so their relative bar is 2 %
+        rel = 2e-2 if O.is_bn_param(name) else 1e-2
+        tol = max(rel * r, 3 * floor)
         e = abs(np.linalg.norm(g) - r)
         worst = max(worst, e / tol)
         assert e <= tol, (tag, name, np.linalg.norm(g), r, floor)

@@ -559,6 +559,8 @@ __global__ void k_bnb_apply_bf8(const uint16_t* __restrict__ dz, const uint16_t*
     bool in[2];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
+      // (predicated loads: a branch-free clamped form measured slower here,
+      // 0.61 -> 0.67 ms per step, as did one for the fp32 twin)
       const int r = r0 + u * gridDim.y;
       const int nn = r / hp, yy = r - nn * hp - pad;
       in[u] = r < rows && colin && yy >= 0 && yy < h;
@@ -772,7 +774,7 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
                                                            const float* scale, const float* shift,
                                                            const float* mean, const float* invstd, int n, int h,
                                                            int w, int C, float* __restrict__ dz,
-                                                           double* __restrict__ bstats, int contig) {
+                                                           double* __restrict__ bstats) {
   const int C4 = C / 4;            // channel groups; C4 divides 256 (C <= 1024, power of 2)
   const int tid = threadIdx.x;
   const int cg = tid % C4;
@@ -795,40 +797,40 @@ __global__ __launch_bounds__(256) void k_maxpool_bwd_fused(const float* __restri
     const int xo = xx >> 1;
     const bool in_skip_x = dskip && xx >= sox && xx < sox + sw;
     const int nq = n * hq;
-    // contig: block y owns one run of consecutive row pairs; else strided by gridDim.y
-    const int per = (nq + gridDim.y - 1) / gridDim.y;
-    const int qb = contig ? blockIdx.y * per : blockIdx.y, qe = contig ? min(nq, qb + per) : nq;
-    const int qs = contig ? 1 : gridDim.y;
-    for (int q0 = qb; q0 < qe; q0 += U * qs) {
+    const int qe = nq, qs = gridDim.y;  // row pairs strided over the grid's y (a contiguous run per block measured the same)
+    for (int q0 = blockIdx.y; q0 < qe; q0 += U * qs) {
+      // Branch-free loads from clamped addresses, validity applied afterwards:
+      // a load inside a conditional region gets its own s_waitcnt at the
+      // region's end, which serialised every load of the trip.
       uchar4 a[U];
       float4 g[U], d[U][2], yv[U][2];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        const int q = q0 + u * qs;
-        a[u] = make_uchar4(255, 255, 255, 255);
-        g[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-        d[u][0] = d[u][1] = yv[u][0] = yv[u][1] = g[u];
-        if (q >= qe) continue;
+        const int q = min(q0 + u * qs, qe - 1);
         const int nn = q / hq, yo = q - nn * hq;
-        if (yo < ho && xo < wo) {
-          const size_t pi = (((size_t)nn * ho + yo) * wo + xo) * C + c;
-          a[u] = *reinterpret_cast<const uchar4*>(arg + pi);
-          g[u] = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dpool) + pi))
-                     : ld4(dpool + pi);
-        }
+        const bool pin = yo < ho && xo < wo;
+        const size_t pi = (((size_t)nn * ho + min(yo, ho - 1)) * wo + min(xo, wo - 1)) * C + c;
+        const uchar4 av = *reinterpret_cast<const uchar4*>(arg + pi);
+        const float4 gv = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dpool) + pi))
+                              : ld4(dpool + pi);
+        a[u] = pin ? av : make_uchar4(255, 255, 255, 255);
+        g[u] = pin ? gv : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
-          const int yy = 2 * yo + k;
-          if (yy >= h) continue;
-          if (in_skip_x && yy >= soy && yy < soy + sh) {
-            const size_t si = (((size_t)nn * sh + yy - soy) * sw + xx - sox) * C + c;
-            d[u][k] = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dskip) + si))
-                          : ld4(dskip + si);
-          }
-          const size_t oi = (((size_t)nn * h + yy) * w + xx) * C + c;
-          if (scale)
-            yv[u][k] = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yr) + oi))
-                           : ld4(yr + oi);
+          const int yy = min(2 * yo + k, h - 1);
+          const bool sin = in_skip_x && yy >= soy && yy < soy + sh;
+          const int sy = min(max(yy - soy, 0), sh - 1), sx = in_skip_x ? xx - sox : 0;
+          // absent operands read element 0 of the pooled gradient instead (no branch)
+          const float* dsp = dskip ? dskip : dpool;
+          const size_t si = dskip ? (((size_t)nn * sh + sy) * sw + sx) * C + c : 0;
+          const float4 dv = G16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(dsp) + si))
+                                : ld4(dsp + si);
+          d[u][k] = sin ? dv : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float* yp = scale ? yr : dpool;
+          const size_t oi = scale ? (((size_t)nn * h + yy) * w + xx) * C + c : 0;
+          const bool y16 = scale ? Y16 != 0 : G16 != 0;
+          yv[u][k] = y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(yp) + oi))
+                         : ld4(yp + oi);
         }
       }
 #pragma unroll
@@ -888,23 +890,21 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
   if ((long long)n * h * w >= (1LL << 31)) return hipErrorInvalidValue;
   const int ppb = 256 / (c / 4);
   const int gx = (w + ppb - 1) / ppb;
-  // ~1024 blocks in all: every block ends in 2*C fp64 BN-statistics atomics, and
-  // those, not the HBM streams, set this kernel's time at larger grids (measured
-  // per step at 512^2 x 8: 256 blocks 1.14 ms, 512 0.73, 1024 0.54, 2048 0.71,
-  // 4096 0.80, 16384 1.28)
-  static const int target = getenv("UNET_MPB_BLOCKS") ? atoi(getenv("UNET_MPB_BLOCKS")) : 1024;
-  static const int contig = getenv("UNET_MPB_CONTIG") ? atoi(getenv("UNET_MPB_CONTIG")) : 0;
-  const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max(1, target / gx))));
+  // ~1024 blocks in all (per step at 512^2 x 8 with the branch-free batched
+  // loads, bf16: 1024 blocks 0.32 ms; 512 and 4096 and a contiguous run of row
+  // pairs per block measured slower or the same; before, each predicated load
+  // waited out its own round trip: 0.51-0.56 ms)
+  const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max(1, 1024 / gx))));
   if (g_h16) {
     if (!y_h16) return hipErrorInvalidValue;
     hipLaunchKernelGGL((k_maxpool_bwd_fused<1, 1>), grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
-                       shift, mean, invstd, n, h, w, c, dz, bstats, contig);
+                       shift, mean, invstd, n, h, w, c, dz, bstats);
   } else if (y_h16)
     hipLaunchKernelGGL(k_maxpool_bwd_fused<1>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
-                       shift, mean, invstd, n, h, w, c, dz, bstats, contig);
+                       shift, mean, invstd, n, h, w, c, dz, bstats);
   else
     hipLaunchKernelGGL(k_maxpool_bwd_fused<0>, grid, dim3(256), 0, s, dpool, arg, dskip, soy, sox, sh, sw, y, scale,
-                       shift, mean, invstd, n, h, w, c, dz, bstats, contig);
+                       shift, mean, invstd, n, h, w, c, dz, bstats);
   return hipGetLastError();
 }
 
@@ -960,14 +960,14 @@ __global__ __launch_bounds__(256) void k_head_fwd(Src s, int n, int h, int w, co
 }
 
 // head backward: dz = W^T dl masked by ReLU'(bn(y)) (+ BN-bwd stats), dW, db.
-template <int K>  // class capacity; kn <= K classes (as k_head_fwd)
+template <int K, int Y16>  // class capacity (kn <= K classes, as k_head_fwd); Y16: y stored bf16
 __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict__ dl, int n, int h, int w,
                                                   const float* __restrict__ wt, const float* __restrict__ mean,
                                                   const float* __restrict__ invstd, float* __restrict__ dz,
                                                   double* __restrict__ bstats, double* __restrict__ acc_out,
                                                   int dz16, int kn) {
   const int tid = threadIdx.x, sub = tid & 15;
-  const long long pixels = (long long)n * h * w;
+  const int pixels = n * h * w;  // < 2^31 (launch_head_bwd)
   const int c = sub * 4;
   float4 wk[K];
 #pragma unroll
@@ -981,50 +981,69 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
     for (int j = 0; j < 4; ++j) dwa[k][j] = 0.f;
   }
   float sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
-  const long long hw = (long long)h * w;
-  for (long long p = (long long)blockIdx.x * 16 + (tid >> 4); p < pixels; p += (long long)gridDim.x * 16) {
-    const int nn = (int)(p / hw);
-    const long long r = p - nn * hw;
-    const size_t ii = ((size_t)(nn * s.H + (int)(r / w) + s.oy) * s.W + (int)(r % w) + s.ox) * 64 + c;
-    const float4 yv = s.h16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + ii))
-                            : ld4(s.ptr + ii);
-    float g[K];
+  const int hw = h * w;
+  // U pixels per loop trip, every load issued (branch-free, clamped) before any
+  // use: the loop was one or two HBM round trips per pixel
+  constexpr int U = 4;
+  const int stride = gridDim.x * 16;
+  for (int p0 = blockIdx.x * 16 + (tid >> 4); p0 < pixels; p0 += U * stride) {
+    float4 yv[U];
+    float g[U][K];
+    int rr[U], nnu[U];
 #pragma unroll
-    for (int k = 0; k < K; ++k) g[k] = k < kn ? dl[((size_t)nn * kn + k) * hw + r] : 0.f;
-    const float zx = fmaf(yv.x, sc.x, sf.x), zy = fmaf(yv.y, sc.y, sf.y), zz = fmaf(yv.z, sc.z, sf.z),
-                zw = fmaf(yv.w, sc.w, sf.w);
-    float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < U; ++u) {
+      const int p = min(p0 + u * stride, pixels - 1);
+      const int nn = p / hw, r = p - nn * hw;
+      const int y = r / w, x = r - y * w;
+      nnu[u] = nn;
+      rr[u] = r;
+      const size_t ii = ((size_t)(nn * s.H + y + s.oy) * s.W + x + s.ox) * 64 + c;
+      yv[u] = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + ii))
+                  : ld4(s.ptr + ii);
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      d.x = fmaf(wk[k].x, g[k], d.x);
-      d.y = fmaf(wk[k].y, g[k], d.y);
-      d.z = fmaf(wk[k].z, g[k], d.z);
-      d.w = fmaf(wk[k].w, g[k], d.w);
-      dwa[k][0] += g[k] * fmaxf(zx, 0.f);
-      dwa[k][1] += g[k] * fmaxf(zy, 0.f);
-      dwa[k][2] += g[k] * fmaxf(zz, 0.f);
-      dwa[k][3] += g[k] * fmaxf(zw, 0.f);
-      dba[k] += g[k];
+      for (int k = 0; k < K; ++k) g[u][k] = dl[((size_t)nn * kn + min(k, kn - 1)) * hw + r];
     }
-    d.x = zx > 0.f ? d.x : 0.f;
-    d.y = zy > 0.f ? d.y : 0.f;
-    d.z = zz > 0.f ? d.z : 0.f;
-    d.w = zw > 0.f ? d.w : 0.f;
-    if (dz16) {  // bf16 plans store dz bf16: statistics of the rounded values
-      d.x = round_bf(d.x);
-      d.y = round_bf(d.y);
-      d.z = round_bf(d.z);
-      d.w = round_bf(d.w);
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int p = p0 + u * stride;
+      if (p >= pixels) continue;
+#pragma unroll
+      for (int k = 0; k < K; ++k) g[u][k] = k < kn ? g[u][k] : 0.f;
+      const float zx = fmaf(yv[u].x, sc.x, sf.x), zy = fmaf(yv[u].y, sc.y, sf.y), zz = fmaf(yv[u].z, sc.z, sf.z),
+                  zw = fmaf(yv[u].w, sc.w, sf.w);
+      float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        d.x = fmaf(wk[k].x, g[u][k], d.x);
+        d.y = fmaf(wk[k].y, g[u][k], d.y);
+        d.z = fmaf(wk[k].z, g[u][k], d.z);
+        d.w = fmaf(wk[k].w, g[u][k], d.w);
+        dwa[k][0] += g[u][k] * fmaxf(zx, 0.f);
+        dwa[k][1] += g[u][k] * fmaxf(zy, 0.f);
+        dwa[k][2] += g[u][k] * fmaxf(zz, 0.f);
+        dwa[k][3] += g[u][k] * fmaxf(zw, 0.f);
+        dba[k] += g[u][k];
+      }
+      d.x = zx > 0.f ? d.x : 0.f;
+      d.y = zy > 0.f ? d.y : 0.f;
+      d.z = zz > 0.f ? d.z : 0.f;
+      d.w = zw > 0.f ? d.w : 0.f;
+      if (dz16) {  // bf16 plans store dz bf16: statistics of the rounded values
+        d.x = round_bf(d.x);
+        d.y = round_bf(d.y);
+        d.z = round_bf(d.z);
+        d.w = round_bf(d.w);
+      }
+      sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
+      sb[0] += d.x * (yv[u].x - mu.x) * is.x;
+      sb[1] += d.y * (yv[u].y - mu.y) * is.y;
+      sb[2] += d.z * (yv[u].z - mu.z) * is.z;
+      sb[3] += d.w * (yv[u].w - mu.w) * is.w;
+      if (dz16)
+        reinterpret_cast<uint2*>(dz)[((size_t)p * 64 + c) / 4] = make_uint2(bf16pack(d.x, d.y), bf16pack(d.z, d.w));
+      else
+        st4(dz + (size_t)p * 64 + c, d);
     }
-    sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
-    sb[0] += d.x * (yv.x - mu.x) * is.x;
-    sb[1] += d.y * (yv.y - mu.y) * is.y;
-    sb[2] += d.z * (yv.z - mu.z) * is.z;
-    sb[3] += d.w * (yv.w - mu.w) * is.w;
-    if (dz16)
-      reinterpret_cast<uint2*>(dz)[((size_t)p * 64 + c) / 4] = make_uint2(bf16pack(d.x, d.y), bf16pack(d.z, d.w));
-    else
-      st4(dz + (size_t)p * 64 + c, d);
   }
   reduce_pairs_to_global(sa, sb, 16, 64, bstats + (size_t)(blockIdx.x % kStatGroups) * 64 * 2);
   __syncthreads();
@@ -1095,15 +1114,26 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
   dim3 grid(grid_cap(pixels, 16 * 8, 512));
   hipError_t me = hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
   if (me != hipSuccess) return me;
+  if (pixels >= (1LL << 31)) return hipErrorInvalidValue;
+#define HEAD_BWD(KK)                                                                                            \
+  do {                                                                                                          \
+    if (s.h16)                                                                                                  \
+      hipLaunchKernelGGL((k_head_bwd<KK, 1>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, \
+                         acc, dz_h16, k);                                                                       \
+    else                                                                                                        \
+      hipLaunchKernelGGL((k_head_bwd<KK, 0>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, \
+                         acc, dz_h16, k);                                                                       \
+  } while (0)
   switch (class_capacity(k)) {
-    case 1: hipLaunchKernelGGL(k_head_bwd<1>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
-    case 2: hipLaunchKernelGGL(k_head_bwd<2>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
-    case 3: hipLaunchKernelGGL(k_head_bwd<3>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
-    case 4: hipLaunchKernelGGL(k_head_bwd<4>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
-    case 8: hipLaunchKernelGGL(k_head_bwd<8>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
-    case 16: hipLaunchKernelGGL(k_head_bwd<16>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
-    default: hipLaunchKernelGGL(k_head_bwd<32>, grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, acc, dz_h16, k); break;
+    case 1: HEAD_BWD(1); break;
+    case 2: HEAD_BWD(2); break;
+    case 3: HEAD_BWD(3); break;
+    case 4: HEAD_BWD(4); break;
+    case 8: HEAD_BWD(8); break;
+    case 16: HEAD_BWD(16); break;
+    default: HEAD_BWD(32); break;
   }
+#undef HEAD_BWD
   hipLaunchKernelGGL(k_d2f, dim3(cdiv(k * 64, 256)), dim3(256), 0, st, acc, k * 64, dw);
   hipLaunchKernelGGL(k_d2f, dim3(1), dim3(64), 0, st, acc + k * 64, k, db);
   return hipGetLastError();

@@ -291,20 +291,31 @@ __global__ __launch_bounds__(256) void k_wino4_in(Gather g, int Th, int Tw, long
   const char* base = reinterpret_cast<const char*>(s.ptr) +
                      ((size_t)(n * s.H + 4 * ty + s.oy) * s.W + 4 * tx + s.ox) * s.C * 4 + (size_t)cl * 4;
   const unsigned rs = (unsigned)s.W * s.C * 4u, cs = (unsigned)s.C * 4u;
+  // all 36 loads first (unconditional, clamped address), then the BatchNorm
+  // branch once: a load consumed inside a branch region is waited for at the
+  // region's boundary, which serialised the 36 loads
+  vec raw[6][6];
+#pragma unroll
+  for (int xx = 0; xx < 6; ++xx)
+#pragma unroll
+    for (int yy = 0; yy < 6; ++yy) {
+      const bool in = yy < vr && xx < vc;
+      raw[yy][xx] = *reinterpret_cast<const vec*>(base + (in ? yy * rs + xx * cs : 0u));
+    }
+  if (s.scale) {
+#pragma unroll
+    for (int xx = 0; xx < 6; ++xx)
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+        for (int k = 0; k < V; ++k) raw[yy][xx][k] = fmaxf(fmaf(raw[yy][xx][k], sc[k], sh[k]), 0.f);
+  }
   vec e[6][6];  // B^T d (rows), per column
 #pragma unroll
   for (int xx = 0; xx < 6; ++xx) {
     vec d[6];
 #pragma unroll
-    for (int yy = 0; yy < 6; ++yy) {
-      const bool in = yy < vr && xx < vc;  // unconditional load, clamped address
-      vec v = *reinterpret_cast<const vec*>(base + (in ? yy * rs + xx * cs : 0u));
-      if (s.scale) {
-#pragma unroll
-        for (int k = 0; k < V; ++k) v[k] = fmaxf(fmaf(v[k], sc[k], sh[k]), 0.f);
-      }
-      d[yy] = in ? v : (vec)0.f;
-    }
+    for (int yy = 0; yy < 6; ++yy) d[yy] = (yy < vr && xx < vc) ? raw[yy][xx] : (vec)0.f;
     e[0][xx] = 4.f * d[0] - 5.f * d[2] + d[4];
     e[1][xx] = -4.f * (d[1] + d[2]) + d[3] + d[4];
     e[2][xx] = 4.f * (d[1] - d[2]) - d[3] + d[4];
@@ -547,10 +558,14 @@ __global__ __launch_bounds__(256) void k_wino6_in(Gather g, int Th, int Tw, long
   const bool second = c >= g.c_split;
   const Src s = pick_src(g, second);
   const int cl = second ? c - g.c_split : c;
-  vec sc, sh;
+  // producer BatchNorm + ReLU as max(fma(x, sc, sh), lo), identity without one:
+  // branch-free, so the 64 loads are not serialised at branch boundaries
+  vec sc = (vec)1.f, sh = (vec)0.f;
+  float lo = -INFINITY;
   if (s.scale) {
     sc = *reinterpret_cast<const vec*>(s.scale + cl);
     sh = *reinterpret_cast<const vec*>(s.shift + cl);
+    lo = 0.f;
   }
   const int vr = min(8, g.Hg + 2 - 6 * ty), vc = min(8, g.Wg + 2 - 6 * tx);
   const char* base = reinterpret_cast<const char*>(s.ptr) +
@@ -566,8 +581,7 @@ __global__ __launch_bounds__(256) void k_wino6_in(Gather g, int Th, int Tw, long
       vec v = *reinterpret_cast<const vec*>(base + (in ? yy * rs + xx * cs : 0u));
 #pragma unroll
       for (int k = 0; k < V; ++k) {
-        float x = v[k];
-        if (s.scale) x = fmaxf(fmaf(x, sc[k], sh[k]), 0.f);
+        const float x = fmaxf(fmaf(v[k], sc[k], sh[k]), lo);
         d[k][yy] = in ? x : 0.f;
       }
     }
@@ -1210,7 +1224,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
                                                      int Th, int Tw, int NB, Epilogue e) {
   constexpr int PU = 32 * 8 + 8;  // U point plane (+8: the two lane rows of a patch store 18 planes apart)
   constexpr int PV = 64 * 8;      // V point plane
-  __shared__ __attribute__((aligned(16))) float lds[36 * 1024];  // U + V, then X [36][32][32]
+  __shared__ __attribute__((aligned(16))) float lds[36 * PU + 36 * PV];  // U, V
   float* Us = lds;
   float* Vs = lds + 36 * PU;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1330,16 +1344,18 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
     }
   };
 
-  // ---- MFMA role: tile half th, points 9 pg .. 9 pg + 8, four channel blocks ----
-  const int th = wave & 1, pg = wave >> 1;
+  // ---- MFMA role: wave = (tile half th, 16-channel block cb), all 36 points ----
+  // C_p = V_p^T U_p (channels as MFMA rows, tiles as columns): lane (mi, mq)
+  // holds every point of channels 4 mq .. 4 mq + 3 of tile mi, applies A^T M A
+  // from registers and stores 4 channels per pixel with one 16-B store (the
+  // LDS output stage and its 64 scalar stores per lane are gone).
+  const int th = wave & 1, cb = wave >> 1;
   const int mi = lane & 15, mq = lane >> 4;
   const int aoff = (16 * th + mi) * 8 + wf8_slot(16 * th + mi, mq);
-  const int boff = mi * 8 + wf8_slot(mi, mq);  // + 128 per 16-channel block (bit 3 of the row unchanged)
-  floatx4 acc[9][4];
+  const int boff = (16 * cb + mi) * 8 + wf8_slot(mi, mq);  // rows 16 cb + mi and mi agree on bit 3
+  floatx4 acc[36];
 #pragma unroll
-  for (int j = 0; j < 9; ++j)
-#pragma unroll
-    for (int c = 0; c < 4; ++c) acc[j][c] = (floatx4){0.f, 0.f, 0.f, 0.f};
+  for (int p = 0; p < 36; ++p) acc[p] = (floatx4){0.f, 0.f, 0.f, 0.f};
   load(0);
   for (int kc = 0; kc < nk; ++kc) {
     commit(kc);
@@ -1347,38 +1363,118 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
     if (!(ABL & 4) && kc + 1 < nk) load(kc + 1);
     if constexpr (!(ABL & 2))
 #pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int p = pg * 9 + j;
+    for (int p = 0; p < 36; ++p) {
       const float2 a = *reinterpret_cast<const float2*>(Us + p * PU + aoff);
-      float2 b[4];
-#pragma unroll
-      for (int c = 0; c < 4; ++c) b[c] = *reinterpret_cast<const float2*>(Vs + p * PV + boff + 128 * c);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[j][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b[c].x, acc[j][c], 0, 0, 0);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) acc[j][c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b[c].y, acc[j][c], 0, 0, 0);
+      const float2 b = *reinterpret_cast<const float2*>(Vs + p * PV + boff);
+      acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.x, a.x, acc[p], 0, 0, 0);
+      acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.y, a.y, acc[p], 0, 0, 0);
     }
     __syncthreads();
   }
-
-  // ---- two 32-channel passes: accumulators -> X[36][32][32] -> wf_output ----
-  if constexpr (ABL & 8) {
-    if (acc[0][0][0] == 1.2345f) e.d[0].ptr[tid] = acc[8][3][3];  // keep the accumulators live
+  if constexpr (ABL & 8) {  // every accumulator stays live (the MFMAs are kept)
+    float sum = 0.f;
+#pragma unroll
+    for (int p = 0; p < 36; ++p) sum += acc[p][0] + acc[p][1] + acc[p][2] + acc[p][3];
+    if (sum == 1.2345f) e.d[0].ptr[tid] = sum;
     return;
   }
-  float* X = lds;
+
+  // ---- output: tile 16 th + mi, channels n0 + 16 cb + 4 mq + (0..3) ----
+  const long long tt = t0 + 16 * th + mi;
+  const int col0 = n0 + 16 * cb + 4 * mq;
+  const bool second = col0 >= e.n_split;  // uniform per 16-channel block (n_split % 16 == 0)
+  float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
+  const int dC = second ? e.d[1].C : e.d[0].C;
+  const int dcol = second ? col0 - e.n_split : col0;
+  const bool bwd_mask = e.yref != nullptr && !second;
+  const float4 bias = e.bias ? ld4(e.bias + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+  float4 bsc = make_float4(0.f, 0.f, 0.f, 0.f), bsh = bsc, bmu = bsc, bis = bsc;
+  if (bwd_mask) { bsc = ld4(e.bn_scale + col0); bsh = ld4(e.bn_shift + col0); bmu = ld4(e.bn_mean + col0); bis = ld4(e.bn_invstd + col0); }
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (tt < T) {
+    float o[4][4][4];  // [channel][row][col]
 #pragma unroll
-  for (int hh = 0; hh < 2; ++hh) {
-    if (hh) __syncthreads();  // pass 0's wf_output has finished reading X / red
+    for (int r = 0; r < 4; ++r) {
+      float w[4][6];
 #pragma unroll
-    for (int j = 0; j < 9; ++j)
+      for (int xx = 0; xx < 6; ++xx) {
+        float m[6];
 #pragma unroll
-      for (int c = 0; c < 2; ++c)
+        for (int yy = 0; yy < 6; ++yy) m[yy] = acc[yy * 6 + xx][r];
+        float t4[4];
+        at4(m, t4);
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          X[(pg * 9 + j) * 1024 + (16 * th + 4 * mq + r) * 32 + 16 * c + mi] = acc[j][2 * hh + c][r];
-    __syncthreads();
-    wf_output(lds, tid, t0, n0 + 32 * hh, T, Th, Tw, N, g, e);
+        for (int a = 0; a < 4; ++a) w[a][xx] = t4[a];
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) at4(w[a], o[r][a]);
+    }
+    const int ox = (int)(tt % Tw);
+    const long long rq = tt / Tw;
+    const int oy = (int)(rq % Th), on = (int)(rq / Th);
+    const float bsv[4] = {bias.x, bias.y, bias.z, bias.w};
+    const float scv[4] = {bsc.x, bsc.y, bsc.z, bsc.w}, shv[4] = {bsh.x, bsh.y, bsh.z, bsh.w};
+    const float muv[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, isv[4] = {bis.x, bis.y, bis.z, bis.w};
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const int y = 4 * oy + a;
+      if (y >= g.Hg) continue;
+#pragma unroll
+      for (int bb = 0; bb < 4; ++bb) {
+        const int x = 4 * ox + bb;
+        if (x >= g.Wg) continue;
+        const size_t idx = ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol;
+        float yv[4] = {0.f, 0.f, 0.f, 0.f};
+        if (bwd_mask) {
+          const float4 y4 = ld4(e.yref + idx);
+          yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
+        }
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = o[r][a][bb] + bsv[r];
+          if (bwd_mask) {
+            v[r] = fmaf(yv[r], scv[r], shv[r]) > 0.f ? v[r] : 0.f;
+            s1[r] += v[r];
+            s2[r] += v[r] * ((yv[r] - muv[r]) * isv[r]);
+          } else if (e.stats) {
+            s1[r] += v[r];
+            s2[r] += v[r] * v[r];
+          } else if (second && e.colsum1) {
+            s1[r] += v[r];
+          }
+          if (e.relu) v[r] = fmaxf(v[r], 0.f);
+        }
+        st4(dptr + idx, make_float4(v[0], v[1], v[2], v[3]));
+      }
+    }
+  }
+  const bool want = e.stats || e.yref || e.colsum1;
+  if (!want) return;
+  // the 16 lanes of a quarter hold the same 4 channels (other tiles)
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) {
+      s1[r] += __shfl_xor(s1[r], o2);
+      s2[r] += __shfl_xor(s2[r], o2);
+    }
+  if (mi == 0) {
+    const int grp = blockIdx.x % kStatGroups;
+    const int nsplit = e.n_split < N ? e.n_split : N;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = col0 + r;
+      if (col < nsplit) {
+        double* st = e.yref ? e.bstats : e.stats;
+        if (st) {
+          atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)s1[r]);
+          atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)s2[r]);
+        }
+      } else if (e.colsum1) {
+        atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (col - nsplit), (double)s1[r]);
+      }
+    }
   }
 }
 
