@@ -24,7 +24,9 @@ def bench_tuning():
     from unet_amd import _lib
     lib = _lib.load()
     lib.unet_tuning_reset()
-    n = lib.unet_tuning_load(TUNE_DB.encode()) if os.path.exists(TUNE_DB) else 0
+    # UNET_TEST_TUNE_DB=<path> replays another database ('' = none: tune live)
+    db = os.environ.get("UNET_TEST_TUNE_DB", TUNE_DB)
+    n = lib.unet_tuning_load(db.encode()) if db and os.path.exists(db) else 0
     print(f"tuning database: {n} entries ({_lib.build_identity()})")
     yield n
     lib.unet_tuning_reset()

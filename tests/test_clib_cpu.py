@@ -192,3 +192,18 @@ def test_library_built_from_this_tree():
     ident = L.build_identity()
     assert ident["src_match"], ident
 
+
+
+def test_pipeline_crop_views_and_cpu_rejection():
+    """unet_amd.pipeline: train.py:39-51's center crop as a strided view (offset
+    (H - oh) // 2, squeeze(1), no copy), and no CPU path for the frames."""
+    import torch
+    from unet_amd.pipeline import HeLaBatches, center_crop_views
+    t = torch.arange(2 * 1 * 9 * 8).reshape(2, 1, 9, 8)
+    v = center_crop_views(t, (4, 3))
+    assert v.shape == (2, 4, 3) and v.data_ptr() == t[:, :, 2:6, 2:5].data_ptr()
+    assert torch.equal(v, t[:, 0, 2:6, 2:5])
+    with pytest.raises(ValueError):
+        center_crop_views(t, (10, 3))
+    with pytest.raises(ValueError):
+        HeLaBatches(torch.zeros((2, 8, 8), dtype=torch.uint8), torch.zeros((2, 8, 8), dtype=torch.int32), 2, (4, 4))

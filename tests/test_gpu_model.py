@@ -512,7 +512,7 @@ def check_grad_digests(named_grads, z, rel=1e-2, vtol=2e-2):
     BN-cancelled biases are compared absolutely."""
     worst = 0.0
     for name, g in named_grads:
-        g = g.detach().double().cpu().numpy().ravel()
+        g = (g.detach().double().cpu().numpy() if hasattr(g, "detach") else np.asarray(g, np.float64)).ravel()
         ref_norm = float(z[f"gnorm/{name}"])
         if O.bn_cancelled(name):
             wn = float(z[f"gnorm/{name.replace('.bias', '.weight')}"])

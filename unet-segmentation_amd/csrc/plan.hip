@@ -296,13 +296,33 @@ std::string wgrad_key(const WgradArgs& a) {
   return b;
 }
 
+// UNET_TUNE_SKIP="73,74": tile ids the autotuner never tries (A/B experiments
+// on accuracy or speed; igemm and wgrad ids alike)
+bool tune_skipped(int tile) {
+  static const std::vector<int> skip = [] {
+    std::vector<int> v;
+    if (const char* e = getenv("UNET_TUNE_SKIP"))
+      for (const char* q = e; *q;) {
+        char* end = nullptr;
+        const long t = strtol(q, &end, 10);
+        if (end == q) { ++q; continue; }
+        v.push_back((int)t);
+        q = end;
+      }
+    return v;
+  }();
+  for (int t : skip)
+    if (t == tile) return true;
+  return false;
+}
+
 std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) {
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
                 36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 81, 82, 83, 84, 70, 71, 72, 73,
                 74}) {  // fits() filters by precision and gather
-    if (!igemm_tile_fits(a, t)) continue;
+    if (!igemm_tile_fits(a, t) || tune_skipped(t)) continue;
     v.push_back({t, 1});
     if (t == 70 || t == 71 || t == 74)  // Winograd: no K split; the tile of its batched point GEMMs
       for (int inner : {1, 2, 3, 4, 6, 7, 8, 9}) v.push_back({t, 100 + inner});
@@ -321,7 +341,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
 std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   std::vector<GemmChoice> v;
   for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 24, 25, 71, 74}) {  // fits() filters by precision
-    if (!wgrad_tile_fits(a, t)) continue;
+    if (!wgrad_tile_fits(a, t) || tune_skipped(t)) continue;
     if (t == 71 || t == 74) {  // Winograd: point-GEMM tile (k_wgrad 0-4) x workgroups per CU
       for (int inner : {0, 1, 2, 3, 4})
         for (int per_cu : {4, 8, 16}) v.push_back({t, per_cu + 100 * (inner + 1)});
