@@ -158,7 +158,7 @@ def full_size_train_case(tag, n, h, n_channels=1, seed=5):
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
-def bf16_oracle_case(tag, n, h, n_channels=1, seed=5):
+def bf16_oracle_case(tag, n, h, n_channels=1, seed=5, dtype=np.float64):
     """The bf16 arithmetic's own distance from the reference (configs[2] and
     configs[4]: bf16-in / fp32-acc GEMMs): the NumPy restatement with the HIP
     bf16 plan's roundings (UNetOracle(gemm="bf16"), every product and sum in
@@ -169,10 +169,14 @@ def bf16_oracle_case(tag, n, h, n_channels=1, seed=5):
     cannot be argmax-exact).  Written to ``train_{tag}_bf16.npz``."""
     params = O.hash_init(n_channels, 2, seed=seed, bn_random=True)
     x, tgt, wmap = F.make_inputs(seed, n, n_channels, h)
-    net = O.UNetOracle(params, gemm="bf16")
+    # dtype=float32: the same roundings with every sum in fp32 -- its distance
+    # from the fp64 run is the rounding-boundary floor (an operand that lands
+    # on the other side of a bf16 rounding boundary under a different fp32
+    # summation order), the bar tests/test_gpu_bf16.py uses at small sizes
+    net = O.UNetOracle(params, gemm="bf16", dtype=dtype)
     lg, cache, nb = net.forward(x)
     loss, dl = O.weighted_ce(lg, tgt, wmap)
-    g = net.backward(dl, cache)
+    g = net.backward(np.asarray(dl, dtype), cache)
     del cache
     out = {"x_seed": np.array(seed), "n": np.array(n), "h": np.array(h), "c": np.array(n_channels),
            "loss": np.array(loss), "logits_sample": lg[:, :, ::7, ::5].copy(),
@@ -184,7 +188,7 @@ def bf16_oracle_case(tag, n, h, n_channels=1, seed=5):
     for k, v in nb.items():
         if "running" in k:
             out[f"buf/{k}"] = np.asarray(v, np.float64)
-    path = os.path.join(HERE, f"train_{tag}_bf16.npz")
+    path = os.path.join(HERE, f"train_{tag}_bf16{'' if dtype == np.float64 else '_f32'}.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes")
 
@@ -447,6 +451,9 @@ if __name__ == "__main__":
         full_size_train_case("n8_512", 8, 512, seed=6)
     if "t572c3" in which:  # configs[4]: 3-ch 572^2 train step (fwd + bwd), batch 2
         full_size_train_case("n2_c3_572", 2, 572, n_channels=3, seed=7)
+    if "bf16f32" in which:  # the same in fp32 sums: the rounding-boundary floor at size
+        bf16_oracle_case("n8_512", 8, 512, seed=6, dtype=np.float32)
+        bf16_oracle_case("n2_c3_572", 2, 572, n_channels=3, seed=7, dtype=np.float32)
     if "bf16" in which:  # the bf16 roundings' own floor for the bf16 tests at size
         bf16_oracle_case("n8_512", 8, 512, seed=6)
         bf16_oracle_case("n2_c3_572", 2, 572, n_channels=3, seed=7)

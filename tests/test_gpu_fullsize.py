@@ -67,9 +67,34 @@ def trainer_step(params, x, tgt, wmap, precision, n_channels=1):
     return tr.logits.double().cpu().numpy(), float(loss.item()), grads, m
 
 
-def check_bf16_vs_reference(z, zb, lg, loss, grads, tag):
+def flip_floors(zb, zf):
+    """The rounding-boundary noise of the bf16 arithmetic at this size: the bf16
+    oracle with every sum in fp32 (zf, tests/golden/make_golden.py bf16f32)
+    against the same oracle in fp64 (zb).  A GPU run (fp32 sums in a different
+    order) is one more sample of that noise: per tensor its own deviation, and
+    per kind (BatchNorm parameters / everything else) the largest deviation of
+    the kind -- measured 0.7-1.0 % median and 2.8-3.3 % max on the BatchNorm
+    parameters (0.05-0.07 % / 0.3-0.7 % on the conv weights) at batch 8 x 512^2
+    and 2 x 3 x 572^2."""
+    per, kind = {}, {True: 0.0, False: 0.0}
+    for k in zb.files:
+        if not k.startswith("gbf16norm/"):
+            continue
+        name = k.split("/", 1)[1]
+        if O.bn_cancelled(name):
+            continue
+        rb = float(zb[k])
+        per[name] = abs(float(zf[k]) - rb)
+        bn = O.is_bn_param(name)
+        kind[bn] = max(kind[bn], per[name] / max(rb, 1e-30))
+    return per, kind
+
+
+def check_bf16_vs_reference(z, zb, lg, loss, grads, tag, zf=None):
     """SURVEY.md §7's bar for bf16 configs against the fp64 reference fixture z,
-    floors from the bf16 oracle's own distance to it (zb)."""
+    floors from the bf16 oracle's own distance to it (zb) and from its
+    rounding-boundary noise (zf: the same oracle in fp32 sums)."""
+    flip, kind = flip_floors(zb, zf) if zf is not None else ({}, {True: 0.0, False: 0.0})
     ref_loss, bf_loss = float(z["loss"]), float(zb["loss"])
     wout = lg.shape[-1]
     lo = abs(loss - ref_loss) / abs(ref_loss)
@@ -93,22 +118,22 @@ def check_bf16_vs_reference(z, zb, lg, loss, grads, tag):
             continue
         floor = abs(float(zb[f"gbf16norm/{name}"]) - r)
         # the GPU result carries its own bf16 rounding pattern (fp32 sums, tuned
-        # tile mix) on top of the one the bf16 oracle measures: within 3 floors.
-        # BatchNorm affine gradients are sums over 0.1-2 M bf16-stored BN-input
-        # gradients with heavy cancellation: two fp32-summing bf16 runs with
-        # different (timing-tuned) kernel mixes differed by up to 1.7 % on them
-        # (GPUTEST runs g9 / g10 of round 3), so their relative bar is 2 %
+        # tile mix) on top of the one the bf16 oracle measures: within 3 floors,
+        # 3 x the tensor's rounding-boundary noise, and 1.5 x the largest such
+        # noise of its kind (BatchNorm affine gradients are sums over 0.1-2 M
+        # bf16-stored BN-input gradients with heavy cancellation)
+        rb = float(zb[f"gbf16norm/{name}"])
+        noise = max(3 * flip.get(name, 0.0), 1.5 * kind[O.is_bn_param(name)] * rb)
         rel = 2e-2 if O.is_bn_param(name) else 1e-2
-        tol = max(rel * r, 3 * floor)
+        tol = max(rel * r, 3 * floor, noise)
         e = abs(np.linalg.norm(g) - r)
         worst = max(worst, e / tol)
         assert e <= tol, (tag, name, np.linalg.norm(g), r, floor)
         # against the bf16 oracle's own gradient (same roundings, fp64 sums): the
         # GPU's fp32 sums move operands across bf16 rounding boundaries, a
         # perturbation of the same kind as bf16's own -- within 3 % or 3 x it
-        rb = float(zb[f"gbf16norm/{name}"])
         eb = abs(np.linalg.norm(g) - rb)
-        tb = max(3e-2 * rb, 3 * floor)
+        tb = max(3e-2 * rb, 3 * floor, noise)
         worst_b = max(worst_b, eb / tb)
         assert eb <= tb, (tag, name, np.linalg.norm(g), rb)
     print(f"{tag}: loss rel {lo:.2e} (bf16 oracle {abs(bf_loss - ref_loss) / abs(ref_loss):.2e}), "
@@ -122,11 +147,12 @@ def test_trainer_bf16_batch8_512_vs_reference():
     fixture (tests/golden/train_n8_512.npz) at the bf16 bar."""
     z = np.load(os.path.join(G, "train_n8_512.npz"), allow_pickle=False)
     zb = np.load(os.path.join(G, "train_n8_512_bf16.npz"), allow_pickle=False)
+    zf = np.load(os.path.join(G, "train_n8_512_bf16_f32.npz"), allow_pickle=False)
     seed, n, h = int(z["x_seed"]), int(z["n"]), int(z["h"])
     params = O.hash_init(1, 2, seed=seed, bn_random=True)
     x, tgt, wmap = F.make_inputs(seed, n, 1, h)
     lg, loss, grads, m = trainer_step(params, x, tgt, wmap, "bf16")
-    check_bf16_vs_reference(z, zb, lg, loss, grads, "bf16 8x512")
+    check_bf16_vs_reference(z, zb, lg, loss, grads, "bf16 8x512", zf)
     sd = m.state_dict()
     for k in zb.files:  # running statistics: the bf16 oracle's (same rounded conv outputs)
         if k.startswith("buf/"):
@@ -147,7 +173,8 @@ def test_c3_572_train_step_vs_reference(precision):
     assert lg.shape == (n, 2, 388, 388)
     if precision == "bf16":
         zb = np.load(os.path.join(G, "train_n2_c3_572_bf16.npz"), allow_pickle=False)
-        check_bf16_vs_reference(z, zb, lg, loss, grads, "bf16 2x3x572")
+        zf = np.load(os.path.join(G, "train_n2_c3_572_bf16_f32.npz"), allow_pickle=False)
+        check_bf16_vs_reference(z, zb, lg, loss, grads, "bf16 2x3x572", zf)
         return
     from test_gpu_model import check_full_size_outputs, check_grad_digests
     low = check_full_size_outputs(lg, loss, z, lg.shape[-1])
