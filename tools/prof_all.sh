@@ -7,12 +7,12 @@
 # every profiled pass come from one plain bench run per precision through the
 # tuning database (UNET_TUNE_DB), so the counters describe the bench's kernels.
 # Raw trace directories are deleted after reduction.
-#   tools/prof_all.sh <outdir> <round tag, e.g. r02>
+#   tools/prof_all.sh <outdir> <round tag, e.g. r02> ["fp32 bf16"] [trace: 1 / 0]
 set -o pipefail
-out=$1; tag=$2
+out=$1; tag=$2; dts=${3:-"fp32 bf16"}; do_trace=${4:-1}
 export TMPDIR=/tmp
 mkdir -p "$out"
-for dt in fp32 bf16; do
+for dt in $dts; do
   raw="$out/raw_$dt"
   extra=""; [ "$dt" = bf16 ] && extra="--dtype bf16"
   # tune once in a plain (unprofiled) bench run; every profiled pass replays
@@ -30,6 +30,7 @@ for dt in fp32 bf16; do
   python3 tools/step_kernels.py "$raw/trace/run_kernel_trace.csv" --top 40 > "$out/${tag}_step_kernels_$dt.txt" || exit 1
   rm -rf "$raw"
 done
+[ "$do_trace" = 1 ] || { echo done; exit 0; }
 echo "== trace 50 steps"
 export UNET_TUNE_DB="$out/tune_fp32.db"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$out/raw_tr" -o run -- python3 bench.py --steps 50 --warmup 10 \

@@ -1091,8 +1091,15 @@ int g_wino_max = env_int("UNET_WINO_MAX", 4);
 int g_wino_dgrad_max = env_int("UNET_WINO_DGRAD_MAX", 4);  // input gradients (no forward BN statistics)
 int g_wino_wgrad_max = env_int("UNET_WINO_WGRAD_MAX", 6);
 // "wino4_fwd_min_cg" / UNET_WINO4_FWD_MIN_CG: forward (BN-statistics) GEMMs use
-// F(4x4) only from this many input channels on (accuracy / speed sweeps)
-int g_wino4_fwd_min_cg = env_int("UNET_WINO4_FWD_MIN_CG", 0);
+// F(4x4) only from this many input channels on.  The forward's rounding feeds
+// the BatchNorm statistics and from there every gradient: with F(4x4) on every
+// forward GEMM the 512^2 every-element gradient check landed at 1.00-1.07 % on
+// a deep BatchNorm parameter against its 1 % bar (fp32 direct GEMMs: 0.72 %);
+// from 128 channels on 1.03 %; from 256 on 0.81 % (profiles/r03_wino_fwd_sweep.txt,
+// fp32 bench 301 / 291 / 277 img/s)
+int g_wino4_fwd_min_cg = env_int("UNET_WINO4_FWD_MIN_CG", 256);
+// ... and also up to this many ("wino4_fwd_small_cg" / UNET_WINO4_FWD_SMALL_CG)
+int g_wino4_fwd_small_cg = env_int("UNET_WINO4_FWD_SMALL_CG", 0);
 static int wino_tile_m(int tile) {
   return tile == 70 ? 2 : tile == 71 || tile == 72 || tile == 73 ? 4 : tile == 74 ? 6 : 0;
 }
@@ -1172,7 +1179,8 @@ static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   // every 3x3 forward conv feeds a BatchNorm (stats); the input gradients do not
   if (wino_tile_m(tile) > (a.e.stats ? g_wino_max : g_wino_dgrad_max)) return false;
-  if (a.e.stats && wino_tile_m(tile) >= 4 && a.a.Cg < g_wino4_fwd_min_cg) return false;
+  if (a.e.stats && wino_tile_m(tile) >= 4 && a.a.Cg < g_wino4_fwd_min_cg && a.a.Cg > g_wino4_fwd_small_cg)
+    return false;
   const TileInfo t = tile_info(tile);
   const bool prec_ok = is_bf16_tile(tile) ? a.bh != nullptr && (a.bl == nullptr || bf16_tile_splits(tile))
                                            : a.b != nullptr;

@@ -12,7 +12,7 @@ using namespace unet;
 
 namespace unet {
 extern int g_tune_igemm, g_tune_wgrad, g_autotune, g_force_split, g_force_tile, g_concurrent, g_wino_max,
-    g_wino_dgrad_max, g_wino_wgrad_max, g_bf16_norm, g_bn_fold, g_wino4_fwd_min_cg;
+    g_wino_dgrad_max, g_wino_wgrad_max, g_bf16_norm, g_bn_fold, g_wino4_fwd_min_cg, g_wino4_fwd_small_cg;
 hipError_t launch_fill(float* p, size_t n, float v, hipStream_t s);
 hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream_t s);
 }  // namespace unet
@@ -390,6 +390,7 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "wino_dgrad_max") g_wino_dgrad_max = value;
   else if (k == "wino_wgrad_max") g_wino_wgrad_max = value;
   else if (k == "wino4_fwd_min_cg") g_wino4_fwd_min_cg = value;
+  else if (k == "wino4_fwd_small_cg") g_wino4_fwd_small_cg = value;
   else if (k == "op_a16") g_op_a16 = value != 0;
   else if (k == "op_precision") {
     if (value != UNET_PREC_FP32 && value != UNET_PREC_BF16 && value != UNET_PREC_BF16X3) return -EINVAL;

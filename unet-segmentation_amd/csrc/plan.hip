@@ -26,7 +26,7 @@
 using namespace unet;
 
 namespace unet {
-extern int g_wino_max, g_wino_dgrad_max, g_wino_wgrad_max;  // igemm.hip (Winograd tile caps)
+extern int g_wino_max, g_wino_dgrad_max, g_wino_wgrad_max, g_wino4_fwd_min_cg, g_wino4_fwd_small_cg;  // igemm.hip (Winograd tile caps)
 // unet_set_tuning("autotune", v) or UNET_AUTOTUNE (default on)
 int g_autotune = getenv("UNET_AUTOTUNE") ? atoi(getenv("UNET_AUTOTUNE")) : 1;
 // unet_set_tuning("concurrent", v) or UNET_CONCURRENT (default on): weight
@@ -274,16 +274,17 @@ constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 constexpr int kTileTableVersion = 6;
 
 std::string igemm_key(const IgemmArgs& a) {
-  char b[240];
+  char b[240], small[16] = "";
+  if (unet::g_wino4_fwd_small_cg) snprintf(small, sizeof small, "/s%d", unet::g_wino4_fwd_small_cg);
   const Epilogue& e = a.e;
   const int epi = (e.shuffle_co ? 1 : 0) | (e.stats ? 2 : 0) | (e.yref ? 4 : 0) | (e.colsum1 ? 8 : 0) |
                   (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0) | (e.relu ? 64 : 0);
   // the Winograd caps decide which candidates exist: a choice tuned under other
   // caps is a different key
-  snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d wino=%d/%d tt=%d",
+  snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d wino=%d/%d/%d%s tt=%d",
            a.bl ? "_bf16x3" : a.bh ? "_bf16" : "", a.M,
            a.N, a.K, a.a.Cg, a.a.taps_h, a.a.taps_w, a.a.stride, a.a.Hg, a.a.Wg, epi, unet::g_wino_max,
-           unet::g_wino_dgrad_max, kTileTableVersion);
+           unet::g_wino_dgrad_max, unet::g_wino4_fwd_min_cg, small, kTileTableVersion);
   return b;
 }
 
