@@ -353,10 +353,12 @@ std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
       continue;
     }
     if (t >= 20) {  // halo-tiled: workgroups per CU (2 resident)
-      for (int per_cu : {2, 4, 8}) v.push_back({t, per_cu});
+      for (int per_cu : {1, 2, 4, 8}) v.push_back({t, per_cu});
       continue;
     }
-    for (int per_cu : {4, 8, 16}) v.push_back({t, per_cu});
+    // pixel-split column tiles: fewer splits trade fill for fewer fp32
+    // atomics per output (the short-pixel convT weight gradients)
+    for (int per_cu : {1, 2, 4, 8, 16}) v.push_back({t, per_cu});
   }
   return v;
 }

@@ -1183,13 +1183,19 @@ hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s) {
 //   * V (k_wino4f_w8, layout [Cg/8][36][N][8], 8-float rows pre-swizzled) is
 //     copied row for row: 9 float4 per thread;
 //   * LDS rows are 8 floats; slot s (2 floats) of row r holds channels (q, q+4)
-//     with s = q ^ (2 ((r >> 3) & 1)), so the ds_read_b64 of a 16x16x4 operand
-//     (lane quarter q: k = q in step 0, q + 4 in step 1) hits 64 banks;
+//     with s = q ^ ((r >> 2) & 3) (wf8_slot), so the operand reads of a
+//     16x16x4 MFMA (lane quarter q: k = q in step 0, q + 4 in step 1) are
+//     conflict-free;
 //   * wave w: tile half w & 1, points 9 (w >> 1) .. +8, the four 16-channel
 //     output blocks: per point one U read, four V reads, eight MFMAs;
 //   * the accumulators leave in two 32-channel passes through wf_output.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ int wf8_slot(int row, int q) { return (q ^ (((row >> 3) & 1) << 1)) << 1; }
+// slot of channel pair (q, q + 4) in an 8-float row: XOR by row bits 2-3, so
+// that 16 consecutive rows hit 16 distinct 8-byte bank pairs both mod 64 banks
+// (ds_read_b64) and mod 32 (the ds_read2_b64 / ds_read2st64_b64 the compiler
+// merges two points' reads into; the bit-3-only swizzle was 2-way conflicted
+// there: 3e8 conflict cycles per step, profiles/r03_pmc_summary_fp32.txt)
+__device__ __forceinline__ int wf8_slot(int row, int q) { return (q ^ ((row >> 2) & 3)) << 1; }
 
 __global__ void k_wino4f_w8(const float* __restrict__ b, int N, int Cg, float* __restrict__ v) {
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -1206,7 +1212,7 @@ __global__ void k_wino4f_w8(const float* __restrict__ b, int N, int Cg, float* _
     for (int a = 0; a < 6; ++a) tg[a][k] = r[a];
   }
   const size_t base = (size_t)(c >> 3) * 36 * N;
-  const int pos = wf8_slot(n, c & 3) + ((c >> 2) & 1);  // n & 63 and n agree on bit 3
+  const int pos = wf8_slot(n, c & 3) + ((c >> 2) & 1);  // n & 63 and n agree on bits 2-3
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
     float r[6];
@@ -1352,7 +1358,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
   const int th = wave & 1, cb = wave >> 1;
   const int mi = lane & 15, mq = lane >> 4;
   const int aoff = (16 * th + mi) * 8 + wf8_slot(16 * th + mi, mq);
-  const int boff = (16 * cb + mi) * 8 + wf8_slot(mi, mq);  // rows 16 cb + mi and mi agree on bit 3
+  const int boff = (16 * cb + mi) * 8 + wf8_slot(mi, mq);  // rows 16 cb + mi and mi agree on bits 2-3
   floatx4 acc[36];
 #pragma unroll
   for (int p = 0; p < 36; ++p) acc[p] = (floatx4){0.f, 0.f, 0.f, 0.f};
