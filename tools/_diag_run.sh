@@ -1,12 +1,12 @@
 set -o pipefail
-o=gpurun_out/g9; mkdir -p $o
-timeout -k 10 300 python -u -m pytest -q --timeout 200 --timeout-method thread -p no:cacheprovider "tests/test_gpu_model.py::test_train_step_gemm_variants_vs_oracle[tile73]" "tests/test_gpu_model.py::test_train_step_gemm_variants_vs_oracle[tile72]" > $o/t73.log 2>&1; rc=$?; tail -2 $o/t73.log; [ $rc -le 1 ] || exit $rc
+o=gpurun_out/g12; mkdir -p $o
+P="python -u -m pytest -q --timeout 300 --timeout-method thread -p no:cacheprovider -rA -s"
+T="tests/test_gpu_fullsize.py::test_fp32_512_every_logit_and_gradient_vs_reference_fp64 tests/test_gpu_model.py::test_sgd_trajectory_vs_reference_fixture tests/test_gpu_model.py::test_hela_train_step_real_data tests/test_gpu_fullsize.py::test_c3_572_train_step_vs_reference"
 B="python3 bench.py --retune --extra-dtypes= --no-extras --no-cpu-baseline --no-iou --steps 20 --warmup 5"
-UNET_WINO4_FWD_MIN_CG=0 UNET_TUNE_VERBOSE=1 timeout -k 10 300 $B --tuning-report $o/tun_m0.txt > $o/b_m0.json 2> $o/b_m0.err || exit 4
-UNET_TUNE_VERBOSE=1 timeout -k 10 300 $B --tuning-report $o/tun_def.txt > $o/b_def.json 2> $o/b_def.err || exit 5
-python3 - $o/b_m0.json $o/b_def.json <<'PY'
-import json, sys
-for f in sys.argv[1:]:
-    d = json.loads(open(f).read().strip().splitlines()[-1])
-    print(f, d["value"], d["ms_per_step"], {k: v["ms"] for k, v in d["kernels"].items()})
-PY
+for cfg in "UNET_WINO4_FWD_MIN_CG=128" "UNET_WINO4_FWD_MIN_CG=256 UNET_WINO4_FWD_SMALL_CG=64" "UNET_WINO4_FWD_MIN_CG=0"; do
+  tag=$(echo $cfg | tr ' =' '__')
+  env UNET_TEST_TUNE_DB= $cfg timeout -k 10 400 $P $T > $o/t_$tag.log 2>&1; echo "$cfg tests rc=$?"
+  grep -E "every element|Max relative|AssertionError: \(" $o/t_$tag.log | head -4
+  env $cfg timeout -k 10 300 $B > $o/b_$tag.json 2> $o/b_$tag.err || exit 5
+  python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])" $o/b_$tag.json
+done

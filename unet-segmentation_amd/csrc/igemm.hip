@@ -1092,12 +1092,14 @@ int g_wino_dgrad_max = env_int("UNET_WINO_DGRAD_MAX", 4);  // input gradients (n
 int g_wino_wgrad_max = env_int("UNET_WINO_WGRAD_MAX", 6);
 // "wino4_fwd_min_cg" / UNET_WINO4_FWD_MIN_CG: forward (BN-statistics) GEMMs use
 // F(4x4) only from this many input channels on.  The forward's rounding feeds
-// the BatchNorm statistics and from there every gradient: with F(4x4) on every
-// forward GEMM the 512^2 every-element gradient check landed at 1.00-1.07 % on
-// a deep BatchNorm parameter against its 1 % bar (fp32 direct GEMMs: 0.72 %);
-// from 128 channels on 1.03 %; from 256 on 0.81 % (profiles/r03_wino_fwd_sweep.txt,
-// fp32 bench 301 / 291 / 277 img/s)
-int g_wino4_fwd_min_cg = env_int("UNET_WINO4_FWD_MIN_CG", 256);
+// the BatchNorm statistics and from there every gradient.  With Lavin's points
+// F(4x4) on every forward put the 512^2 every-element gradient check at
+// 1.00-1.07 % of its 1 % bar (direct GEMMs: 0.72 %), >= 128 channels 1.03 %,
+// >= 256 0.81 %.  With the better-conditioned points (winograd.hip, round 3):
+// every forward 0.97-0.98 (and the 3-step SGD trajectory at 1.02 % in one of two
+// tunings), >= 128 channels 0.85 -- the default (profiles/r03_wino_fwd_sweep.txt;
+// fp32 bench 301 / 292 / 278 img/s for 0 / 128 / 256)
+int g_wino4_fwd_min_cg = env_int("UNET_WINO4_FWD_MIN_CG", 128);
 // ... and also up to this many ("wino4_fwd_small_cg" / UNET_WINO4_FWD_SMALL_CG)
 int g_wino4_fwd_small_cg = env_int("UNET_WINO4_FWD_SMALL_CG", 0);
 static int wino_tile_m(int tile) {

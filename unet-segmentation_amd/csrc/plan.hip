@@ -344,8 +344,10 @@ std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 24, 25, 71, 74}) {  // fits() filters by precision
     if (!wgrad_tile_fits(a, t) || tune_skipped(t)) continue;
     if (t == 71 || t == 74) {  // Winograd: point-GEMM tile (k_wgrad 0-4) x workgroups per CU
+      // (each pixel split adds a full points x Co x Ci slab by fp32 atomics:
+      // 1-2 per CU cut that traffic on the deep, few-tile layers)
       for (int inner : {0, 1, 2, 3, 4})
-        for (int per_cu : {4, 8, 16}) v.push_back({t, per_cu + 100 * (inner + 1)});
+        for (int per_cu : {1, 2, 4, 8, 16}) v.push_back({t, per_cu + 100 * (inner + 1)});
       continue;
     }
     if (t == 24 || t == 25) {  // wide halo-tiled: one resident workgroup per CU

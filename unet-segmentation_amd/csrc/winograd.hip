@@ -211,35 +211,43 @@ __global__ __launch_bounds__(256) void k_wino_out(const float* __restrict__ m, l
 // ---------------------------------------------------------------------------
 // F(4x4, 3x3) (tile 71): 6x6 input patches, 36 points, 4x4 outputs -- 4x fewer
 // MACs than direct and 2.25 points per output pixel instead of 4 (less
-// transform traffic).  Interpolation points 0, +-1, +-2, inf (Lavin & Gray):
-//   B^T = [4 0 -5 0 1 0; 0 -4 -4 1 1 0; 0 4 -4 -1 1 0; 0 -2 -1 2 1 0;
-//          0 2 -1 -2 1 0; 0 4 0 -5 0 1]
-//   G   = [1/4 0 0; -1/6 -1/6 -1/6; -1/6 1/6 -1/6; 1/24 1/12 1/6;
-//          1/24 -1/12 1/6; 0 0 1]
-//   A^T = [1 1 1 1 1 0; 0 1 -1 2 -2 0; 0 1 1 4 4 0; 0 1 -1 8 -8 1]
-// One channel per thread (36 values in registers), coalesced across channels.
+// transform traffic).  Interpolation points 0, 1, -1, 2, -1/2, inf (Toom-Cook,
+// G carrying the Lagrange denominators).  Against Lavin & Gray's 0, +-1, +-2,
+// inf the fp32 output error is ~1.6x smaller (NumPy emulation, post-ReLU
+// inputs, 64-256 channels: 6.3e-7 vs 1.06e-6 ... 1.9e-6 vs 3.1e-6 rel-RMS):
+// that rounding reaches every gradient through the BatchNorm statistics of the
+// forward GEMMs.
+//   B^T = [1 3/2 -2 -3/2 1 0; 0 -1 -5/2 -1/2 1 0; 0 1 1/2 -5/2 1 0;
+//          0 -1/2 -1 1/2 1 0; 0 2 -1 -2 1 0; 0 1 3/2 -2 -3/2 1]
+//   G   = [1 0 0; -1/3 -1/3 -1/3; 1/3 -1/3 1/3; 1/15 2/15 4/15;
+//          -16/15 8/15 -4/15; 0 0 1]
+//   A^T = [1 1 1 1 1 0; 0 1 -1 2 -1/2 0; 0 1 1 4 1/4 0; 0 1 -1 8 -1/8 1]
+// (every coefficient but 1/3 and 1/15 is exact in fp32).  One channel per
+// thread (36 values in registers), coalesced across channels.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void bt6(const float (&d)[6], float (&r)[6]) {
-  r[0] = 4.f * d[0] - 5.f * d[2] + d[4];
-  r[1] = -4.f * d[1] - 4.f * d[2] + d[3] + d[4];
-  r[2] = 4.f * d[1] - 4.f * d[2] - d[3] + d[4];
-  r[3] = -2.f * d[1] - d[2] + 2.f * d[3] + d[4];
-  r[4] = 2.f * d[1] - d[2] - 2.f * d[3] + d[4];
-  r[5] = 4.f * d[1] - 5.f * d[3] + d[5];
+template <class T>
+__device__ __forceinline__ void bt6v(const T (&d)[6], T (&r)[6]) {
+  r[0] = d[0] + 1.5f * (d[1] - d[3]) - 2.f * d[2] + d[4];
+  r[1] = d[4] - d[1] - 2.5f * d[2] - 0.5f * d[3];
+  r[2] = d[1] + 0.5f * d[2] - 2.5f * d[3] + d[4];
+  r[3] = 0.5f * (d[3] - d[1]) - d[2] + d[4];
+  r[4] = 2.f * (d[1] - d[3]) - d[2] + d[4];
+  r[5] = d[1] + 1.5f * (d[2] - d[4]) - 2.f * d[3] + d[5];
 }
+__device__ __forceinline__ void bt6(const float (&d)[6], float (&r)[6]) { bt6v(d, r); }
 __device__ __forceinline__ void g6(const float (&g)[3], float (&r)[6]) {
-  r[0] = 0.25f * g[0];
-  r[1] = -(g[0] + g[1] + g[2]) * (1.f / 6.f);
-  r[2] = -(g[0] - g[1] + g[2]) * (1.f / 6.f);
-  r[3] = g[0] * (1.f / 24.f) + g[1] * (1.f / 12.f) + g[2] * (1.f / 6.f);
-  r[4] = g[0] * (1.f / 24.f) - g[1] * (1.f / 12.f) + g[2] * (1.f / 6.f);
+  r[0] = g[0];
+  r[1] = -(g[0] + g[1] + g[2]) * (1.f / 3.f);
+  r[2] = (g[0] - g[1] + g[2]) * (1.f / 3.f);
+  r[3] = (g[0] + 2.f * g[1] + 4.f * g[2]) * (1.f / 15.f);
+  r[4] = (8.f * g[1] - 16.f * g[0] - 4.f * g[2]) * (1.f / 15.f);
   r[5] = g[2];
 }
 __device__ __forceinline__ void at4(const float (&m)[6], float (&o)[4]) {
   o[0] = m[0] + m[1] + m[2] + m[3] + m[4];
-  o[1] = m[1] - m[2] + 2.f * (m[3] - m[4]);
-  o[2] = m[1] + m[2] + 4.f * (m[3] + m[4]);
-  o[3] = m[1] - m[2] + 8.f * (m[3] - m[4]) + m[5];
+  o[1] = m[1] - m[2] + 2.f * m[3] - 0.5f * m[4];
+  o[2] = m[1] + m[2] + 4.f * m[3] + 0.25f * m[4];
+  o[3] = m[1] - m[2] + 8.f * m[3] - 0.125f * m[4] + m[5];
 }
 
 __global__ void k_wino4_w(const float* __restrict__ b, int N, int Cg, float* __restrict__ v) {
@@ -316,26 +324,18 @@ __global__ __launch_bounds__(256) void k_wino4_in(Gather g, int Th, int Tw, long
     vec d[6];
 #pragma unroll
     for (int yy = 0; yy < 6; ++yy) d[yy] = (yy < vr && xx < vc) ? raw[yy][xx] : (vec)0.f;
-    e[0][xx] = 4.f * d[0] - 5.f * d[2] + d[4];
-    e[1][xx] = -4.f * (d[1] + d[2]) + d[3] + d[4];
-    e[2][xx] = 4.f * (d[1] - d[2]) - d[3] + d[4];
-    e[3][xx] = 2.f * (d[3] - d[1]) - d[2] + d[4];
-    e[4][xx] = 2.f * (d[1] - d[3]) - d[2] + d[4];
-    e[5][xx] = 4.f * d[1] - 5.f * d[3] + d[5];
+    vec r[6];
+    bt6v(d, r);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) e[a][xx] = r[a];
   }
   const size_t plane = (size_t)T * g.Cg, o = (size_t)t * g.Cg + c;
   char* ub = reinterpret_cast<char*>(u + o);
   const unsigned pbytes = (unsigned)(plane * 4);
 #pragma unroll
   for (int a = 0; a < 6; ++a) {
-    const vec* d = e[a];
     vec rr[6];
-    rr[0] = 4.f * d[0] - 5.f * d[2] + d[4];
-    rr[1] = -4.f * (d[1] + d[2]) + d[3] + d[4];
-    rr[2] = 4.f * (d[1] - d[2]) - d[3] + d[4];
-    rr[3] = 2.f * (d[3] - d[1]) - d[2] + d[4];
-    rr[4] = 2.f * (d[1] - d[3]) - d[2] + d[4];
-    rr[5] = 4.f * d[1] - 5.f * d[3] + d[5];
+    bt6v(e[a], rr);
 #pragma unroll
     for (int bb = 0; bb < 6; ++bb) *reinterpret_cast<vec*>(ub + (unsigned)(a * 6 + bb) * pbytes) = rr[bb];
   }
@@ -1521,18 +1521,18 @@ hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s) {
 // instead of 9.  U is the forward's input transform (same gather, BN + ReLU on
 // load), Vd the dY transform below, dW[co][tap][ci] = G^T Mw[co][ci] G.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ void a6(const float (&y)[4], float (&r)[6]) {
+__device__ __forceinline__ void a6(const float (&y)[4], float (&r)[6]) {  // A = (A^T)^T
   r[0] = y[0];
   r[1] = y[0] + y[1] + y[2] + y[3];
   r[2] = y[0] - y[1] + y[2] - y[3];
   r[3] = y[0] + 2.f * y[1] + 4.f * y[2] + 8.f * y[3];
-  r[4] = y[0] - 2.f * y[1] + 4.f * y[2] - 8.f * y[3];
+  r[4] = y[0] - 0.5f * y[1] + 0.25f * y[2] - 0.125f * y[3];
   r[5] = y[3];
 }
-__device__ __forceinline__ void gt3(const float (&m)[6], float (&r)[3]) {
-  r[0] = 0.25f * m[0] - (m[1] + m[2]) * (1.f / 6.f) + (m[3] + m[4]) * (1.f / 24.f);
-  r[1] = (m[2] - m[1]) * (1.f / 6.f) + (m[3] - m[4]) * (1.f / 12.f);
-  r[2] = (m[3] + m[4] - m[1] - m[2]) * (1.f / 6.f) + m[5];
+__device__ __forceinline__ void gt3(const float (&m)[6], float (&r)[3]) {  // G^T
+  r[0] = m[0] + (m[2] - m[1]) * (1.f / 3.f) + (m[3] - 16.f * m[4]) * (1.f / 15.f);
+  r[1] = -(m[1] + m[2]) * (1.f / 3.f) + (2.f * m[3] + 8.f * m[4]) * (1.f / 15.f);
+  r[2] = (m[2] - m[1]) * (1.f / 3.f) + (4.f * m[3] - 4.f * m[4]) * (1.f / 15.f) + m[5];
 }
 
 // Vd[p][t][co], one (tile, channel) per thread; dY outside the Hg x Wg grid is 0
