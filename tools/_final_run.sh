@@ -1,5 +1,5 @@
 set -o pipefail
-o=gpurun_out/f1; mkdir -p $o
+o=gpurun_out/f2; mkdir -p $o
 timeout -k 10 480 python bench.py --steps 20 --warmup 5 --retune --tune-db-out profiles/tune_db.txt --tuning-report $o/tuning.txt > $o/bench.json 2> $o/bench.err || { echo bench rc=$?; tail -5 $o/bench.err; exit 3; }
 cp profiles/tune_db.txt $o/tune_db.txt
 timeout -k 10 660 python -u -m pytest tests -m gpu -q --timeout 300 --timeout-method thread -p no:cacheprovider -rf > $o/gpu_tests.log 2>&1; echo tests rc=$?
