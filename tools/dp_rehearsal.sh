@@ -1,5 +1,6 @@
+#!/bin/bash
 set -o pipefail
-o=gpurun_out/dp; mkdir -p $o
+o=${1:-gpurun_out/dp}; mkdir -p $o
 # 2-rank rehearsal of the DP bench path on the box's one GPU (gloo stages CUDA
 # tensors through the host; timings say nothing about RCCL over xGMI)
 timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 \
