@@ -385,7 +385,7 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "force_tile") g_force_tile = value;
   else if (k == "concurrent") g_concurrent = value;
   else if (k == "wino_max") g_wino_max = value;
-  else if (k == "bf16_norm") g_bf16_norm = value != 0;
+  else if (k == "bf16_norm") g_bf16_norm = value;
   else if (k == "bn_fold") g_bn_fold = value != 0;
   else if (k == "wino_dgrad_max") g_wino_dgrad_max = value;
   else if (k == "wino_wgrad_max") g_wino_wgrad_max = value;

@@ -34,7 +34,10 @@ int g_autotune = getenv("UNET_AUTOTUNE") ? atoi(getenv("UNET_AUTOTUNE")) : 1;
 int g_concurrent = getenv("UNET_CONCURRENT") ? atoi(getenv("UNET_CONCURRENT")) : 1;
 // unet_set_tuning("bf16_norm", v) or UNET_BF16_NORM (default off): bf16 plans
 // materialise relu(bn(y)) once per element (the normalised copy every GEMM
-// consumer stages as a plain operand); off: consumers transform on load.
+// consumer stages as a plain operand); 2: only the encoder outputs, whose copy
+// the max-pool writes while it reads them anyway (no extra pass: the skip
+// operand of the up blocks' first convs and their weight gradients becomes a
+// plain LDS-DMA-able copy); off: consumers transform on load.
 // Read at plan creation (workspace layout).
 int g_bf16_norm = getenv("UNET_BF16_NORM") ? atoi(getenv("UNET_BF16_NORM")) : 0;
 // unet_set_tuning("bn_fold", v) or UNET_BN_FOLD (default on): eval forwards
@@ -1180,7 +1183,8 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     L.scale = al.take(fsz(L.co));
     L.shift = al.take(fsz(L.co));
     L.coef = al.take(fsz(4LL * L.co));
-    if (prec == UNET_PREC_BF16 && unet::g_bf16_norm && l < 17)
+    if (prec == UNET_PREC_BF16 &&
+        ((unet::g_bf16_norm == 1 && l < 17) || (unet::g_bf16_norm == 2 && l <= 7 && l % 2 == 1)))
       L.a = al.take((size_t)pix * L.co * 2);  // head reads y17 itself
   }
   for (int k = 0; k < 4; ++k) {
