@@ -57,7 +57,14 @@ static void test_plans() {
           unet_plan_destroy(p);
         }
   CHECK(unet_plan_create(1, 1, 100, 100, 2) == nullptr);  // too small
-  CHECK(unet_plan_create(1, 5, 512, 512, 2) == nullptr);  // c_in > 4
+  CHECK(unet_plan_create(1, 17, 512, 512, 2) == nullptr);  // c_in > 16
+  CHECK(unet_plan_create(1, 1, 512, 512, 33) == nullptr);  // n_classes > 32
+  if (unet_plan* q = unet_plan_create(1, 5, 188, 188, 5)) {  // 5 channels / 5 classes take a plan
+    CHECK(unet_plan_num_params(q) == 136);
+    unet_plan_destroy(q);
+  } else {
+    CHECK(false);
+  }
   CHECK(unet_plan_create_ex(1, 1, 512, 512, 2, 7) == nullptr);
   CHECK(unet_plan_forward(nullptr, nullptr, nullptr, nullptr, nullptr, 1, nullptr) != 0);
   CHECK(unet_plan_backward(nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, 9, nullptr) != 0);
