@@ -29,6 +29,9 @@ def bench_tuning():
     n = lib.unet_tuning_load(db.encode()) if db and os.path.exists(db) else 0
     print(f"tuning database: {n} entries ({_lib.build_identity()})")
     yield n
+    # GEMM shapes these tests met that the database did not hold (tuned live)
+    live = [ln.split(" | ")[0] for ln in _lib.tuning_report().splitlines() if ln and "tuning db" not in ln]
+    print(f"\ntuning database misses (shapes tuned live): {len(live)}" + "".join(f"\n  {k}" for k in live))
     lib.unet_tuning_reset()
 
 

@@ -4,8 +4,10 @@ backward, the bucketed asynchronous all-reduce and the 1/world SGD scale --
 on this rank's shard.  Ranks share the one GPU of the test box and talk over
 gloo (RCCL needs one GPU per rank; the all-reduce call pattern is the same).
 
-    python tests/dp_worker.py <out.npz> <overlap 0|1> <steps> [comm dtype fp32|bf16]
-    env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT
+    python tests/dp_worker.py <out.npz> <overlap 0|1> <steps> [comm fp32|bf16] [precision fp32|bf16]
+                              [batch] [size]
+    env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT;
+         UNET_DP_TUNE_DB=<path>: replay that GEMM tuning database (the bench's)
 """
 import os
 import sys
@@ -25,26 +27,33 @@ from oracle import unet_oracle as O  # noqa: E402
 SEED, BATCH, SIZE = 51, 2, 188
 
 
-def shard(rank):
-    return F.make_inputs(100 + rank, BATCH, 1, SIZE)
+def shard(rank, batch=BATCH, size=SIZE):
+    return F.make_inputs(100 + rank, batch, 1, size)
 
 
 def main():
     out, overlap, steps = sys.argv[1], bool(int(sys.argv[2])), int(sys.argv[3])
     comm = {"fp32": torch.float32, "bf16": torch.bfloat16}[sys.argv[4] if len(sys.argv) > 4 else "fp32"]
+    precision = sys.argv[5] if len(sys.argv) > 5 else "fp32"
+    batch = int(sys.argv[6]) if len(sys.argv) > 6 else BATCH
+    size = int(sys.argv[7]) if len(sys.argv) > 7 else SIZE
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
     dist.init_process_group("gloo")
-    from unet_amd import UNet
+    from unet_amd import UNet, _lib
     from unet_amd.train import Trainer
+    db = os.environ.get("UNET_DP_TUNE_DB")
+    if db:
+        n = _lib.load().unet_tuning_load(db.encode())
+        assert n > 0, (db, n)
     params = O.hash_init(1, 2, seed=SEED, bn_random=True)
     m = UNet(1, 2)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     m = m.cuda().train()
-    tr = Trainer(m, BATCH, SIZE, SIZE, lr=1e-4, momentum=0.99, process_group=dist.group.WORLD, overlap=overlap,
-                 comm_dtype=comm)
+    tr = Trainer(m, batch, size, size, lr=1e-4, momentum=0.99, process_group=dist.group.WORLD, overlap=overlap,
+                 comm_dtype=comm, precision=precision)
     tr.defer_join = os.environ.get("UNET_DP_DEFER", "1") != "0"
-    x, t, w = (torch.from_numpy(a).cuda() for a in shard(rank))
+    x, t, w = (torch.from_numpy(a).cuda() for a in shard(rank, batch, size))
     res = {}
     for s in range(steps):
         res[f"w{s}"] = tr.flat.flat.cpu().numpy().copy()         # weights this step starts from
@@ -59,6 +68,9 @@ def main():
     res["buffers_before_sync"] = np.concatenate([b.double().cpu().numpy().ravel() for b in m.buffers()])
     tr.sync_buffers()
     res["buffers"] = np.concatenate([b.double().cpu().numpy().ravel() for b in m.buffers()])
+    if db:
+        rep = _lib.tuning_report()
+        res["tune_live"] = np.array(sum(1 for ln in rep.splitlines() if ln and "tuning db" not in ln))
     np.savez(out, **res)
     dist.barrier()
     dist.destroy_process_group()

@@ -391,24 +391,23 @@ def op_cases():
     print("wrote", path, os.path.getsize(path), "bytes")
 
 
-def real_data_case(n_frames=3):
-    """Real HeLa frames (data/raw/train/DIC-C2DH-HeLa/01, 01_ST/SEG) through the
-    reference model with hash weights: masks + IoU (utils/metrics.py:6-37)."""
+HELA_GOLD = (2, 5, 21, 31, 33, 34, 39, 54, 67)  # the gold-truth frames of 01_GT/SEG
+
+
+def _hela_frames(root, ids, seg_dir):
     from PIL import Image
-    root = os.path.join(REF, "data/raw/train/DIC-C2DH-HeLa")
-    params = O.hash_init(1, 2, seed=7, bn_random=True)
-    m = ref_model(params)
-    # put plausible running stats in place: one train-mode pass over the frames
-    imgs, segs = [], []
-    for i in range(n_frames):
-        imgs.append(np.array(Image.open(os.path.join(root, "01", f"t{i:03d}.tif")).convert("L")))
-        segs.append(np.array(Image.open(os.path.join(root, "01_ST", "SEG", f"man_seg{i:03d}.tif"))))
-    imgs = np.stack(imgs)
-    segs = np.stack(segs)
-    x = imgs.astype(np.float64)[:, None] / 255.0            # ToTensor (dataset.py:96)
-    xn = x * 2.0 - 1.0                                       # Normalize(0.5,0.5) (predict.py:50-54)
-    # running stats := batch stats of these frames (momentum 1.0), so that the
-    # eval-mode masks are not degenerate for hash-initialised weights
+    imgs = np.stack([np.array(Image.open(os.path.join(root, "01", f"t{i:03d}.tif")).convert("L")) for i in ids])
+    segs = np.stack([np.array(Image.open(os.path.join(root, seg_dir, "SEG", f"man_seg{i:03d}.tif"))) for i in ids])
+    return imgs, segs
+
+
+def _hela_eval_model(root, n_frames=3):
+    """The reference model of real_data_case: hash weights (seed 7), running
+    statistics := the batch statistics of the first n_frames 01 frames
+    (momentum 1.0, one train-mode pass), then eval mode."""
+    m = ref_model(O.hash_init(1, 2, seed=7, bn_random=True))
+    imgs, _ = _hela_frames(root, range(n_frames), "01_ST")
+    xn = imgs.astype(np.float64)[:, None] / 255.0 * 2.0 - 1.0
     for mod in m.modules():
         if isinstance(mod, torch.nn.BatchNorm2d):
             mod.momentum = 1.0
@@ -416,6 +415,19 @@ def real_data_case(n_frames=3):
     with torch.no_grad():
         m(_t(xn))
     m.eval()
+    return m
+
+
+def real_data_case(n_frames=3):
+    """Real HeLa frames (data/raw/train/DIC-C2DH-HeLa/01, 01_ST/SEG) through the
+    reference model with hash weights: masks + IoU (utils/metrics.py:6-37)."""
+    root = os.path.join(REF, "data/raw/train/DIC-C2DH-HeLa")
+    # running stats := batch stats of these frames (momentum 1.0), so that the
+    # eval-mode masks are not degenerate for hash-initialised weights
+    m = _hela_eval_model(root, n_frames)
+    imgs, segs = _hela_frames(root, range(n_frames), "01_ST")
+    x = imgs.astype(np.float64)[:, None] / 255.0            # ToTensor (dataset.py:96)
+    xn = x * 2.0 - 1.0                                       # Normalize(0.5,0.5) (predict.py:50-54)
     with torch.no_grad():
         logits = m(_t(xn)).numpy()
     masks = O.predict_mask(logits)
@@ -429,6 +441,31 @@ def real_data_case(n_frames=3):
     path = os.path.join(HERE, "hela_real.npz")
     np.savez_compressed(path, **out)
     print("wrote", path, os.path.getsize(path), "bytes", "IoUs", ious)
+
+
+def gold_data_case():
+    """The nine gold-truth frames of DIC-C2DH-HeLa 01 (01_GT/SEG man_seg002 ...
+    067) through real_data_case's eval model (same weights, same running
+    statistics): masks, margins and IoU against the GOLD segmentations
+    (utils/metrics.py:6-37, predict.py's Normalize(0.5, 0.5)).  Masks, margins
+    and segmentation foregrounds are bit-packed."""
+    root = os.path.join(REF, "data/raw/train/DIC-C2DH-HeLa")
+    m = _hela_eval_model(root)
+    imgs, segs = _hela_frames(root, HELA_GOLD, "01_GT")
+    xn = imgs.astype(np.float64)[:, None] / 255.0 * 2.0 - 1.0
+    with torch.no_grad():
+        logits = m(_t(xn)).numpy()
+    masks = O.predict_mask(logits)
+    oy = (512 - 324) // 2
+    gt = segs[:, oy:oy + 324, oy:oy + 324]
+    ious = np.array([O.calculate_iou(masks[i], gt[i]) for i in range(len(HELA_GOLD))])
+    margin = np.abs(logits[:, 1] - logits[:, 0])
+    out = {"frames": np.array(HELA_GOLD), "images": imgs.astype(np.uint8),
+           "seg_fg": np.packbits(segs > 0, axis=-1), "masks": np.packbits(masks.astype(bool), axis=-1),
+           "sure": np.packbits(margin > 1e-3, axis=-1), "ious": ious, "seed": np.array(7)}
+    path = os.path.join(HERE, "hela_gold.npz")
+    np.savez_compressed(path, **out)
+    print("wrote", path, os.path.getsize(path), "bytes", "IoUs", ious, "low-margin pixels", int((margin <= 1e-3).sum()))
 
 
 if __name__ == "__main__":
@@ -445,6 +482,8 @@ if __name__ == "__main__":
         forward_only_case("n1_c3_572", 1, 572, n_channels=3, seed=4)
     if "hela" in which:
         real_data_case()
+    if "gold" in which:  # the 9 gold-truth frames (01_GT/SEG) for the IoU check
+        gold_data_case()
     if "t512" in which:
         full_size_train_case("n2_512", 2, 512, seed=5)
     if "t512b8" in which:  # the bench configuration (configs[1]): batch 8 x 512^2

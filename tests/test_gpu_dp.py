@@ -32,23 +32,29 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def run_ranks(tmp_path, overlap, world=2, comm="fp32"):
+def run_ranks(tmp_path, overlap, world=2, comm="fp32", precision="fp32", batch=W.BATCH, size=W.SIZE, steps=STEPS,
+              tune_db=None):
     port = _free_port()
     procs, outs = [], []
     for r in range(world):
-        # fixed GEMM variants (no autotuning) in every process: the comparison is
-        # then between identical kernels, not between timing-dependent tile
-        # choices whose different roundings small-sample BatchNorm amplifies
+        # fixed GEMM variants in every process: no autotuning (small sizes), or
+        # the bench's tuning database (tune_db, at size); the comparison is then
+        # between identical kernels, not between timing-dependent tile choices
+        # whose different roundings small-sample BatchNorm amplifies
         env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r), MASTER_ADDR="127.0.0.1",
-                   MASTER_PORT=str(port), UNET_AUTOTUNE="0")
+                   MASTER_PORT=str(port))
+        if tune_db:
+            env["UNET_DP_TUNE_DB"] = tune_db
+        else:
+            env["UNET_AUTOTUNE"] = "0"
         out = str(tmp_path / f"rank{r}.npz")
         outs.append(out)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "dp_worker.py"), out, str(int(overlap)),
-                                       str(STEPS), comm], env=env))
+                                       str(steps), comm, precision, str(batch), str(size)], env=env))
     rcs = []
     for p in procs:
         try:
-            rcs.append(p.wait(timeout=240))
+            rcs.append(p.wait(timeout=400))
         except subprocess.TimeoutExpired:
             for q in procs:
                 q.kill()
@@ -57,7 +63,7 @@ def run_ranks(tmp_path, overlap, world=2, comm="fp32"):
     return [np.load(o) for o in outs]
 
 
-def single_process_reference(weights, world=2):
+def single_process_reference(weights, world=2, **kw):
     """Per-shard GPU gradients without a process group, summed on the host, at
     the weights each rank step started from (``weights[s]``): every step is
     then compared from identical weights.  (Chaining the reference's own SGD
@@ -66,22 +72,30 @@ def single_process_reference(weights, world=2):
     step: tools/dp_diag.py measures 1e-4..1e-2 rel between two runs of one
     single-process reference.)"""
     from unet_amd import _lib
-    _lib.load().unet_set_tuning(b"autotune", 0)
+    lib = _lib.load()
+    db = kw.pop("tune_db", None)
+    if db:
+        lib.unet_tuning_reset()
+        assert lib.unet_tuning_load(db.encode()) > 0
+    else:
+        lib.unet_set_tuning(b"autotune", 0)
     try:
-        return _single_process_reference(weights, world)
+        return _single_process_reference(weights, world, **kw)
     finally:
-        _lib.load().unet_set_tuning(b"autotune", 1)
+        lib.unet_set_tuning(b"autotune", 1)
+        if db:
+            lib.unet_tuning_reset()
 
 
-def _single_process_reference(weights, world):
+def _single_process_reference(weights, world, precision="fp32", batch=W.BATCH, size=W.SIZE):
     from unet_amd import UNet
     from unet_amd.train import Trainer
     params = O.hash_init(1, 2, seed=W.SEED, bn_random=True)
     m = UNet(1, 2)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     m = m.cuda().train()
-    tr = Trainer(m, W.BATCH, W.SIZE, W.SIZE, lr=1e-4, momentum=0.99)
-    shards = [tuple(torch.from_numpy(a).cuda() for a in W.shard(r)) for r in range(world)]
+    tr = Trainer(m, batch, size, size, lr=1e-4, momentum=0.99, precision=precision)
+    shards = [tuple(torch.from_numpy(a).cuda() for a in W.shard(r, batch, size)) for r in range(world)]
     sums = []
     for w in weights:
         tr.flat.flat.copy_(torch.from_numpy(w).cuda())
@@ -145,3 +159,50 @@ def test_two_rank_trainer_bf16_gradient_allreduce(tmp_path):
     rel = np.linalg.norm(g - ref) / np.linalg.norm(ref)
     assert rel <= 2.0 ** -7, rel
     assert rel > 0  # the wire really was bf16
+
+
+def test_two_rank_trainer_bf16_plans_at_size(tmp_path):
+    """configs[2]'s per-rank composition: bf16 GEMM plans under a process group
+    at the per-GPU batch of 8 x 512^2 (scripts/train.py:114-131 per rank; the
+    bench's tuned kernel mix from profiles/tune_db.txt in every process), fp32
+    wire, segmented backward with the bucketed overlap, 2 steps.  Both ranks end
+    with identical gradients and weights; each step's all-reduced gradient is
+    the host sum of the two shards' bf16 gradients computed by one process
+    without a group at the same weights, per tensor within the bf16 bar of
+    test_gpu_fullsize.py (rel-L2 <= 1 %, BatchNorm parameters 2 %) or 3 x the
+    run-to-run spread of that reference itself (fp32 atomic order moving bf16
+    roundings), whichever is larger; the update is SGD(0.99) with 1/world."""
+    db = os.path.join(os.path.dirname(HERE), "profiles", "tune_db.txt")
+    kw = dict(precision="bf16", batch=8, size=512)
+    ranks = run_ranks(tmp_path, True, steps=2, tune_db=db, **kw)
+    for s in range(2):
+        np.testing.assert_array_equal(ranks[0][f"grad{s}"], ranks[1][f"grad{s}"])
+        np.testing.assert_array_equal(ranks[0][f"w{s}"], ranks[1][f"w{s}"])
+    np.testing.assert_array_equal(ranks[0]["params"], ranks[1]["params"])
+    print("GEMM shapes tuned live per rank (not in the tuning database):", [int(r["tune_live"]) for r in ranks])
+    ws = [ranks[0]["w0"], ranks[0]["w1"], ranks[0]["w0"]]
+    sums = single_process_reference(ws, tune_db=db, **kw)
+    from unet_amd import UNet
+    m = UNet(1, 2)
+    names = [k for k, _ in m.named_parameters()]
+    offs, o = [], 0
+    for _, p in m.named_parameters():
+        offs.append((o, o + p.numel()))
+        o += (p.numel() + 3) // 4 * 4
+    worst = 0.0
+    for s in range(2):
+        g, ref = ranks[0][f"grad{s}"], sums[s]
+        for name, (a, b) in zip(names, offs):
+            if O.bn_cancelled(name):
+                continue
+            nr = max(np.linalg.norm(ref[a:b]), 1e-30)
+            e = np.linalg.norm(g[a:b] - ref[a:b]) / nr
+            spread = np.linalg.norm(sums[2][a:b] - sums[0][a:b]) / nr   # reference run to run, step-0 weights
+            tol = max(2e-2 if O.is_bn_param(name) else 1e-2, 3 * spread)
+            worst = max(worst, e / tol)
+            assert e <= tol, (s, name, e, spread)
+    p = ranks[0]["params"]
+    want = sgd_replay(ranks[0]["w0"], [ranks[0]["grad0"], ranks[0]["grad1"]], 2)
+    assert np.abs(p - want).max() <= 1e-6 * np.abs(want).max()
+    print(f"bf16 DP 2 x 8 x 512^2: worst per-tensor gradient rel-L2 / tol {worst:.2f}, "
+          f"losses {float(ranks[0]['loss0']):.5f} / {float(ranks[1]['loss0']):.5f}")

@@ -108,8 +108,15 @@ def check_bf16_vs_reference(z, zb, lg, loss, grads, tag, zf=None):
     # move rare operands across a bf16 rounding boundary, nothing more
     agree_bf = float(((lg[:, 1] > lg[:, 0]) == bf_mask).mean())
     assert agree_bf >= 0.995, (tag, agree_bf)
+    # element level against the bf16 oracle (same roundings, fp64 sums): the
+    # logit sample within 3 x the rounding-boundary noise of the same oracle in
+    # fp32 sums (zf), and the 32 sampled entries of every gradient (below)
     lt = np.abs(lg[:, :, ::7, ::5] - zb["logits_sample"]).max()
+    if zf is not None:
+        lflip = float(np.abs(zf["logits_sample"] - zb["logits_sample"]).max())
+        assert lt <= 3 * lflip, (tag, lt, lflip)
     worst = worst_b = 0.0
+    ratios, worst_s = [], (0.0, "")
     for name, g in grads.items():
         r = float(z[f"gnorm/{name}"])
         if O.bn_cancelled(name):
@@ -136,6 +143,28 @@ def check_bf16_vs_reference(z, zb, lg, loss, grads, tag, zf=None):
         tb = max(3e-2 * rb, 3 * floor, noise)
         worst_b = max(worst_b, eb / tb)
         assert eb <= tb, (tag, name, np.linalg.norm(g), rb)
+        if zf is not None and f"gbf16val/{name}" in zb.files:
+            # sampled entries (indices of the fp64 fixture) vs the bf16 oracle: a
+            # bf16 rounding flip moves a BatchNorm channel's backward
+            # coefficients and with them every entry of the channel coherently,
+            # so single entries carry 10-80 % (median 27 %) rel-L2 of that noise
+            # (zf vs zb); the GPU's sample is one more draw of it: within 3 x the
+            # tensor's own noise (at least 5 %), and never above 1.2 -- a
+            # sign-flipped (~2) or permuted / uncorrelated (~1.4) slice fails
+            idx = z[f"gidx/{name}"]
+            vb, vf = zb[f"gbf16val/{name}"], zf[f"gbf16val/{name}"]
+            nb = max(np.linalg.norm(vb), 1e-30)
+            es, fs = np.linalg.norm(g.ravel()[idx] - vb) / nb, np.linalg.norm(vf - vb) / nb
+            ratios.append(es / max(fs, 0.05))
+            if es / min(1.2, max(3 * fs, 0.05)) > worst_s[0]:
+                worst_s = (es / min(1.2, max(3 * fs, 0.05)), name)
+            assert es <= min(1.2, max(3 * fs, 0.05)), (tag, name, es, fs)
+    if ratios:
+        # statistically the GPU is one more draw of the oracle's own boundary
+        # noise: its typical sample error sits at ~1x that noise, not above 2x
+        assert float(np.median(ratios)) <= 2.0, (tag, float(np.median(ratios)))
+        print(f"{tag}: sampled gradient entries vs bf16 oracle: median err / own noise {np.median(ratios):.2f}, "
+              f"worst err / bar {worst_s[0]:.2f} ({worst_s[1]})")
     print(f"{tag}: loss rel {lo:.2e} (bf16 oracle {abs(bf_loss - ref_loss) / abs(ref_loss):.2e}), "
           f"mask agreement {agree:.5f} (bf16 oracle {bf_agree:.5f}; vs bf16 oracle {agree_bf:.5f}), "
           f"logits vs bf16 oracle max {lt:.3f}, worst grad-norm err / tol {worst:.2f} (vs bf16 oracle {worst_b:.2f})")

@@ -227,6 +227,27 @@ def test_hela_real_frames_iou_vs_reference():
     np.testing.assert_allclose(ious, z["ious"], rtol=0, atol=1e-12)
 
 
+def test_hela_gold_frames_vs_reference():
+    """hela_gold.npz (the nine 01_GT/SEG frames through the reference's eval
+    model): the oracle reproduces the reference's masks and IoUs on two of them
+    (t002, t067; the GPU test checks all nine), with hela_real's running
+    statistics (pinned above)."""
+    zr, z = _load("hela_real.npz"), _load("hela_gold.npz")
+    params = O.hash_init(1, 2, seed=int(z["seed"]), bn_random=True)
+    for k in zr.files:
+        if k.startswith("buf/"):
+            params[k[4:]] = zr[k]
+    pick = [0, len(z["frames"]) - 1]
+    x = z["images"][pick].astype(np.float64)[:, None] / 255.0 * 2.0 - 1.0
+    logits, _, _ = O.UNetOracle(params).forward(x, train=False)
+    masks = O.predict_mask(logits)
+    ref = np.unpackbits(z["masks"][pick], axis=-1)[..., :324]
+    np.testing.assert_array_equal(masks > 0, ref > 0)
+    gt = np.unpackbits(z["seg_fg"][pick], axis=-1)[..., :512][:, 94:418, 94:418]
+    ious = [O.calculate_iou(masks[i], gt[i]) for i in range(len(pick))]
+    np.testing.assert_allclose(ious, z["ious"][pick], rtol=0, atol=1e-12)
+
+
 def test_iou_semantics():
     # utils/metrics.py:6-37
     assert O.calculate_iou(np.zeros((3, 3)), np.zeros((3, 3))) == 1.0

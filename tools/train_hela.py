@@ -103,6 +103,7 @@ def main():
         model.train()
         t0 = time.perf_counter()
         losses = [trainer.step(x, t, wt) for x, t, wt in data]
+        trainer.check_targets()  # every step of the epoch, the last one included
         train_loss = float(torch.stack(losses).mean().item())
         dt = time.perf_counter() - t0
         val_loss = None

@@ -1,0 +1,70 @@
+"""Add the full-size parity tests' GEMM shapes to the bench's tuning database
+(VERDICT r03 item 2), so that every GEMM those tests run replays a recorded
+choice instead of timing candidates live on the test box.
+
+Loads the database, runs one train step of each configuration the tests run
+that the bench does not (tests/test_gpu_fullsize.py: fp32 batch 2 x 512^2,
+3-channel 572^2 batch 2 in fp32 and bf16; tests/test_gpu_model.py's
+channel/class cases at 188^2), letting the autotuner time what is missing,
+and writes the whole cache back.  Run after `bench.py --tune-db-out`:
+
+    python tools/tune_test_shapes.py profiles/tune_db.txt
+"""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..")
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "unet-segmentation_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+from oracle import fixtures as F  # noqa: E402
+from oracle import unet_oracle as O  # noqa: E402
+
+# (channels, classes, batch, size, precision, how): "module" = drop-in autograd
+# step (the every-element fp32 test), "trainer" = unet_amd.train.Trainer
+CASES = [(1, 2, 2, 512, "fp32", "module"), (3, 2, 2, 572, "fp32", "trainer"), (3, 2, 2, 572, "bf16", "trainer"),
+         (1, 2, 8, 512, "fp32", "trainer"), (1, 2, 8, 512, "bf16", "trainer")]
+# tests/test_gpu_model.py::test_channel_and_class_counts_vs_oracle (bench_tuning)
+CASES += [(c, k, 2, 188, "fp32", "module") for c, k in ((2, 3), (3, 1), (4, 4), (5, 5), (1, 9), (16, 2), (1, 17),
+                                                            (3, 32))]
+
+
+def main():
+    db = sys.argv[1]
+    from unet_amd import UNet, WeightedCrossEntropyLoss, _lib
+    from unet_amd.train import Trainer
+    lib = _lib.load()
+    lib.unet_tuning_reset()
+    n0 = lib.unet_tuning_load(db.encode()) if os.path.exists(db) else 0
+    for c, k, n, h, prec, how in CASES:
+        params = O.hash_init(c, k, seed=5, bn_random=True)
+        x, _, wmap = F.make_inputs(5, n, c, h)
+        ho = O.output_size(h)
+        tgt = np.minimum((O.hash_uniform(5, 1002, n * ho * ho) * k).astype(np.int64), k - 1).reshape(n, ho, ho)
+        m = UNet(c, k)
+        m.load_state_dict({kk: torch.from_numpy(np.asarray(v)) for kk, v in params.items()})
+        m = m.cuda().train()
+        xd, td, wd = (torch.from_numpy(a).cuda() for a in (x, tgt, wmap))
+        if how == "module":
+            m.precision = prec
+            WeightedCrossEntropyLoss()(m(xd), td, wd).backward()
+        else:
+            tr = Trainer(m, n, h, h, precision=prec)
+            tr.forward_loss(xd, td, wd)
+            tr.backward_and_reduce(xd)
+            del tr
+        torch.cuda.synchronize()
+        del m
+        torch.cuda.empty_cache()
+        print(f"tuned {c}ch/{k}cls batch {n} x {h}^2 {prec} ({how})", flush=True)
+    rep = _lib.tuning_report().splitlines()
+    live = sum(1 for ln in rep if ln and "tuning db" not in ln)
+    rc = lib.unet_tuning_save(db.encode())
+    print(f"{db}: {n0} entries loaded, {live} shapes tuned here, saved rc={rc}")
+
+
+if __name__ == "__main__":
+    main()

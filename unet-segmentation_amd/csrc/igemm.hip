@@ -15,6 +15,7 @@
 // double buffered.  The next K-step's global loads are issued before the MFMA
 // block and consumed (transform + ds_write) after it, so each wave's HBM/L2
 // latency hides under its own 32 MFMAs (2048 cycles) plus its SIMD partners'.
+#include <cstdio>
 #include <cstdlib>
 
 #include "gemm_common.h"
@@ -1071,6 +1072,18 @@ int num_cus() {
       g_num_cus = 256;
   }
   return g_num_cus;
+}
+
+int ablation_env(const char* name) {
+  const char* v = getenv(name);
+  if (!v || !*v) return 0;
+#ifdef UNET_ABLATIONS
+  return atoi(v);
+#else
+  fprintf(stderr, "unet_hip: %s=%s ignored (timing ablations need a build with -DUNET_ABLATIONS: make ABLATIONS=1)\n",
+          name, v);
+  return 0;
+#endif
 }
 
 static int env_int(const char* name, int dflt) {

@@ -1193,7 +1193,7 @@ static hipError_t go_wgrad3(const WgradArgs& a, hipStream_t s, int per_cu) {
   int splits = (per_cu * num_cus() + blocks - 1) / blocks;
   splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
   dim3 grid(a.Mo / 64, a.gb.Cg / 64, splits);
-  static const int abl = getenv("UNET_WG_ABL") ? atoi(getenv("UNET_WG_ABL")) : 0;
+  static const int abl = ablation_env("UNET_WG_ABL");
   WgradArgs b = a;
   b.abl = abl;
   hipLaunchKernelGGL((k_wgrad3_bf<TH, TW, D16, SPLIT>), grid, dim3(512), smem, s, b);
@@ -1442,7 +1442,7 @@ static hipError_t go_wgrad3w(const WgradArgs& a, hipStream_t s, int per_cu) {
   const int gx = a.Mo / BCO, gy = a.gb.Cg / BCI, blocks = gx * gy;
   int splits = (per_cu * num_cus() + blocks - 1) / blocks;
   splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
-  static const int abl = getenv("UNET_WG_ABL") ? atoi(getenv("UNET_WG_ABL")) : 0;
+  static const int abl = ablation_env("UNET_WG_ABL");
   WgradArgs b = a;
   b.abl = abl;
   hipLaunchKernelGGL((k_wgrad3w_bf<BCO, BCI>), dim3((unsigned)(blocks * splits)), dim3(512), smem, s, b, gx, gy);

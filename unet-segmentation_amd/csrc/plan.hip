@@ -1003,7 +1003,12 @@ extern "C" {
 // the hash of the sources this library was built from (csrc/Makefile: sha256
 // over $(SRCS), the internal headers and include/unet_hip.h, first 16 hex
 // digits), so a run's record names the code it ran
-const char* unet_version(void) { return "unet_hip 0.4 gfx950 fp32/bf16/bf16x3-mfma src " UNET_SRC_HASH; }
+#ifdef UNET_ABLATIONS
+#define UNET_BUILD_KIND " ablations"
+#else
+#define UNET_BUILD_KIND ""
+#endif
+const char* unet_version(void) { return "unet_hip 0.4 gfx950 fp32/bf16/bf16x3-mfma src " UNET_SRC_HASH UNET_BUILD_KIND; }
 const char* unet_last_error(void) { return g_err.c_str(); }
 
 unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {

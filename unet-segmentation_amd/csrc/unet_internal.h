@@ -155,6 +155,13 @@ bool conv3_ring_tile_shape(int tile, int& th, int& bn, int& ck);
 bool conv3_ring_fits(const IgemmArgs& a, int tile);
 hipError_t go_conv3_ring_tile(const IgemmArgs& a, hipStream_t s, int tile);
 int num_cus();
+
+// Timing-ablation switches (UNET_WG_ABL, UNET_WF_ABL, UNET_WF64_ABL: kernel
+// variants with work removed, results WRONG).  They are read only in a build
+// with -DUNET_ABLATIONS (make ABLATIONS=1; unet_version() then says
+// "ablations"); a production build ignores such a variable and says so once on
+// stderr, so a leftover environment can never corrupt a run.
+int ablation_env(const char* name);
 hipError_t launch_igemm(const IgemmArgs& a, hipStream_t s);  // heuristic
 hipError_t launch_igemm_v(const IgemmArgs& a, hipStream_t s, GemmChoice c);
 bool igemm_tile_fits(const IgemmArgs& a, int tile);

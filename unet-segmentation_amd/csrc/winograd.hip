@@ -1154,7 +1154,7 @@ hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s) {
   const int NB = a.N / 32;
   const long long G = (T + 31) / 32 * NB;
   hipLaunchKernelGGL(k_wino4f_w<16>, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
-  static const int abl = getenv("UNET_WF_ABL") ? atoi(getenv("UNET_WF_ABL")) : 0;
+  static const int abl = ablation_env("UNET_WF_ABL");
   switch (abl) {
     case 1: hipLaunchKernelGGL(k_wino4f<1>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;
     case 2: hipLaunchKernelGGL(k_wino4f<2>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;
@@ -1498,7 +1498,7 @@ hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s) {
   const int NB = a.N / 64;
   const long long G = (T + 31) / 32 * NB;
   hipLaunchKernelGGL(k_wino4f_w8, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
-  static const int abl = getenv("UNET_WF64_ABL") ? atoi(getenv("UNET_WF64_ABL")) : 0;
+  static const int abl = ablation_env("UNET_WF64_ABL");
   switch (abl) {
 #define WF64(A) \
   case A: hipLaunchKernelGGL(k_wino4f64<A>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;

@@ -157,9 +157,10 @@ def build_identity() -> dict:
     """unet_version() of the loaded library, the hash of the tree's sources and
     whether the two agree (a stale .so shows up as src_match False)."""
     v = load().unet_version().decode()
-    built = v.rsplit(" src ", 1)[-1] if " src " in v else "unknown"
+    built = v.rsplit(" src ", 1)[-1].split()[0] if " src " in v else "unknown"
     tree = source_hash()
-    return {"version": v, "lib_src": built, "tree_src": tree, "src_match": built == tree}
+    return {"version": v, "lib_src": built, "tree_src": tree, "src_match": built == tree,
+            "ablation_build": v.endswith(" ablations")}
 
 
 def tuning_report() -> str:

@@ -58,6 +58,12 @@ class HeLaBatches:
             raise ValueError("weights must be 'static' (the reference's precomputed maps) or 'warped'")
         self.images = images.contiguous()
         if labels.dtype != torch.uint16:
+            # instance ids are uint16 in the reference's man_seg*.tif files; a wider
+            # label map must fit that range (65536 would wrap to 0 = background)
+            if labels.numel():
+                lo, hi = torch.aminmax(labels)
+                if int(lo) < 0 or int(hi) > 65535:
+                    raise ValueError(f"label ids must lie in [0, 65535] (uint16 instance ids), got [{int(lo)}, {int(hi)}]")
             labels = labels.to(torch.int32).to(torch.int16).view(torch.uint16)
         self.labels = labels.contiguous()
         self.batch, self.out_hw = int(batch), tuple(out_hw)

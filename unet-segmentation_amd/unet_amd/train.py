@@ -199,7 +199,11 @@ class Trainer:
         for the same input tensors); any other call runs eagerly."""
         if (self._graph is not None and not self.plan.timing_on and
                 self._graph_key == self._key(x, targets, weights)):
+            self.labels.check()  # an earlier step's out-of-range target (raises IndexError)
             self._graph.replay()
+            # the replayed loss kernel wrote this step's label flag into acc: queue
+            # its host copy behind the replay like an eager step does
+            self.labels.record(self.acc)
             return self.loss
         if self._graph is not None and self._graph_key[1:] != (self.lr, self.mom):
             self._graph = None  # stale hyper-parameters: capture again after this eager step
@@ -214,6 +218,14 @@ class Trainer:
                 not self.plan.timing_on):
             self._capture(x, targets, weights)
         return loss
+
+    def check_targets(self):
+        """Wait for every step issued so far and raise IndexError if any of them
+        met a target outside [0, K) other than ignore_index -100 (torch's
+        CrossEntropyLoss raises at once; the fused loss flags it on the device
+        and the flag is otherwise read at the next step).  Call it at the end of
+        an epoch / run so the last step's labels are checked too."""
+        self.labels.check(wait=True)
 
     def _key(self, x, targets, weights):
         # lr / momentum are baked into the captured SGD launch: a change re-captures
