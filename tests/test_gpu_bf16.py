@@ -146,11 +146,16 @@ def test_bf16_conv3x3_dgrad(op_bf16, n, h, w, ci, co, variant):
 DMA = [63, 65, 66, 67, 68]
 
 
-@pytest.mark.parametrize("variant", DMA + [31, 33])
+@pytest.mark.parametrize("variant", DMA + [31, 33, 81, 82, 83, 84])
 @pytest.mark.parametrize("n,h,w,ci,co,tf", [(2, 14, 13, 64, 128, False), (2, 11, 17, 64, 64, True),
                                               (1, 30, 41, 128, 256, True), (3, 9, 9, 256, 64, False),
-                                              (1, 40, 70, 64, 64, True)])
+                                              (1, 40, 70, 64, 64, True), (2, 21, 37, 192, 128, True)])
 def test_bf16_conv3x3_fwd_a16(op_bf16, n, h, w, ci, co, tf, variant):
+    """bf16-stored input (op_a16): the LDS-DMA halo kernels and the LDS-DMA ring
+    (81-84), whose consumer BN+ReLU (tf) is applied to the raw halo in LDS, on
+    ragged grids (chunks 32 / 64 channels: ci 192 runs three 64-channel chunks)."""
+    if variant in (81, 84) and ci % 64 or variant in (81, 83) and co % 128:
+        pytest.skip("shape outside the ring tile's channel blocking")
     lib = op_bf16
     lib.unet_set_tuning(b"op_a16", 1)
     try:
@@ -223,15 +228,20 @@ def test_bf16_conv3x3_wgrad(op_bf16, n, h, w, ci, co, variant):
     assert rel_err(host(db), rdb) < 2e-5
 
 
-@pytest.mark.parametrize("variant", [-1, 20, 24, 25])
+@pytest.mark.parametrize("variant", [-1, 20, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33])
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 128, 128), (1, 40, 37, 128, 128), (2, 21, 44, 256, 128),
                                          (1, 7, 5, 128, 64), (2, 30, 19, 64, 256), (1, 3, 3, 128, 128)])
 def test_bf16_conv3x3_wgrad_bf16_storage(op_bf16, n, h, w, ci, co, variant):
-    """bf16-stored dY and X (op_a16, as a bf16 plan stores them): the halo-tiled
-    k_wgrad3_bf (20) and the wide two-stage-ring k_wgrad3w_bf (24: 128 co x 64
-    ci, 25: 64 co x 128 ci per workgroup) on ragged grids, including a grid
-    smaller than one 8x16 pixel tile."""
-    if variant == 24 and (co % 128 or ci % 64) or variant == 25 and (co % 64 or ci % 128):
+    """bf16-stored dY (zero-bordered padded copy) and X (op_a16, as a bf16 plan
+    stores them): the halo-tiled k_wgrad3_bf (20), the wide two-stage-ring
+    k_wgrad3w_bf (24: 128 co x 64 ci, 25: 64 co x 128 ci per workgroup) and the
+    LDS-DMA ring k_wgrad3_ring (26: 128 co x 64 ci with 4x16 pixel tiles, 27:
+    the same with 8x8 tiles, 28: 64 x 64, 29: 64 co x 128 ci, 30 / 31: 64 x 64
+    with 8x16 / 8x8 tiles, 32 / 33: the all-taps "slide" mapping at 128 x 64 /
+    64 x 128) on ragged grids, including a grid smaller than one pixel tile."""
+    need = {24: (128, 64), 25: (64, 128), 26: (128, 64), 27: (128, 64), 28: (64, 64), 29: (64, 128), 30: (64, 64),
+            31: (64, 64), 32: (128, 64), 33: (64, 128)}
+    if variant in need and (co % need[variant][0] or ci % need[variant][1]):
         pytest.skip("shape outside the tile's channel blocking")
     lib = op_bf16
     lib.unet_set_tuning(b"op_a16", 1)
@@ -356,7 +366,10 @@ def gemm_mode(request, lib):
             lib.unet_set_tuning(b"force_split", int(part[5:]))
         elif part.startswith("tile"):
             lib.unet_set_tuning(b"force_tile", int(part[4:]))
+        elif part.startswith("wtile"):  # every weight gradient that fits it (with "heuristic")
+            lib.unet_set_tuning(b"wgrad_variant", int(part[5:]))
     yield mode
+    lib.unet_set_tuning(b"wgrad_variant", -1)
     lib.unet_set_tuning(b"bf16_norm", 0)
     lib.unet_set_tuning(b"autotune", 1)
     lib.unet_set_tuning(b"force_split", 0)
@@ -370,7 +383,11 @@ def gemm_mode(request, lib):
                                        "tile43", "tile44", "tile41+split3", "tile63", "tile65", "tile66",
                                        "tile67", "tile67+split3", "tile63+split2", "norm+tile81", "norm+tile82",
                                        "norm+tile83", "norm+tile84", "norm+tile81+split3", "norm+tile83+split2",
-                                       "norm+tile31", "norm+heuristic"],
+                                       "norm+tile31", "norm+heuristic", "tile81", "tile82", "tile83", "tile84",
+                                       "tile81+split3", "heuristic+wtile26", "heuristic+wtile27",
+                                       "heuristic+wtile28", "heuristic+wtile29", "heuristic+wtile30",
+                                       "heuristic+wtile31", "heuristic+wtile32", "heuristic+wtile33",
+                                       "norm+heuristic+wtile26"],
                          indirect=True)
 def test_bf16_gemm_variants_vs_bf16_oracle(gemm_mode):
     """Every bf16 tile (21-26 row gather, 31-36 halo-tiled 3x3, 63-67 LDS-DMA

@@ -58,9 +58,12 @@ def main():
     if args.variants:
         variants = [int(v) for v in args.variants.split(",")]
     knob = b"igemm_variant"
-    if args.wgrad:  # -1 built-in; fp32 22/23 halo; bf16 / bf16x3 10-14 pixel-column, 20/21 halo
+    if args.wgrad:  # -1 built-in; fp32 22/23 halo; bf16 / bf16x3 10-14 pixel-column, 20/21 halo,
+        # 24/25 wide halo, 26-31 LDS-DMA ring (bf16-stored operands: --a16)
         knob = b"wgrad_variant"
         variants = [-1, 1, 22, 23] if args.prec == 0 else [-1, 10, 12, 13, 20, 21]
+        if args.variants:
+            variants = [int(v) for v in args.variants.split(",")]
     st = ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
     for name, n, h, w, ci, co in SHAPES:
         if args.shapes and name not in args.shapes.split(","):

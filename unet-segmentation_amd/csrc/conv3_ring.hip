@@ -25,49 +25,24 @@
 //    on the fragment read, so every ds_read_b128 lane group hits distinct
 //    bank quads for any tap offset (halo rows use a 36-pixel pitch so the
 //    swizzle depends on the pixel's column only).
+//  * XTF (round 4): a source with a consumer transform (relu(bn(y)) of the
+//    producer, bf16 raw conv output) is DMA'd raw and transformed in LDS, in
+//    place, once per chunk: at the chunk's last tap step every piece of the
+//    next chunk's halo has landed (issued >= 2 steps earlier, retired by the
+//    counted vmcnt + barrier), the waves rewrite it (BN scale / shift of its
+//    channels from an LDS table), and the next chunk's first barrier releases
+//    it to the MFMAs -- so every forward conv of a bf16 plan runs on the ring
+//    without a normalised copy of its input.
 // MFMA: v_mfma_f32_32x32x16_bf16, fp32 accumulation; each wave computes
 // (TM x 32) pixels x (TN x 32) columns.  The epilogue is the shared one
 // (igemm_finish: bias, BN statistics / ReLU mask + BN-backward statistics,
 // concat split, split-K partials).
 #include "gemm_common.h"
+#include "ring_common.h"
 
 namespace unet {
 
 typedef __bf16 bf16x8r_t __attribute__((ext_vector_type(8)));
-typedef __attribute__((address_space(3))) unsigned char lds_u8_t;
-
-// one global_load_lds_dwordx4: 16 B per lane from sbase + voff into LDS at the
-// wave-uniform byte address `lds` + lane * 16 (M0); the caller retires it with
-// a counted vmcnt.  Inline asm: hipcc does not track it (see conv3_dma.hip).
-__device__ __forceinline__ void dma_sv(unsigned voff, unsigned long long sbase, unsigned lds_addr) {
-  // wave-uniform by construction (wave index, slot, piece); readfirstlane puts it in an SGPR
-  const unsigned lds = __builtin_amdgcn_readfirstlane(lds_addr);
-  unsigned keep;
-  asm volatile(
-      "s_mov_b32 %0, m0\n\t"
-      "s_mov_b32 m0, %3\n\t"
-      "s_nop 0\n\t"
-      "global_load_lds_dwordx4 %1, %2\n\t"
-      "s_mov_b32 m0, %0"
-      : "=&s"(keep)
-      : "v"(voff), "s"(sbase), "s"(lds)
-      : "memory");
-}
-
-__device__ __forceinline__ unsigned long long uniform_u64(const void* p) {
-  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  return ((unsigned long long)hi << 32) | lo;
-}
-
-template <int N>
-__device__ __forceinline__ void vm_wait() {
-  static_assert(N >= 0 && N < 64, "vmcnt");
-  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
-}
-__device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
-
 template <int TH, int BN, int CK>
 struct RingGeo {
   static constexpr int TW = 32, HP = 36, RB = CK * 2, KS = CK / 16;
@@ -80,7 +55,7 @@ struct RingGeo {
   static constexpr size_t smem = (size_t)H0 + 2 * HSZ;
 };
 
-template <int TH, int BN, int WM, int WN, int CK, int TWO, int MINW>
+template <int TH, int BN, int WM, int WN, int CK, int TWO, int MINW, int XTF>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmArgs args) {
   using G = RingGeo<TH, BN, CK>;
   constexpr int HP = G::HP, RB = G::RB, KS = G::KS, RPB = G::RPB, CPR = G::CPR;
@@ -109,6 +84,20 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
   const int y0 = (tt % tiles_y) * TH;
   const int n = tt / tiles_y;
   const int n0 = blockIdx.y * BN;
+
+  // XTF: BN scale / shift of source 0 (the only source that can carry a
+  // transform: a skip or a previous conv output; the convT output never does)
+  // in LDS after the ring: [2][C of source 0]
+  const int xtc = TWO ? g.c_split : Cg;
+  float* xts = reinterpret_cast<float*>(lds + G::smem);
+  const bool xtf0 = XTF && g.s[0].scale != nullptr;
+  if constexpr (XTF) {
+    if (xtf0)
+      for (int c = tid; c < xtc; c += NT) {
+        xts[c] = g.s[0].scale[c];
+        xts[xtc + c] = g.s[0].shift[c];
+      }
+  }
 
   // ---- per-lane DMA offsets (bytes), computed once ----
   unsigned woff[IWW];
@@ -217,6 +206,29 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
     if constexpr (KS > 3) step(std::integral_constant<int, 3>{});
   };
 
+  // XTF: relu(bn(.)) of chunk c's raw halo in slot hs, in place (every piece
+  // landed and visible: called after a barrier that follows their vmcnt)
+  auto transform_h = [&](int c, int hs) {
+    const int c0 = c * CK;
+    if (!xtf0 || (TWO && c0 >= g.c_split)) return;  // the plain source needs nothing
+    unsigned char* hb = lds + H0 + hs * HSZ;
+    constexpr int PCS = PH * CPR;  // 16-B pieces of the halo rows
+#pragma unroll
+    for (int k = 0; k < (PCS + NT - 1) / NT; ++k) {
+      const int p = tid + NT * k;
+      if (p < PCS) {
+        const int r = p / CPR, hx = r % HP;
+        const int q = (p % CPR) ^ ((hx / RPB) % CPR);  // logical 8-channel group of the piece
+        const float* sc = xts + c0 + q * 8;
+        const float* sh = xts + xtc + c0 + q * 8;
+        uint4* pv = reinterpret_cast<uint4*>(hb + p * 16);
+        const uint4 u = *pv;
+        *pv = bf16pack8(affine_relu4(bf16x4_to_f4(make_uint2(u.x, u.y)), ld4(sc), ld4(sh)),
+                        affine_relu4(bf16x4_to_f4(make_uint2(u.z, u.w)), ld4(sc + 4), ld4(sh + 4)));
+      }
+    }
+  };
+
   // one chunk: 9 tap steps; step (c, t): wait for this wave's DMAs of step
   // (c, t) - 2 and older, barrier (everyone's landed, everyone done reading
   // the slot refilled next), issue the weights of step (c, t) + 2 and a piece
@@ -232,7 +244,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
       int cw = nx ? c + 1 : c, tw = nx ? t - 7 : t + 2;
       if (cw >= kc1) { cw = kc1 - 1; tw = 8; }  // tail: reload the last slab into a free slot
       issue_w(cw, tw, (t + 2) % 3);
-      issue_h(cn, t < NHS ? t : NHS - 1, cn == c ? hs : hs ^ 1);
+      // the next chunk's halo goes to the other slot; past the last chunk the
+      // re-issued bytes land there too (never read; the slot being read keeps
+      // its -- possibly transformed -- contents)
+      issue_h(cn, t < NHS ? t : NHS - 1, hs ^ 1);
+      if constexpr (XTF && t == 8) {
+        if (cn != c) transform_h(cn, hs ^ 1);
+      }
       tap_mfma(HSc, Tc);
     };
     tap(std::integral_constant<int, 0>{});
@@ -253,6 +271,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
     issue_w(kc0, 0, 0);
     issue_w(kc0, 1, 1);
     vm_wait<0>();
+    if constexpr (XTF) {
+      __syncthreads();  // the halo (and the BN table) visible to every wave
+      transform_h(kc0, 0);
+    }
     raw_barrier();
     for (int c = kc0; c < kc1; ++c) {
       if ((c - kc0) & 1) chunk(std::integral_constant<int, 1>{}, c);
@@ -278,38 +300,60 @@ bool conv3_ring_tile_shape(int tile, int& th, int& bn, int& ck) {
   }
 }
 
+// the LDS image of a launch: the ring, plus the BN table of source 0 (XTF)
+template <int TH, int BN, int CK>
+static size_t ring_smem(const IgemmArgs& a, bool xtf) {
+  const Gather& g = a.a;
+  return RingGeo<TH, BN, CK>::smem + (xtf ? 8 * (size_t)(g.c_split < g.Cg ? g.c_split : g.Cg) : 0);
+}
+
 template <int TH, int BN, int WM, int WN, int CK, int MINW>
 static hipError_t go_ring(const IgemmArgs& a, hipStream_t s) {
   const Gather& g = a.a;
-  const bool two = g.c_split < g.Cg;
-  using Gm = RingGeo<TH, BN, CK>;
-  static bool attr[2] = {false, false};
-  const void* fn = two ? reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 1, MINW>)
-                       : reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 0, MINW>);
-  if (!attr[two]) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)Gm::smem);
+  const bool two = g.c_split < g.Cg, xtf = g.s[0].scale != nullptr;
+  const int v = (two ? 1 : 0) | (xtf ? 2 : 0);
+  static bool attr[4] = {false, false, false, false};
+  const void* fns[4] = {reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 0, MINW, 0>),
+                        reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 1, MINW, 0>),
+                        reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 0, MINW, 1>),
+                        reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 1, MINW, 1>)};
+  const size_t smem = ring_smem<TH, BN, CK>(a, xtf);
+  if (!attr[v]) {  // the largest image any launch of this variant can ask for
+    hipError_t e = hipFuncSetAttribute(fns[v], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;
-    attr[two] = true;
+    attr[v] = true;
   }
   const long long tiles = (long long)g.nimg * ((g.Hg + TH - 1) / TH) * ((g.Wg + 31) / 32);
   dim3 grid((unsigned)tiles, a.N / BN, a.ksplit > 1 ? a.ksplit : 1);
-  if (two)
-    hipLaunchKernelGGL((k_conv3_ring<TH, BN, WM, WN, CK, 1, MINW>), grid, dim3(WM * WN * 64), Gm::smem, s, a);
-  else
-    hipLaunchKernelGGL((k_conv3_ring<TH, BN, WM, WN, CK, 0, MINW>), grid, dim3(WM * WN * 64), Gm::smem, s, a);
+  switch (v) {
+    case 0: hipLaunchKernelGGL((k_conv3_ring<TH, BN, WM, WN, CK, 0, MINW, 0>), grid, dim3(WM * WN * 64), smem, s, a); break;
+    case 1: hipLaunchKernelGGL((k_conv3_ring<TH, BN, WM, WN, CK, 1, MINW, 0>), grid, dim3(WM * WN * 64), smem, s, a); break;
+    case 2: hipLaunchKernelGGL((k_conv3_ring<TH, BN, WM, WN, CK, 0, MINW, 1>), grid, dim3(WM * WN * 64), smem, s, a); break;
+    default: hipLaunchKernelGGL((k_conv3_ring<TH, BN, WM, WN, CK, 1, MINW, 1>), grid, dim3(WM * WN * 64), smem, s, a); break;
+  }
   return hipGetLastError();
 }
 
-// A sources bf16 without a consumer transform (the plan's normalised copies,
-// padded dY, pooled maps, convT outputs), no split operands
+// A sources bf16 (the plan's raw conv outputs with their consumer transform,
+// normalised copies, padded dY, pooled maps, convT outputs); a transform only
+// on source 0 (the second source of a concat is the convT output); no split
+// operands; the BN table must fit the LDS beside the ring
 bool conv3_ring_fits(const IgemmArgs& a, int tile) {
   int th, bn, ck;
   if (!conv3_ring_tile_shape(tile, th, bn, ck)) return false;
   const Gather& g = a.a;
-  const bool two = g.c_split < g.Cg;
+  const bool two = g.c_split < g.Cg, xtf = g.s[0].scale != nullptr;
+  size_t smem = 0;
+  switch (tile) {
+    case 81: smem = ring_smem<8, 128, 64>(a, xtf); break;
+    case 82: smem = ring_smem<8, 64, 32>(a, xtf); break;
+    case 83: smem = ring_smem<4, 128, 32>(a, xtf); break;
+    default: smem = ring_smem<8, 64, 64>(a, xtf); break;
+  }
   return a.bh != nullptr && a.bl == nullptr && a.N % bn == 0 && g.taps_h == 3 && g.taps_w == 3 && g.stride == 1 &&
-         a.K == 9 * g.Cg && g.Cg % ck == 0 && g.c_split % ck == 0 && g.s[0].h16 && g.s[0].scale == nullptr &&
-         (!two || (g.s[1].h16 && g.s[1].scale == nullptr));
+         a.K == 9 * g.Cg && g.Cg % ck == 0 && g.c_split % ck == 0 && g.s[0].h16 &&
+         (!two || (g.s[1].h16 && g.s[1].scale == nullptr)) && (!xtf || g.s[0].shift != nullptr) &&
+         smem <= 160 * 1024;
 }
 
 hipError_t go_conv3_ring_tile(const IgemmArgs& a, hipStream_t s, int tile) {

@@ -1396,6 +1396,7 @@ bool wgrad_tile_fits(const WgradArgs& a, int tile) {
   if (tile == 20 || tile == 21) return wgrad3_fits(a);  // halo-tiled 3x3, all taps
   if (tile == 22 || tile == 23) return wgrad3_f32_fits(a);  // fp32 twin
   if (tile == 24 || tile == 25) return wgrad3w_fits(a, tile);  // wide halo-tiled 3x3, two-stage ring
+  if (tile >= 26 && tile <= 33) return wgrad3_ring_fits(a, tile);  // LDS-DMA ring of pixel tiles
   int bm, bn;
   wgrad_tile(tile, bm, bn);
   return bm > 0 && (tile >= 10) == (a.bf16 != 0) && a.Mo % bm == 0 && a.No % bn == 0;
@@ -1428,6 +1429,7 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   if (tile == 20 || tile == 21) return go_wgrad3_bf16(a, s, tile, c.split > 0 ? c.split : 4);
   if (tile == 22) return go_wgrad3_f32<8, 16>(a, s, c.split > 0 ? c.split : 4);
   if (tile == 24 || tile == 25) return go_wgrad3w_bf16(a, s, tile, c.split > 0 ? c.split : 1);
+  if (tile >= 26 && tile <= 33) return go_wgrad3_ring(a, s, tile, c.split > 0 ? c.split : 1);
   if (tile == 23) return go_wgrad3_f32<4, 32>(a, s, c.split > 0 ? c.split : 4);
   int bm, bn;
   wgrad_tile(tile, bm, bn);

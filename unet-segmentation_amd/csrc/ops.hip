@@ -180,13 +180,21 @@ int unet_conv3x3_wgrad(const float* x, const float* dy, int n, int h, int w, int
   a.bf16 = g_op_prec != UNET_PREC_FP32;
   a.split = g_op_prec == UNET_PREC_BF16X3;
   if (g_op_prec == UNET_PREC_BF16 && g_op_a16) {  // bf16-stored dY and X, as in a bf16 plan
-    uint16_t* dy16 = reinterpret_cast<uint16_t*>(p + 2 * wb);  // the (unused) padded-dY region
+    // dY as the plan keeps it: a zero-bordered padded bf16 copy (border 2),
+    // written by the BN-backward apply with identity coefficients
+    uint16_t* dy16 = reinterpret_cast<uint16_t*>(p + 2 * wb);
+    float* coef = reinterpret_cast<float*>(p + 2 * wb + al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co));
     uint16_t* x16 = reinterpret_cast<uint16_t*>(p + 2 * wb + al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co) +
                                                 al256(sizeof(float) * 4 * co) +
                                                 al256(sizeof(double) * kStatGroups * 2 * co));
-    OPCK(launch_f2bf(dy, dy16, (size_t)n * (h - 2) * (w - 2) * co, s));
+    OPCK(launch_fill(coef, co, 1.f, s));
+    OPCK(launch_fill(coef + co, 3 * (size_t)co, 0.f, s));
+    OPCK(launch_bnb_apply(dy, dy, coef, n, h - 2, w - 2, co, reinterpret_cast<float*>(dy16), 2, s, 1, 0));
     OPCK(launch_f2bf(x, x16, (size_t)n * h * w * ci, s));
     a.ga.s[0].ptr = a.ga.s[1].ptr = reinterpret_cast<const float*>(dy16);
+    a.ga.s[0].H = a.ga.s[1].H = h + 2;
+    a.ga.s[0].W = a.ga.s[1].W = w + 2;
+    a.ga.s[0].oy = a.ga.s[1].oy = a.ga.s[0].ox = a.ga.s[1].ox = 2;
     a.ga.s[0].h16 = a.ga.s[1].h16 = 1;
     a.gb.s[0].ptr = a.gb.s[1].ptr = reinterpret_cast<const float*>(x16);
     a.gb.s[0].h16 = a.gb.s[1].h16 = 1;

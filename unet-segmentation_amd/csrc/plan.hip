@@ -274,7 +274,7 @@ constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 // Version of the GEMM variant tables (tile ids and their kernels): part of every
 // tuning key, so a database written by a build with another tile set is never
 // replayed (its lines simply miss).  Bump whenever a tile id changes meaning.
-constexpr int kTileTableVersion = 6;
+constexpr int kTileTableVersion = 7;
 
 std::string igemm_key(const IgemmArgs& a) {
   char b[240], small[16] = "";
@@ -344,7 +344,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
 
 std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   std::vector<GemmChoice> v;
-  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 24, 25, 71, 74}) {  // fits() filters by precision
+  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 71, 74}) {  // fits() filters by precision
     if (!wgrad_tile_fits(a, t) || tune_skipped(t)) continue;
     if (t == 71 || t == 74) {  // Winograd: point-GEMM tile (k_wgrad 0-4) x workgroups per CU
       // (each pixel split adds a full points x Co x Ci slab by fp32 atomics:
@@ -353,7 +353,7 @@ std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
         for (int per_cu : {1, 2, 4, 8, 16}) v.push_back({t, per_cu + 100 * (inner + 1)});
       continue;
     }
-    if (t == 24 || t == 25) {  // wide halo-tiled: one resident workgroup per CU
+    if (t >= 24 && t <= 33) {  // wide halo-tiled / LDS-DMA ring: one resident workgroup per CU
       for (int per_cu : {1, 2}) v.push_back({t, per_cu});
       continue;
     }

@@ -180,6 +180,10 @@ hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid)
 // halo-tiled 3x3 weight gradient (wgrad tiles 20, 21): all 9 taps per workgroup
 bool wgrad3_fits(const WgradArgs& a);
 hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
+// 3x3 weight gradient with every operand staged by LDS-DMA through a 4-slot
+// ring of pixel tiles (wgrad tiles 26-33, wgrad3_ring.hip)
+bool wgrad3_ring_fits(const WgradArgs& a, int tile);
+hipError_t go_wgrad3_ring(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
 // wide halo-tiled 3x3 weight gradient with a two-stage ring (wgrad tiles 24, 25)
 bool wgrad3w_fits(const WgradArgs& a, int tile);
 hipError_t go_wgrad3w_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
