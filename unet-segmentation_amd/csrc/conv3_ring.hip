@@ -52,7 +52,11 @@ struct RingGeo {
   static constexpr int IH = (PH * RB + 1023) / 1024;   // halo DMA instructions per chunk
   static constexpr int HSZ = IH * 1024;
   static constexpr int H0 = 3 * WSZ;                   // LDS: 3 weight slots, then 2 halo slots
-  static constexpr size_t smem = (size_t)H0 + 2 * HSZ;
+  // + 1 KB junk target: the tap steps past the halo's last piece re-issue a
+  // DMA only to keep the per-step vmcnt arithmetic uniform; landing in a halo
+  // slot it would overwrite bytes transformed in place meanwhile (XTF)
+  static constexpr size_t JNK = (size_t)H0 + 2 * HSZ;
+  static constexpr size_t smem = JNK + 1024;
 };
 
 template <int TH, int BN, int WM, int WN, int CK, int TWO, int MINW, int XTF>
@@ -155,7 +159,11 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
 #pragma unroll
     for (int u = 0; u < IWW; ++u) dma_sv(woff[u], base, lds0 + slot * WSZ + (wave + NW * u) * 1024);
   };
-  // halo piece k of chunk c -> halo slot hs
+  auto issue_w1 = [&](int c, int t, int slot, int u) {
+    const unsigned long long base = uniform_u64(args.bh + (size_t)t * Cg + (size_t)c * CK);
+    dma_sv(woff[u], base, lds0 + slot * WSZ + (wave + NW * u) * 1024);
+  };
+  // halo piece k of chunk c -> halo slot hs (hs < 0: the junk KB)
   auto issue_h = [&](int c, int k, int hs) {
     const int c0 = c * CK;
     const bool second = TWO && c0 >= g.c_split;
@@ -163,7 +171,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
     const int cl = second ? c0 - g.c_split : c0;
     const unsigned long long base = uniform_u64(reinterpret_cast<const uint16_t*>(s.ptr) + cl);
     const unsigned off = second ? hoff1[TWO ? k : 0] : hoff0[k];
-    dma_sv(off, base, lds0 + H0 + hs * HSZ + min(k * NW + wave, IH - 1) * 1024);
+    dma_sv(off, base, hs < 0 ? lds0 + (unsigned)G::JNK : lds0 + H0 + hs * HSZ + min(k * NW + wave, IH - 1) * 1024);
   };
 
   floatx16 acc[TM][TN];
@@ -176,7 +184,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
 
   // one tap step: KS k-steps of TM x TN MFMAs; the next k-step's fragments are
   // read while this one's MFMAs issue
-  auto tap_mfma = [&](auto HSc, auto Tc) {
+  auto tap_mfma = [&](auto HSc, auto Tc, auto&& after) {
     constexpr int hs = decltype(HSc)::value, t = decltype(Tc)::value;
     constexpr int ky = t / 3, kx = t % 3, ws = t % 3;
     bf16x8r_t fa[2][TM], fb[2][TN];
@@ -199,6 +207,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
 #pragma unroll
         for (int j = 0; j < TN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[s & 1][i], fb[s & 1][j], acc[i][j], 0, 0, 0);
+      after(s);
     };
     step(std::integral_constant<int, 0>{});
     if constexpr (KS > 1) step(std::integral_constant<int, 1>{});
@@ -243,15 +252,26 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
       const bool nx = t + 2 >= 9;
       int cw = nx ? c + 1 : c, tw = nx ? t - 7 : t + 2;
       if (cw >= kc1) { cw = kc1 - 1; tw = 8; }  // tail: reload the last slab into a free slot
-      issue_w(cw, tw, (t + 2) % 3);
-      // the next chunk's halo goes to the other slot; past the last chunk the
-      // re-issued bytes land there too (never read; the slot being read keeps
-      // its -- possibly transformed -- contents)
-      issue_h(cn, t < NHS ? t : NHS - 1, hs ^ 1);
       if constexpr (XTF && t == 8) {
         if (cn != c) transform_h(cn, hs ^ 1);
       }
-      tap_mfma(HSc, Tc);
+      // this step's D DMAs go out one per k-step between the MFMAs (all at
+      // once after the barrier they put every wave of the CU in its DMA phase
+      // together): the weights of step + 2, then a piece of the next chunk's
+      // halo to the other slot (past the last chunk the re-issued bytes land
+      // there too: never read), or -- once the halo's pieces are out -- a
+      // dummy piece to the junk KB (keeps D DMAs per step for the vmcnt count
+      // without touching a halo that may be transformed in place)
+      auto after = [&](int k) {
+#pragma unroll
+        for (int u = 0; u < D; ++u) {
+          if (u == k || (k == KS - 1 && u > k)) {
+            if (u < IWW) issue_w1(cw, tw, (t + 2) % 3, u);
+            else issue_h(cn, t < NHS ? t : NHS - 1, t < NHS ? hs ^ 1 : -1);
+          }
+        }
+      };
+      tap_mfma(HSc, Tc, after);
     };
     tap(std::integral_constant<int, 0>{});
     tap(std::integral_constant<int, 1>{});

@@ -153,28 +153,42 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
   }
   // local tile i (tile z + i * gz; past the end: the last one again, so every
   // wave always has D DMAs per tile in flight) -> ring slot i % NS
-  auto issue = [&](int i) {
+  struct TileRef {
+    unsigned slot, zrow;
+    int arow, y0, x0, n;
+  };
+  auto tile_ref = [&](int i) {
     const int t = z + min(i, cnt - 1) * gz;
     const int tx0 = t % tiles_x, r = t / tiles_x;
-    const int y0 = (r % tiles_y) * TH, x0 = tx0 * TW, n = r / tiles_y;
-    const unsigned slot = lds0 + (unsigned)((i % NS) * SSZ);
-    const int arow = (n * dH + y0) * dW + x0;  // + the lane's pixel and the origin in a_rel
-    const unsigned zrow = (unsigned)(n * dH * dW * dC);
-#pragma unroll
-    for (int u = 0; u < DA; ++u) {
-      const bool ok = a_ty[u] < Hg - y0 && a_tx[u] < Wg - x0;
+    TileRef T;
+    T.y0 = (r % tiles_y) * TH;
+    T.x0 = tx0 * TW;
+    T.n = r / tiles_y;
+    T.slot = lds0 + (unsigned)((i % NS) * SSZ);
+    T.arow = (T.n * dH + T.y0) * dW + T.x0;  // + the lane's pixel and the origin in a_rel
+    T.zrow = (unsigned)(T.n * dH * dW * dC);
+    return T;
+  };
+  // DMA u (0 .. D-1: the dY pieces, then the X halo pieces) of tile T
+  auto dma_piece = [&](const TileRef& T, int u) {
+    if (u < DA) {
+      const bool ok = a_ty[u] < Hg - T.y0 && a_tx[u] < Wg - T.x0;
       // select by mask: a plain ?: between the two lane arrays was turned into
       // a select of their addresses (the arrays then live in scratch)
-      const unsigned v = (unsigned)(arow * dC) + a_rel[u], zv = zrow + a_zero[u];
+      const unsigned v = (unsigned)(T.arow * dC) + a_rel[u], zv = T.zrow + a_zero[u];
       const unsigned off = zv ^ ((v ^ zv) & (0u - (unsigned)ok));
-      dma_sv(off * 2u, abase, slot + (wave + 8 * u) * 1024);
+      dma_sv(off * 2u, abase, T.slot + (wave + 8 * u) * 1024);
+    } else {
+      const int k = u - DA;
+      const int yy = min(T.y0 + x_hy[k], Hg + 1), xx = min(T.x0 + x_hx[k], Wg + 1);
+      const unsigned off = (unsigned)(((T.n * xH + yy + xoy) * xW + xx + xox) * xC + x_c[k]);
+      dma_sv(off * 2u, xbase, T.slot + ASZ + min(wave + 8 * k, NDX - 1) * 1024);
     }
+  };
+  auto issue = [&](int i) {
+    const TileRef T = tile_ref(i);
 #pragma unroll
-    for (int u = 0; u < DX; ++u) {
-      const int yy = min(y0 + x_hy[u], Hg + 1), xx = min(x0 + x_hx[u], Wg + 1);
-      const unsigned off = (unsigned)(((n * xH + yy + xoy) * xW + xx + xox) * xC + x_c[u]);
-      dma_sv(off * 2u, xbase, slot + ASZ + min(wave + 8 * u, NDX - 1) * 1024);
-    }
+    for (int u = 0; u < D; ++u) dma_piece(T, u);
   };
 
   // ---- in-LDS BN+ReLU of a slot's X halo (XTF) ----
@@ -241,7 +255,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
   // one tile from slot S, taps TG*5 .. : KS k-steps of TMC x NT MFMAs; the
   // fragments of k-step ks + 1 are read (into the other register buffer)
   // before k-step ks's MFMAs issue, so LDS latency hides behind them
-  auto compute = [&](auto Sc, auto TGc) {
+  auto compute = [&](auto Sc, auto TGc, auto&& after) {
     constexpr int S = decltype(Sc)::value, TG = decltype(TGc)::value;
     constexpr int T0 = TG * 5, NT = TG ? 4 : 5;
     const unsigned sbase = lds0 + S * SSZ;
@@ -272,6 +286,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
 #pragma unroll
         for (int i = 0; i < TMC1; ++i)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[b][i], fb[b][j], acc[i][j], 0, 0, 0);
+      after(ks);
     };
     if constexpr (TMC > 1) {
       // two co tiles per wave: no register room for a second fragment buffer;
@@ -294,6 +309,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
           for (int i = 0; i < TMC; ++i)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[i], b, acc[i][j], 0, 0, 0);
         }
+        after(ks);
       }
       return;
     }
@@ -313,7 +329,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
   // k-steps (tile rows) are read once, then per tap column kx the halo rows
   // r = 0 .. TH+1 in order, each feeding MFMAs (ks = r - ky, ky) for ky = 0..2;
   // the next row's fragment is read before the current row's MFMAs issue
-  auto compute_slide = [&](auto Sc) {
+  auto compute_slide = [&](auto Sc, auto&& after) {
     constexpr int S = decltype(Sc)::value;
     const unsigned sbase = lds0 + S * SSZ;
     bf16x8w_t fa[TH];
@@ -341,6 +357,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
           if (ks >= 0 && ks < TH)
             acc[0][ky * 3 + kx] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[ks], b, acc[0][ky * 3 + kx], 0, 0, 0);
         }
+        after(kx * (TH + 2) + r);
         b = bn;
       }
   };
@@ -353,13 +370,23 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
     if constexpr (XTF) vm_wait<D>();
     else vm_wait<2 * D>();
     raw_barrier();
-    issue(i + 3);
     if constexpr (XTF) {
       if (i + 1 < cnt) transform(i + 1);
     }
-    if constexpr (SLIDE) compute_slide(Sc);
-    else if (tg == 0) compute(Sc, std::integral_constant<int, 0>{});
-    else compute(Sc, std::integral_constant<int, 1>{});
+    // tile i + 3's DMAs go out one per k-step between the MFMAs (issued all at
+    // once after the barrier they held every wave of the CU in its DMA phase
+    // together, with the matrix pipes idle)
+    const TileRef T = tile_ref(i + 3);
+    constexpr int KLAST = SLIDE ? 3 * (TH + 2) - 1 : KS - 1;  // index of the last k-step callback
+    auto after = [&](int k) {
+      if (k < D) dma_piece(T, k);
+      if (k == KLAST)  // fewer k-steps than DMAs: the rest after the last one
+#pragma unroll
+        for (int u = KLAST + 1; u < D; ++u) dma_piece(T, u);
+    };
+    if constexpr (SLIDE) compute_slide(Sc, after);
+    else if (tg == 0) compute(Sc, std::integral_constant<int, 0>{}, after);
+    else compute(Sc, std::integral_constant<int, 1>{}, after);
   };
 
   issue(0);

@@ -1512,6 +1512,313 @@ hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s) {
 
 
 // ---------------------------------------------------------------------------
+// k_wino2f64: fused Winograd F(2x2, 3x3), 64 output channels x 64 tiles per
+// workgroup (igemm tile 75, round 4).  The 64-channel forwards (inc.c1, up4.c1)
+// ran direct (k_conv3_f32, ~73 % MFMA busy, 1.9 ms of the fp32 step) because
+// F(4x4)'s rounding on them sits at the every-element parity bar;
+// F(2x2)'s transforms are exact in their +-1 / 1/2 coefficients and its error
+// is the direct sum's order (r03 sweep: 0.56 of the bar with F(2x2) forwards),
+// at 16 point products per 2x2 outputs = 4/9 of the direct MFMA work.
+// Structure of k_wino4f64 with 4x4 patches:
+//   * per 8-channel chunk a thread owns one (tile, channel) patch: 16 loads
+//     (the next chunk's issued before this chunk's MFMAs), the producer's
+//     BN+ReLU, B^T d B (24 adds), 16 points into U[p][tile][8] in LDS; V (the
+//     chunk's 16 x 64 x 8 transformed weights, k_wino2f_w8) goes through
+//     registers into LDS too;
+//   * wave w: tile quarter w & 3, output-channel half w >> 2 (two 16-channel
+//     blocks): per point one U read, two V reads, four v_mfma_f32_16x16x4_f32;
+//     lane (mi, mq) ends with all 16 points of channels 4 mq .. +3 of tile mi
+//     for each block: A^T M A and the epilogue from registers, 16-B stores.
+// ---------------------------------------------------------------------------
+__global__ void k_wino2f_w8(const float* __restrict__ b, int N, int Cg, float* __restrict__ v) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= (long long)N * Cg) return;
+  const int n = (int)(i / Cg), c = (int)(i - (long long)n * Cg);
+  float g[3][3];
+#pragma unroll
+  for (int t = 0; t < 9; ++t) g[t / 3][t % 3] = b[((size_t)n * 9 + t) * Cg + c];
+  float tg[4][3];  // G g (k_wino_w's G)
+#pragma unroll
+  for (int k = 0; k < 3; ++k) {
+    tg[0][k] = g[0][k];
+    tg[1][k] = 0.5f * (g[0][k] + g[1][k] + g[2][k]);
+    tg[2][k] = 0.5f * (g[0][k] - g[1][k] + g[2][k]);
+    tg[3][k] = g[2][k];
+  }
+  const size_t base = (size_t)(c >> 3) * 16 * N;
+  const int pos = wf8_slot(n, c & 3) + ((c >> 2) & 1);
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const float w4[4] = {tg[r][0], 0.5f * (tg[r][0] + tg[r][1] + tg[r][2]), 0.5f * (tg[r][0] - tg[r][1] + tg[r][2]),
+                         tg[r][2]};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[(base + (size_t)(r * 4 + q) * N + n) * 8 + pos] = w4[q];
+  }
+}
+
+__global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __restrict__ V, int N, long long T,
+                                                     int Th, int Tw, int NB, Epilogue e) {
+  constexpr int TT = 64;      // tiles per workgroup
+  constexpr int PU = TT * 8;  // U point plane
+  constexpr int PV = 64 * 8;  // V point plane
+  __shared__ __attribute__((aligned(16))) float lds[16 * PU + 16 * PV];
+  float* Us = lds;
+  float* Vs = lds + 16 * PU;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  long long bid = blockIdx.x;
+  const long long G = gridDim.x;
+  if ((G & 7) == 0) bid = (bid & 7) * (G >> 3) + (bid >> 3);  // an XCD's workgroups share tiles
+  const int nb = (int)(bid % NB);
+  const long long t0 = (bid / NB) * TT;
+  const int n0 = nb * 64;
+
+  // ---- loader role: patch (tile lt, channel lc) ----
+  const int lt = tid >> 3, lc = tid & 7;
+  const long long t = t0 + lt;
+  int img = 0, ty = 0, tx = 0;
+  if (t < T) {
+    tx = (int)(t % Tw);
+    const long long r = t / Tw;
+    ty = (int)(r % Th);
+    img = (int)(r / Th);
+  }
+  // rows / columns of the 4x4 patch inside the gather's input grid (Hg+2, Wg+2)
+  const int vrows = t < T ? min(4, g.Hg + 2 - 2 * ty) : 0;
+  const int vcols = t < T ? min(4, g.Wg + 2 - 2 * tx) : 0;
+  const bool wfull = __all(vrows == 4 && vcols == 4);
+  float* const ubase = Us + lt * 8 + wf8_slot(lt, lc & 3) + (lc >> 2);
+  float raw[16];
+  float4 vr[4];
+  const int nk = g.Cg >> 3;
+  auto load = [&](int kc) {
+    const bool second = kc * 8 >= g.c_split;  // c_split % 8 == 0: uniform source
+    const float* sp = second ? g.s[1].ptr : g.s[0].ptr;
+    const int sH = second ? g.s[1].H : g.s[0].H, sW = second ? g.s[1].W : g.s[0].W;
+    const int sC = second ? g.s[1].C : g.s[0].C;
+    const int soy = second ? g.s[1].oy : g.s[0].oy, sox = second ? g.s[1].ox : g.s[0].ox;
+    const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    const char* sb = reinterpret_cast<const char*>(sp);
+    const unsigned o0 = ((unsigned)((img * sH + 2 * ty + soy) * sW + 2 * tx + sox) * sC + cl) * 4u;
+    const unsigned rs = (unsigned)sW * sC * 4u, cs = (unsigned)sC * 4u;
+    if (wfull) {
+#pragma unroll
+      for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 4; ++xx)
+          raw[yy * 4 + xx] = *reinterpret_cast<const float*>(sb + (o0 + (yy * rs + xx * cs)));
+    } else {  // clamp to the last in-window row / column (zeroed in commit)
+      const unsigned lr = (unsigned)max(vrows - 1, 0), lcn = (unsigned)max(vcols - 1, 0);
+#pragma unroll
+      for (int yy = 0; yy < 4; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 4; ++xx)
+          raw[yy * 4 + xx] = *reinterpret_cast<const float*>(
+              sb + (o0 + (min((unsigned)yy, lr) * rs + min((unsigned)xx, lcn) * cs)));
+    }
+    const char* vb = reinterpret_cast<const char*>(V + ((size_t)kc * 16 * N + n0) * 8);
+    const unsigned vo = ((unsigned)(tid >> 7) * N * 8u + (tid & 127) * 4u) * 4u;
+    const unsigned vstep = 4u * N * 8u * 4u;  // 4 points per 512 float4
+#pragma unroll
+    for (int j = 0; j < 4; ++j) vr[j] = *reinterpret_cast<const float4*>(vb + (vo + j * vstep));
+  };
+  auto commit = [&](int kc) {
+    const bool second = kc * 8 >= g.c_split;
+    const float* scp = second ? g.s[1].scale : g.s[0].scale;
+    const float* shp = second ? g.s[1].shift : g.s[0].shift;
+    const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    if (scp) {
+      const float sc = scp[cl], sh = shp[cl];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) raw[q] = fmaxf(fmaf(raw[q], sc, sh), 0.f);
+    }
+    if (!wfull) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) raw[q] = (q / 4 < vrows && q % 4 < vcols) ? raw[q] : 0.f;
+    }
+    // B^T d (rows), then (.) B (columns): k_wino_in's transform
+    float ev[4][4];
+#pragma unroll
+    for (int xx = 0; xx < 4; ++xx) {
+      ev[0][xx] = raw[0 * 4 + xx] - raw[2 * 4 + xx];
+      ev[1][xx] = raw[1 * 4 + xx] + raw[2 * 4 + xx];
+      ev[2][xx] = raw[2 * 4 + xx] - raw[1 * 4 + xx];
+      ev[3][xx] = raw[1 * 4 + xx] - raw[3 * 4 + xx];
+    }
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      ubase[(a * 4 + 0) * PU] = ev[a][0] - ev[a][2];
+      ubase[(a * 4 + 1) * PU] = ev[a][1] + ev[a][2];
+      ubase[(a * 4 + 2) * PU] = ev[a][2] - ev[a][1];
+      ubase[(a * 4 + 3) * PU] = ev[a][1] - ev[a][3];
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int q = tid + 512 * j;
+      st4(Vs + (q >> 7) * PV + (q & 127) * 4, vr[j]);
+    }
+  };
+
+  // ---- MFMA role: wave = (tile quarter th, channel half ch), all 16 points ----
+  const int th = wave & 3, ch = wave >> 2;
+  const int mi = lane & 15, mq = lane >> 4;
+  const int aoff = (16 * th + mi) * 8 + wf8_slot(16 * th + mi, mq);
+  const int boff = (32 * ch + mi) * 8 + wf8_slot(mi, mq);  // rows 32 ch + 16 j + mi and mi agree on bits 2-3
+  floatx4 acc[16][2];
+#pragma unroll
+  for (int p = 0; p < 16; ++p)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[p][j] = (floatx4){0.f, 0.f, 0.f, 0.f};
+  load(0);
+  for (int kc = 0; kc < nk; ++kc) {
+    commit(kc);
+    __syncthreads();
+    if (kc + 1 < nk) load(kc + 1);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      const float2 a = *reinterpret_cast<const float2*>(Us + p * PU + aoff);
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const float2 b = *reinterpret_cast<const float2*>(Vs + p * PV + boff + 16 * j * 8);
+        acc[p][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.x, a.x, acc[p][j], 0, 0, 0);
+        acc[p][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.y, a.y, acc[p][j], 0, 0, 0);
+      }
+    }
+    __syncthreads();
+  }
+
+  // ---- output: tile 16 th + mi, channels n0 + 32 ch + 16 j + 4 mq + (0..3) ----
+  const long long tt = t0 + 16 * th + mi;
+  const bool want = e.stats || e.yref || e.colsum1;
+  const int nsplit = e.n_split < N ? e.n_split : N;
+  const int grp = blockIdx.x % kStatGroups;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int col0 = n0 + 32 * ch + 16 * j + 4 * mq;
+    const bool second = col0 >= e.n_split;  // uniform per 16-channel block (n_split % 16 == 0)
+    float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
+    const int dC = second ? e.d[1].C : e.d[0].C;
+    const int dcol = second ? col0 - e.n_split : col0;
+    const bool bwd_mask = e.yref != nullptr && !second;
+    const float4 bias = e.bias ? ld4(e.bias + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 bsc = make_float4(0.f, 0.f, 0.f, 0.f), bsh = bsc, bmu = bsc, bis = bsc;
+    if (bwd_mask) { bsc = ld4(e.bn_scale + col0); bsh = ld4(e.bn_shift + col0); bmu = ld4(e.bn_mean + col0); bis = ld4(e.bn_invstd + col0); }
+    float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+    if (tt < T) {
+      float o[4][2][2];  // [channel][row][col] = A^T M A
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float w[2][4];
+#pragma unroll
+        for (int xx = 0; xx < 4; ++xx) {
+          const float m0 = acc[0 * 4 + xx][j][r], m1 = acc[1 * 4 + xx][j][r];
+          const float m2 = acc[2 * 4 + xx][j][r], m3 = acc[3 * 4 + xx][j][r];
+          w[0][xx] = m0 + m1 + m2;
+          w[1][xx] = m1 - m2 - m3;
+        }
+#pragma unroll
+        for (int a = 0; a < 2; ++a) {
+          o[r][a][0] = w[a][0] + w[a][1] + w[a][2];
+          o[r][a][1] = w[a][1] - w[a][2] - w[a][3];
+        }
+      }
+      const int ox = (int)(tt % Tw);
+      const long long rq = tt / Tw;
+      const int oy = (int)(rq % Th), on = (int)(rq / Th);
+      const float bsv[4] = {bias.x, bias.y, bias.z, bias.w};
+      const float scv[4] = {bsc.x, bsc.y, bsc.z, bsc.w}, shv[4] = {bsh.x, bsh.y, bsh.z, bsh.w};
+      const float muv[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, isv[4] = {bis.x, bis.y, bis.z, bis.w};
+#pragma unroll
+      for (int a = 0; a < 2; ++a) {
+        const int y = 2 * oy + a;
+        if (y >= g.Hg) continue;
+#pragma unroll
+        for (int bb = 0; bb < 2; ++bb) {
+          const int x = 2 * ox + bb;
+          if (x >= g.Wg) continue;
+          const size_t idx = ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol;
+          float yv[4] = {0.f, 0.f, 0.f, 0.f};
+          if (bwd_mask) {
+            const float4 y4 = ld4(e.yref + idx);
+            yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
+          }
+          float v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = o[r][a][bb] + bsv[r];
+            if (bwd_mask) {
+              v[r] = fmaf(yv[r], scv[r], shv[r]) > 0.f ? v[r] : 0.f;
+              s1[r] += v[r];
+              s2[r] += v[r] * ((yv[r] - muv[r]) * isv[r]);
+            } else if (e.stats) {
+              s1[r] += v[r];
+              s2[r] += v[r] * v[r];
+            } else if (second && e.colsum1) {
+              s1[r] += v[r];
+            }
+            if (e.relu) v[r] = fmaxf(v[r], 0.f);
+          }
+          st4(dptr + idx, make_float4(v[0], v[1], v[2], v[3]));
+        }
+      }
+    }
+    if (!want) continue;
+    // the 16 lanes of a quarter hold the same 4 channels (other tiles)
+#pragma unroll
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o2 = 1; o2 < 16; o2 <<= 1) {
+        s1[r] += __shfl_xor(s1[r], o2);
+        s2[r] += __shfl_xor(s2[r], o2);
+      }
+    if (mi == 0) {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int col = col0 + r;
+        if (col < nsplit) {
+          double* st = e.yref ? e.bstats : e.stats;
+          if (st) {
+            atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)s1[r]);
+            atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)s2[r]);
+          }
+        } else if (e.colsum1) {
+          atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (col - nsplit), (double)s1[r]);
+        }
+      }
+    }
+  }
+}
+
+bool wino_fused2_applies(const IgemmArgs& a) {
+  const Gather& g = a.a;
+  if (a.b == nullptr || a.bh != nullptr || a.batch != 1) return false;
+  if (g.taps_h != 3 || g.taps_w != 3 || g.stride != 1 || a.K != 9 * g.Cg || g.Cg % 8 != 0 || g.c_split % 8 != 0 ||
+      a.N % 64 != 0 || (a.e.n_split < a.N && a.e.n_split % 16 != 0))
+    return false;
+  if (g.s[0].h16 || g.s[1].h16 || a.e.shuffle_co || a.e.d[0].h16 || a.e.d[1].h16 || a.e.yref_h16) return false;
+  if (a.e.d[0].oy || a.e.d[0].ox || a.e.d[0].H != g.Hg || a.e.d[0].W != g.Wg) return false;
+  if (a.e.n_split < a.N && (a.e.d[1].oy || a.e.d[1].ox || a.e.d[1].H != g.Hg || a.e.d[1].W != g.Wg)) return false;
+  for (int k = 0; k < 2; ++k)  // 32-bit byte offsets into the sources
+    if ((long long)g.nimg * g.s[k].H * g.s[k].W * g.s[k].C * 4 >= (1ll << 32)) return false;
+  const long long T = (long long)g.nimg * ((g.Hg + 1) / 2) * ((g.Wg + 1) / 2);
+  if ((T + 63) / 64 * (a.N / 64) > 0x7fffffffLL) return false;
+  return a.wino_ws != nullptr && (size_t)16 * a.N * g.Cg * 4 <= a.wino_ws_bytes;
+}
+
+hipError_t launch_wino_fused2(const IgemmArgs& a, hipStream_t s) {
+  if (!wino_fused2_applies(a)) return hipErrorInvalidValue;
+  const Gather& g = a.a;
+  const int Th = (g.Hg + 1) / 2, Tw = (g.Wg + 1) / 2;
+  const long long T = (long long)g.nimg * Th * Tw;
+  float* V = reinterpret_cast<float*>(a.wino_ws);
+  const long long nw = (long long)a.N * g.Cg;
+  const int NB = a.N / 64;
+  const long long G = (T + 63) / 64 * NB;
+  hipLaunchKernelGGL(k_wino2f_w8, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
+  hipLaunchKernelGGL(k_wino2f64, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
 // Weight gradient, F(4x4, 3x3) (wgrad tile 71).  The forward bilinear form
 // sum_p (A y)_p (G g)_p (B^T d)_p gives, differentiated by g,
 //   dW = G^T [ sum_tiles (A dY A^T) . (B^T X B) ] G,
