@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "gemm_common.h"
+#include "ring_common.h"
 
 namespace unet {
 
@@ -1225,6 +1226,18 @@ __global__ void k_wino4f_w8(const float* __restrict__ b, int N, int Cg, float* _
 // ABL: timing ablations (UNET_WF64_ABL; results wrong with any bit set): 1 = no
 // BatchNorm / transform arithmetic, 2 = no MFMA, 4 = no operand loads after the
 // first chunk, 8 = no output stage
+// One output element of the register-output fused kernels: the dgrad ReLU
+// mask + BN-backward statistics (bwd_mask) or the forward sums (s1 = sum v,
+// s2 = sum v^2; the caller reduces s1 only where it wants a column sum), then
+// the optional ReLU.  Branch-free in the per-wave flags.
+__device__ __forceinline__ float wf_epi(float v, float yv, float sc, float sh, float mu, float is, bool bwd_mask,
+                                        bool relu, float& s1, float& s2) {
+  v = (bwd_mask && !(fmaf(yv, sc, sh) > 0.f)) ? 0.f : v;
+  s1 += v;
+  s2 += v * (bwd_mask ? (yv - mu) * is : v);
+  return relu ? fmaxf(v, 0.f) : v;
+}
+
 template <int ABL>
 __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __restrict__ V, int N, long long T,
                                                      int Th, int Tw, int NB, Epilogue e) {
@@ -1393,11 +1406,11 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
   const int dC = second ? e.d[1].C : e.d[0].C;
   const int dcol = second ? col0 - e.n_split : col0;
   const bool bwd_mask = e.yref != nullptr && !second;
-  const float4 bias = e.bias ? ld4(e.bias + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
-  float4 bsc = make_float4(0.f, 0.f, 0.f, 0.f), bsh = bsc, bmu = bsc, bis = bsc;
-  if (bwd_mask) { bsc = ld4(e.bn_scale + col0); bsh = ld4(e.bn_shift + col0); bmu = ld4(e.bn_mean + col0); bis = ld4(e.bn_invstd + col0); }
   float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
   if (tt < T) {
+    const int ox = (int)(tt % Tw);
+    const long long rq = tt / Tw;
+    const int oy = (int)(rq % Th), on = (int)(rq / Th);
     float o[4][4][4];  // [channel][row][col]
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -1415,43 +1428,46 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
 #pragma unroll
       for (int a = 0; a < 4; ++a) at4(w[a], o[r][a]);
     }
-    const int ox = (int)(tt % Tw);
-    const long long rq = tt / Tw;
-    const int oy = (int)(rq % Th), on = (int)(rq / Th);
+    const float4 bias = e.bias ? ld4(e.bias + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 bsc = make_float4(0.f, 0.f, 0.f, 0.f), bsh = bsc, bmu = bsc, bis = bsc;
+    if (bwd_mask) { bsc = ld4(e.bn_scale + col0); bsh = ld4(e.bn_shift + col0); bmu = ld4(e.bn_mean + col0); bis = ld4(e.bn_invstd + col0); }
     const float bsv[4] = {bias.x, bias.y, bias.z, bias.w};
     const float scv[4] = {bsc.x, bsc.y, bsc.z, bsc.w}, shv[4] = {bsh.x, bsh.y, bsh.z, bsh.w};
     const float muv[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, isv[4] = {bis.x, bis.y, bis.z, bis.w};
+    // The dgrad's mask operand y (16 B per pixel and lane) comes in by LDS-DMA,
+    // 8 pixels at a time into this wave's 8 KB of the (now idle) LDS, one wait
+    // per 8: register loads here made the compiler chain load -> wait -> store
+    // per pixel (the in-order vmcnt counts the stores), with nothing else on the
+    // CU to hide it (round 4: ~0.9 ms of the fp32 step, UNET_WF64_ABL=8).
+    const unsigned long long ybase = uniform_u64(e.yref);  // kernel argument: SGPRs (unused unless bwd_mask)
+    const unsigned ylds = (unsigned)(size_t)(lds_u8_t*)lds + (unsigned)wave * 8192u;
 #pragma unroll
-    for (int a = 0; a < 4; ++a) {
-      const int y = 4 * oy + a;
-      if (y >= g.Hg) continue;
+    for (int h = 0; h < 2; ++h) {
+      if (bwd_mask) {
 #pragma unroll
-      for (int bb = 0; bb < 4; ++bb) {
-        const int x = 4 * ox + bb;
-        if (x >= g.Wg) continue;
-        const size_t idx = ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol;
-        float yv[4] = {0.f, 0.f, 0.f, 0.f};
-        if (bwd_mask) {
-          const float4 y4 = ld4(e.yref + idx);
-          yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
+        for (int q = 0; q < 8; ++q) {
+          const int y = min(4 * oy + 2 * h + (q >> 2), g.Hg - 1), x = min(4 * ox + (q & 3), g.Wg - 1);
+          dma_sv((((unsigned)(on * g.Hg + y) * g.Wg + x) * dC + dcol) * 4u, ybase, ylds + q * 1024u);
         }
+      }
+      // vmcnt(0) as a builtin, not asm: it retires the DMAs and, visibly to the
+      // compiler's wait-count tracking, the coefficient loads above, so no
+      // per-pixel branch join leaves them pending (it then re-waited, stores
+      // included, before every pixel)
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int a = 2 * h + (q >> 2), bb = q & 3;
+        const int y = 4 * oy + a, x = 4 * ox + bb;
+        if (y >= g.Hg || x >= g.Wg) continue;
+        const float4 yq = bwd_mask ? *reinterpret_cast<const float4*>(lds + wave * 2048 + q * 256 + lane * 4)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float yv[4] = {yq.x, yq.y, yq.z, yq.w};
         float v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = o[r][a][bb] + bsv[r];
-          if (bwd_mask) {
-            v[r] = fmaf(yv[r], scv[r], shv[r]) > 0.f ? v[r] : 0.f;
-            s1[r] += v[r];
-            s2[r] += v[r] * ((yv[r] - muv[r]) * isv[r]);
-          } else if (e.stats) {
-            s1[r] += v[r];
-            s2[r] += v[r] * v[r];
-          } else if (second && e.colsum1) {
-            s1[r] += v[r];
-          }
-          if (e.relu) v[r] = fmaxf(v[r], 0.f);
-        }
-        st4(dptr + idx, make_float4(v[0], v[1], v[2], v[3]));
+        for (int r = 0; r < 4; ++r) v[r] = wf_epi(o[r][a][bb] + bsv[r], yv[r], scv[r], shv[r], muv[r], isv[r],
+                                                   bwd_mask, e.relu, s1[r], s2[r]);
+        st4(dptr + ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol, make_float4(v[0], v[1], v[2], v[3]));
       }
     }
   }
@@ -1485,7 +1501,9 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
 }
 
 bool wino_fused64_applies(const IgemmArgs& a) {
-  return wino_fused_applies(a) && a.N % 64 == 0;  // Cg, c_split % 16 == 0 imply % 8
+  // Cg, c_split % 16 == 0 imply % 8; the mask operand's LDS-DMA takes 32-bit byte offsets
+  return wino_fused_applies(a) && a.N % 64 == 0 &&
+         (a.e.yref == nullptr || (long long)a.a.nimg * a.a.Hg * a.a.Wg * a.e.d[0].C * 4 < (1ll << 32));
 }
 
 hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s) {
@@ -1704,6 +1722,20 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
     if (bwd_mask) { bsc = ld4(e.bn_scale + col0); bsh = ld4(e.bn_shift + col0); bmu = ld4(e.bn_mean + col0); bis = ld4(e.bn_invstd + col0); }
     float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
     if (tt < T) {
+      const int ox = (int)(tt % Tw);
+      const long long rq = tt / Tw;
+      const int oy = (int)(rq % Th), on = (int)(rq / Th);
+      float4 y4[4];  // mask operands first, one wait (k_wino4f64)
+      if (bwd_mask) {
+#pragma unroll
+        for (int a = 0; a < 2; ++a)
+#pragma unroll
+          for (int bb = 0; bb < 2; ++bb) {
+            const int y = min(2 * oy + a, g.Hg - 1), x = min(2 * ox + bb, g.Wg - 1);
+            y4[a * 2 + bb] = ld4(e.yref + ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol);
+          }
+      }
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0) once: see k_wino4f64's epilogue
       float o[4][2][2];  // [channel][row][col] = A^T M A
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -1721,9 +1753,6 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
           o[r][a][1] = w[a][1] - w[a][2] - w[a][3];
         }
       }
-      const int ox = (int)(tt % Tw);
-      const long long rq = tt / Tw;
-      const int oy = (int)(rq % Th), on = (int)(rq / Th);
       const float bsv[4] = {bias.x, bias.y, bias.z, bias.w};
       const float scv[4] = {bsc.x, bsc.y, bsc.z, bsc.w}, shv[4] = {bsh.x, bsh.y, bsh.z, bsh.w};
       const float muv[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, isv[4] = {bis.x, bis.y, bis.z, bis.w};
@@ -1736,27 +1765,12 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
           const int x = 2 * ox + bb;
           if (x >= g.Wg) continue;
           const size_t idx = ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol;
-          float yv[4] = {0.f, 0.f, 0.f, 0.f};
-          if (bwd_mask) {
-            const float4 y4 = ld4(e.yref + idx);
-            yv[0] = y4.x; yv[1] = y4.y; yv[2] = y4.z; yv[3] = y4.w;
-          }
+          const float4 yq = bwd_mask ? y4[a * 2 + bb] : make_float4(0.f, 0.f, 0.f, 0.f);
+          const float yv[4] = {yq.x, yq.y, yq.z, yq.w};
           float v[4];
 #pragma unroll
-          for (int r = 0; r < 4; ++r) {
-            v[r] = o[r][a][bb] + bsv[r];
-            if (bwd_mask) {
-              v[r] = fmaf(yv[r], scv[r], shv[r]) > 0.f ? v[r] : 0.f;
-              s1[r] += v[r];
-              s2[r] += v[r] * ((yv[r] - muv[r]) * isv[r]);
-            } else if (e.stats) {
-              s1[r] += v[r];
-              s2[r] += v[r] * v[r];
-            } else if (second && e.colsum1) {
-              s1[r] += v[r];
-            }
-            if (e.relu) v[r] = fmaxf(v[r], 0.f);
-          }
+          for (int r = 0; r < 4; ++r) v[r] = wf_epi(o[r][a][bb] + bsv[r], yv[r], scv[r], shv[r], muv[r], isv[r],
+                                                     bwd_mask, e.relu, s1[r], s2[r]);
           st4(dptr + idx, make_float4(v[0], v[1], v[2], v[3]));
         }
       }
