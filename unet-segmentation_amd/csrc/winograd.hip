@@ -1272,8 +1272,14 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
   // this thread's three output rows 3 hf .. 3 hf + 2 of the transformed patch
   float* const ubase = Us + (3 * hf) * 6 * PU + lt * 8 + wf8_slot(lt, lc & 3) + (lc >> 2);
   float raw[18];  // [row 0..5][column 3 hf + 0..2]
-  float4 vr[9];
+  float sc = 1.f, sh = 0.f;  // the chunk's producer BN+ReLU (loaded with raw)
   const int nk = g.Cg >> 3;
+  // V (the chunk's 36 x 64 x 8 transformed weights, 2 KB contiguous per point
+  // in k_wino4f_w8's layout) goes global -> LDS by DMA, 9 x 1 KB per wave,
+  // during the input transform (round 4; through registers it held 36 VGPRs of
+  // a kernel at the 256 limit)
+  const unsigned long long vbase = uniform_u64(V);
+  const unsigned vlds = (unsigned)(size_t)(lds_u8_t*)lds + (unsigned)(36 * PU * 4);
   auto load = [&](int kc) {
     const bool second = kc * 8 >= g.c_split;  // c_split % 8 == 0: uniform source
     const float* sp = second ? g.s[1].ptr : g.s[0].ptr;
@@ -1281,6 +1287,11 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
     const int sC = second ? g.s[1].C : g.s[0].C;
     const int soy = second ? g.s[1].oy : g.s[0].oy, sox = second ? g.s[1].ox : g.s[0].ox;
     const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    const float* scp = second ? g.s[1].scale : g.s[0].scale;
+    if (scp) {
+      sc = scp[cl];
+      sh = (second ? g.s[1].shift : g.s[0].shift)[cl];
+    }
     const char* sb = reinterpret_cast<const char*>(sp);
     const unsigned o0 = ((unsigned)((img * sH + 4 * ty + soy) * sW + 4 * tx + sox) * sC + cl) * 4u;
     const unsigned rs = (unsigned)sW * sC * 4u, cs = (unsigned)sC * 4u;
@@ -1300,17 +1311,20 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
           raw[yy * 3 + xx] = *reinterpret_cast<const float*>(
               sb + (o0 + (min((unsigned)yy, lr) * rs + min((unsigned)(3 * hf + xx), lcn) * cs)));
     }
-    const char* vb = reinterpret_cast<const char*>(V + ((size_t)kc * 36 * N + n0) * 8);
-    const unsigned vo = ((unsigned)(tid >> 7) * N * 8u + (tid & 127) * 4u) * 4u;
-    const unsigned vstep = 4u * N * 8u * 4u;  // 4 points per 512 float4
-#pragma unroll
-    for (int j = 0; j < 9; ++j) vr[j] = *reinterpret_cast<const float4*>(vb + (vo + j * vstep));
   };
   auto commit = [&](int kc) {
     const bool second = kc * 8 >= g.c_split;
     const float* scp = second ? g.s[1].scale : g.s[0].scale;
-    const float* shp = second ? g.s[1].shift : g.s[0].shift;
-    const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    // raw(kc) and its BN coefficients (issued a whole MFMA phase ago): retired
+    // by a wait the compiler sees, so nothing it tracks is pending behind the
+    // V DMAs queued next (in-order vmcnt: a later wait would cover them)
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int pc = wave + 8 * j;  // 1-KB piece: point pc >> 1, half pc & 1
+      dma_sv((unsigned)((((size_t)kc * 36 + (pc >> 1)) * N + n0) * 32) + (unsigned)((pc & 1) * 1024 + lane * 16),
+             vbase, vlds + (unsigned)((pc >> 1) * PV * 4 + (pc & 1) * 1024));
+    }
     if constexpr (ABL & 1) {
 #pragma unroll
       for (int a = 0; a < 3; ++a)
@@ -1318,7 +1332,6 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
         for (int bb = 0; bb < 6; ++bb) ubase[(a * 6 + bb) * PU] = raw[a * 6 + bb];
     } else {
     if (scp) {
-      const float sc = scp[cl], sh = shp[cl];
 #pragma unroll
       for (int q = 0; q < 18; ++q) raw[q] = fmaxf(fmaf(raw[q], sc, sh), 0.f);
     }
@@ -1356,11 +1369,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
       for (int bb = 0; bb < 6; ++bb) ubase[(a * 6 + bb) * PU] = rr[bb];
     }
     }
-#pragma unroll
-    for (int j = 0; j < 9; ++j) {
-      const int q = tid + 512 * j;
-      st4(Vs + (q >> 7) * PV + (q & 127) * 4, vr[j]);
-    }
+    vm_wait<0>();  // V(kc) landed (the DMAs are asm: invisible to the compiler's counts)
   };
 
   // ---- MFMA role: wave = (tile half th, 16-channel block cb), all 36 points ----
@@ -1606,8 +1615,12 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
   const bool wfull = __all(vrows == 4 && vcols == 4);
   float* const ubase = Us + lt * 8 + wf8_slot(lt, lc & 3) + (lc >> 2);
   float raw[16];
-  float4 vr[4];
+  float sc = 1.f, sh = 0.f;  // the chunk's producer BN+ReLU (loaded with raw)
   const int nk = g.Cg >> 3;
+  // V (16 points x 2 KB per chunk) by LDS-DMA during the input transform,
+  // 4 x 1 KB per wave (as k_wino4f64)
+  const unsigned long long vbase = uniform_u64(V);
+  const unsigned vlds = (unsigned)(size_t)(lds_u8_t*)lds + (unsigned)(16 * PU * 4);
   auto load = [&](int kc) {
     const bool second = kc * 8 >= g.c_split;  // c_split % 8 == 0: uniform source
     const float* sp = second ? g.s[1].ptr : g.s[0].ptr;
@@ -1615,6 +1628,11 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
     const int sC = second ? g.s[1].C : g.s[0].C;
     const int soy = second ? g.s[1].oy : g.s[0].oy, sox = second ? g.s[1].ox : g.s[0].ox;
     const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    const float* scp = second ? g.s[1].scale : g.s[0].scale;
+    if (scp) {
+      sc = scp[cl];
+      sh = (second ? g.s[1].shift : g.s[0].shift)[cl];
+    }
     const char* sb = reinterpret_cast<const char*>(sp);
     const unsigned o0 = ((unsigned)((img * sH + 2 * ty + soy) * sW + 2 * tx + sox) * sC + cl) * 4u;
     const unsigned rs = (unsigned)sW * sC * 4u, cs = (unsigned)sC * 4u;
@@ -1633,19 +1651,18 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
           raw[yy * 4 + xx] = *reinterpret_cast<const float*>(
               sb + (o0 + (min((unsigned)yy, lr) * rs + min((unsigned)xx, lcn) * cs)));
     }
-    const char* vb = reinterpret_cast<const char*>(V + ((size_t)kc * 16 * N + n0) * 8);
-    const unsigned vo = ((unsigned)(tid >> 7) * N * 8u + (tid & 127) * 4u) * 4u;
-    const unsigned vstep = 4u * N * 8u * 4u;  // 4 points per 512 float4
-#pragma unroll
-    for (int j = 0; j < 4; ++j) vr[j] = *reinterpret_cast<const float4*>(vb + (vo + j * vstep));
   };
   auto commit = [&](int kc) {
     const bool second = kc * 8 >= g.c_split;
     const float* scp = second ? g.s[1].scale : g.s[0].scale;
-    const float* shp = second ? g.s[1].shift : g.s[0].shift;
-    const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // raw(kc), sc, sh: retired visibly before the DMAs queue
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int pc = wave + 8 * j;  // 1-KB piece: point pc >> 1, half pc & 1
+      dma_sv((unsigned)((((size_t)kc * 16 + (pc >> 1)) * N + n0) * 32) + (unsigned)((pc & 1) * 1024 + lane * 16),
+             vbase, vlds + (unsigned)((pc >> 1) * PV * 4 + (pc & 1) * 1024));
+    }
     if (scp) {
-      const float sc = scp[cl], sh = shp[cl];
 #pragma unroll
       for (int q = 0; q < 16; ++q) raw[q] = fmaxf(fmaf(raw[q], sc, sh), 0.f);
     }
@@ -1669,11 +1686,7 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
       ubase[(a * 4 + 2) * PU] = ev[a][2] - ev[a][1];
       ubase[(a * 4 + 3) * PU] = ev[a][1] - ev[a][3];
     }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int q = tid + 512 * j;
-      st4(Vs + (q >> 7) * PV + (q & 127) * 4, vr[j]);
-    }
+    vm_wait<0>();  // V(kc) landed
   };
 
   // ---- MFMA role: wave = (tile quarter th, channel half ch), all 16 points ----
