@@ -12,10 +12,13 @@ for p in (ROOT, PKG, HERE):
 # the GEMM choices bench.py timed (bench.py --tune-db-out); full-size tests load
 # them so that they check the benchmarked kernel mix
 TUNE_DB = os.path.join(ROOT, "profiles", "tune_db.txt")
+# per test module that loaded the database: (module, entries, misses, missed keys),
+# written to the terminal summary (fixture output is captured by pytest)
+_TUNE_REPORT = []
 
 
 @pytest.fixture(scope="module")
-def bench_tuning():
+def bench_tuning(request):
     """Load profiles/tune_db.txt into the library's tuning cache (shapes it does
     not hold are tuned live); reset the cache afterwards."""
     import torch
@@ -32,7 +35,15 @@ def bench_tuning():
     # GEMM shapes these tests met that the database did not hold (tuned live)
     live = [ln.split(" | ")[0] for ln in _lib.tuning_report().splitlines() if ln and "tuning db" not in ln]
     print(f"\ntuning database misses (shapes tuned live): {len(live)}" + "".join(f"\n  {k}" for k in live))
+    _TUNE_REPORT.append((request.module.__name__, n, live))
     lib.unet_tuning_reset()
+
+
+def pytest_terminal_summary(terminalreporter):
+    for mod, n, live in _TUNE_REPORT:
+        terminalreporter.write_line(f"{mod}: tuning database {n} entries, misses (shapes tuned live): {len(live)}")
+        for k in live:
+            terminalreporter.write_line(f"    {k}")
 
 
 def pytest_configure(config):
