@@ -1403,6 +1403,70 @@ hipError_t launch_pack_convT(const float* w, int ci, int co, float* wf, float* w
   return hipGetLastError();
 }
 
+// Every per-step weight repack of a forward in ONE launch (round 4; it was 2
+// launches per layer, 42 small-grid kernels in front of every forward): block =
+// (job, 32 x 32 channel tile).  Conv jobs: W[co][ci][9] (OIHW) -> wf[co][t][ci]
+// (forward B operand) and wd[ci*9 + 8-t][co] (input-gradient B operand, taps
+// flipped); convT jobs: W[ci][co][4] -> wd[ci][ab][co] and wf[ab*co + c][ci].
+// The tile goes through LDS (rows padded by one word: conflict-free transposed
+// reads), every global access is a 128-B run.
+__global__ __launch_bounds__(256) void k_pack_all(const PackJobs jobs) {
+  __shared__ float t[32 * 289];
+  int j = 0;
+  while (j + 1 < jobs.n && (int)blockIdx.x >= jobs.first[j + 1]) ++j;
+  const PackJob& J = jobs.j[j];
+  const int b = blockIdx.x - jobs.first[j];
+  const int tid = threadIdx.x;
+  if (J.kind == 0) {  // conv 3x3
+    const int CI = J.ci, CO = J.co, nct = CI / 32;
+    const int co0 = (b / nct) * 32, ci0 = (b % nct) * 32;
+    for (int i = tid; i < 32 * 288; i += 256) {
+      const int r = i / 288, q = i - r * 288;  // q = ci_l * 9 + tap
+      t[r * 289 + q] = J.w[((size_t)(co0 + r) * CI + ci0) * 9 + q];
+    }
+    __syncthreads();
+    for (int i = tid; i < 32 * 9 * 32; i += 256) {  // wf: ci fastest
+      const int c = i & 31, rt = i >> 5, r = rt / 9, tp = rt - r * 9;
+      J.wf[((size_t)(co0 + r) * 9 + tp) * CI + ci0 + c] = t[r * 289 + c * 9 + tp];
+    }
+    if (J.wd)
+      for (int i = tid; i < 32 * 9 * 32; i += 256) {  // wd: co fastest
+        const int r = i & 31, ct = i >> 5, c = ct / 9, tp = ct - c * 9;
+        J.wd[((size_t)(ci0 + c) * 9 + 8 - tp) * CO + co0 + r] = t[r * 289 + c * 9 + tp];
+      }
+  } else {  // convT 2x2 stride 2
+    const int CI = J.ci, CO = J.co, nct = CO / 32;
+    const int ci0 = (b / nct) * 32, co0 = (b % nct) * 32;
+    for (int i = tid; i < 32 * 128; i += 256) {
+      const int r = i >> 7, q = i & 127;  // q = co_l * 4 + ab
+      t[r * 129 + q] = J.w[((size_t)(ci0 + r) * CO + co0) * 4 + q];
+    }
+    __syncthreads();
+    for (int i = tid; i < 32 * 4 * 32; i += 256) {  // wd[ci][ab][co]: co fastest
+      const int c = i & 31, ra = i >> 5, r = ra >> 2, ab = ra & 3;
+      J.wd[((size_t)(ci0 + r) * 4 + ab) * CO + co0 + c] = t[r * 129 + c * 4 + ab];
+    }
+    for (int i = tid; i < 32 * 4 * 32; i += 256) {  // wf[ab*CO + co][ci]: ci fastest
+      const int r = i & 31, ac = i >> 5, ab = ac >> 5, c = ac & 31;
+      J.wf[((size_t)ab * CO + co0 + c) * CI + ci0 + r] = t[r * 129 + c * 4 + ab];
+    }
+  }
+}
+
+hipError_t launch_pack_all(PackJobs jobs, hipStream_t s) {
+  int blocks = 0;
+  for (int j = 0; j < jobs.n; ++j) {
+    const PackJob& J = jobs.j[j];
+    if (J.ci % 32 || J.co % 32 || !J.w || !J.wf || (J.kind == 1 && !J.wd)) return hipErrorInvalidValue;
+    jobs.first[j] = blocks;
+    blocks += (J.ci / 32) * (J.co / 32);
+  }
+  if (jobs.n <= 0 || jobs.n > kPackJobsMax) return hipErrorInvalidValue;
+  jobs.first[jobs.n] = blocks;
+  hipLaunchKernelGGL(k_pack_all, dim3(blocks), dim3(256), 0, s, jobs);
+  return hipGetLastError();
+}
+
 __global__ void k_fill(float* p, size_t n, float v) {
   for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
 }

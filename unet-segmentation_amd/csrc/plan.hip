@@ -274,7 +274,7 @@ constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 // Version of the GEMM variant tables (tile ids and their kernels): part of every
 // tuning key, so a database written by a build with another tile set is never
 // replayed (its lines simply miss).  Bump whenever a tile id changes meaning.
-constexpr int kTileTableVersion = 8;
+constexpr int kTileTableVersion = 9;
 
 std::string igemm_key(const IgemmArgs& a) {
   char b[240], small[16] = "";
@@ -325,7 +325,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
                 36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 81, 82, 83, 84, 70, 71, 72, 73,
-                74, 75}) {  // fits() filters by precision and gather
+                74, 75, 88}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t) || tune_skipped(t)) continue;
     v.push_back({t, 1});
     if (t == 70 || t == 71 || t == 74)  // Winograd: no K split; the tile of its batched point GEMMs
@@ -617,14 +617,16 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
   // ---- repack weights (per call: the optimizer moves them every step) ----
   {
     Timer t(p, s, UNET_KC_ELEMWISE, 0, 0);
+    PackJobs jobs{};
     for (int l = 1; l < 18; ++l) {
       Conv& L = p->L[l];
-      CK(launch_pack_conv(P<float>(prm, L.pw), L.co, L.ci, 3, 3, c.f(L.wf), train ? c.f(L.wd) : nullptr, s));
+      jobs.j[jobs.n++] = PackJob{P<float>(prm, L.pw), c.f(L.wf), train ? c.f(L.wd) : nullptr, L.co, L.ci, 0};
     }
     for (int k = 0; k < 4; ++k) {
       ConvT& T = p->T[k];
-      CK(launch_pack_convT(P<float>(prm, T.pw), T.ci, T.co, c.f(T.wf), c.f(T.wd), s));
+      jobs.j[jobs.n++] = PackJob{P<float>(prm, T.pw), c.f(T.wf), c.f(T.wd), T.co, T.ci, 1};
     }
+    CK(launch_pack_all(jobs, s));
     if (!train) {  // BatchNorm from the running statistics (scripts/predict.py:70 model.eval())
       for (int l = 0; l < 18; ++l) {
         Conv& L = p->L[l];

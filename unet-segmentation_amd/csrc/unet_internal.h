@@ -153,9 +153,11 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
 bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch);
 hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);
 // bf16 3x3 conv with LDS-DMA halo / weight rings (conv3_ring.hip), tile ids 81-84
+// (88: the geometry of 84, persistent)
 bool conv3_ring_tile_shape(int tile, int& th, int& bn, int& ck);
 bool conv3_ring_fits(const IgemmArgs& a, int tile);
 hipError_t go_conv3_ring_tile(const IgemmArgs& a, hipStream_t s, int tile);
+hipError_t go_conv3_ring_pt(const IgemmArgs& a, hipStream_t s, int tile);  // conv3_ring_pt.hip (88)
 int num_cus();
 
 // Timing-ablation switches (UNET_WG_ABL, UNET_WF_ABL, UNET_WF64_ABL: kernel
@@ -290,6 +292,20 @@ hipError_t launch_scale_by_dev(const float* x, float* y, size_t n, const float* 
 hipError_t launch_pack_conv(const float* w_oihw, int co, int ci, int kh, int kw, float* wf,
                             float* wd, hipStream_t s);
 hipError_t launch_pack_convT(const float* w, int ci, int co, float* wf, float* wd, hipStream_t s);
+// all of a forward's conv / convT weight repacks in one launch (k_pack_all)
+struct PackJob {
+  const float* w;  // conv: W[co][ci][9] (OIHW); convT: W[ci][co][4]
+  float* wf;       // conv: [co][9][ci]; convT: [4*co][ci]
+  float* wd;       // conv: [ci*9 + 8-t][co] (nullptr: eval, not needed); convT: [ci][4][co]
+  int co, ci, kind;  // kind 0 conv 3x3, 1 convT 2x2 s2; co, ci multiples of 32
+};
+constexpr int kPackJobsMax = 24;
+struct PackJobs {
+  PackJob j[kPackJobsMax];
+  int first[kPackJobsMax + 1];
+  int n;
+};
+hipError_t launch_pack_all(PackJobs jobs, hipStream_t s);
 // out[a][c][b] = in[a][b][c]
 hipError_t launch_permute_last2(const float* in, int A, int B, int C, float* out, hipStream_t s);
 // column sums over rows: out[c] = sum_r in[r][c] via double groups
