@@ -1,5 +1,6 @@
-// k_conv3_ring tiles 81-84 and the ring tile table (kernel: conv3_ring_kernel.h;
-// the persistent tile 88 is built in conv3_ring_pt.hip).
+// k_conv3_ring tiles 81, 82 and the ring tile table (kernel:
+// conv3_ring_kernel.h; tiles 83, 84 and the persistent 88 are instantiated in
+// conv3_ring_pt.hip, a second translation unit that compiles in parallel).
 #include "conv3_ring_kernel.h"
 
 namespace unet {
@@ -46,9 +47,7 @@ hipError_t go_conv3_ring_tile(const IgemmArgs& a, hipStream_t s, int tile) {
   switch (tile) {
     case 81: return go_ring<8, 128, 4, 2, 64, 2, 0>(a, s);
     case 82: return go_ring<8, 64, 4, 1, 32, 2, 0>(a, s);
-    case 83: return go_ring<4, 128, 2, 2, 32, 2, 0>(a, s);
-    case 84: return go_ring<8, 64, 8, 1, 64, 2, 0>(a, s);
-    case 88: return go_conv3_ring_pt(a, s, tile);
+    case 83: case 84: case 88: return go_conv3_ring_pt(a, s, tile);
     default: return hipErrorInvalidValue;
   }
 }

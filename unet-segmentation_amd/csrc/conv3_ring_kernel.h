@@ -86,7 +86,6 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int h = lane >> 5, l = lane & 31;
   const Gather& g = args.a;
   const int Cg = g.Cg, K = args.K, Hg = g.Hg, Wg = g.Wg;
   const int tiles_x = (Wg + 31) / 32, tiles_y = (Hg + TH - 1) / TH;
