@@ -9,10 +9,6 @@ namespace unet {
 // TH x 32 pixels x BN columns, CK-channel chunks
 bool conv3_ring_tile_shape(int tile, int& th, int& bn, int& ck) {
   if (tile == 88) tile -= 4;
-  if (tile == 89) {  // 8 waves (4 x 2), 32 x 32 per wave; 9 resident weight slabs; 127 KB, 1 WG/CU
-    th = 4; bn = 64; ck = 64;
-    return true;
-  }
   switch (tile) {
     case 81: th = 8; bn = 128; ck = 64; return true;  // 8 waves (4 x 2), 64 x 64 per wave; 138 KB, 1 WG/CU
     case 82: th = 8; bn = 64; ck = 32; return true;   // 4 waves (4 x 1), 64 x 64 per wave; 57 KB, 2 WG/CU
@@ -37,11 +33,9 @@ bool conv3_ring_fits(const IgemmArgs& a, int tile) {
     case 81: smem = ring_smem<8, 128, 64>(a, xtf); break;
     case 82: smem = ring_smem<8, 64, 32>(a, xtf); break;
     case 83: smem = ring_smem<4, 128, 32>(a, xtf); break;
-    case 89: smem = ring_smem<4, 64, 64, 9>(a, xtf); break;
     default: smem = ring_smem<8, 64, 64>(a, xtf); break;
   }
-  if ((tile == 88 || tile == 89) && a.ksplit > 1) return false;
-  if (tile == 89 && g.Cg != ck) return false;  // weights resident: one chunk
+  if (tile == 88 && a.ksplit > 1) return false;
   return a.bh != nullptr && a.bl == nullptr && a.N % bn == 0 && g.taps_h == 3 && g.taps_w == 3 && g.stride == 1 &&
          a.K == 9 * g.Cg && g.Cg % ck == 0 && g.c_split % ck == 0 && g.s[0].h16 &&
          (!two || (g.s[1].h16 && g.s[1].scale == nullptr)) && (!xtf || g.s[0].shift != nullptr) &&
@@ -53,7 +47,7 @@ hipError_t go_conv3_ring_tile(const IgemmArgs& a, hipStream_t s, int tile) {
   switch (tile) {
     case 81: return go_ring<8, 128, 4, 2, 64, 2, 0>(a, s);
     case 82: return go_ring<8, 64, 4, 1, 32, 2, 0>(a, s);
-    case 83: case 84: case 88: case 89: return go_conv3_ring_pt(a, s, tile);
+    case 83: case 84: case 88: return go_conv3_ring_pt(a, s, tile);
     default: return hipErrorInvalidValue;
   }
 }

@@ -50,7 +50,7 @@
 namespace unet {
 
 typedef __bf16 bf16x8r_t __attribute__((ext_vector_type(8)));
-template <int TH, int BN, int CK, int NWS = 3>
+template <int TH, int BN, int CK>
 struct RingGeo {
   static constexpr int TW = 32, HP = 36, RB = CK * 2, KS = CK / 16;
   static constexpr int RPB = 256 / RB, CPR = RB / 16;  // pixel rows per 256-B bank row, 16-B pieces per row
@@ -58,7 +58,7 @@ struct RingGeo {
   static constexpr int PH = (TH + 2) * HP;             // halo pixel rows (36-pixel pitch)
   static constexpr int IH = (PH * RB + 1023) / 1024;   // halo DMA instructions per chunk
   static constexpr int HSZ = IH * 1024;
-  static constexpr int H0 = NWS * WSZ;                 // LDS: NWS weight slots, then 2 halo slots
+  static constexpr int H0 = 3 * WSZ;                   // LDS: 3 weight slots, then 2 halo slots
   // + 1 KB junk target: the tap steps past the halo's last piece re-issue a
   // DMA only to keep the per-step vmcnt arithmetic uniform; landing in a halo
   // slot it would overwrite bytes transformed in place meanwhile (XTF)
@@ -68,19 +68,14 @@ struct RingGeo {
 
 template <int TH, int BN, int WM, int WN, int CK, int TWO, int MINW, int XTF, int PT>
 __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmArgs args) {
-  // PT 2 (weights resident, tile 89): single-chunk GEMMs (Cg == CK) keep all
-  // 9 taps' weight slabs in LDS for the workgroup's lifetime and stream only
-  // the halo ring -- for the 64-channel layers the 3-slot weight ring re-read
-  // 9 x BN x 128 B per pixel tile, more LDS-DMA bytes than the halo itself
-  constexpr bool WR = PT == 2;
-  using G = RingGeo<TH, BN, CK, WR ? 9 : 3>;
+  using G = RingGeo<TH, BN, CK>;
   constexpr int HP = G::HP, RB = G::RB, KS = G::KS, RPB = G::RPB, CPR = G::CPR;
   constexpr int WSZ = G::WSZ, IH = G::IH, HSZ = G::HSZ, H0 = G::H0, PH = G::PH;
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int TM = TH / WM, TN = BN / (WN * 32);
   constexpr int IW = WSZ / 1024, IWW = IW / NW;  // weight DMAs per tap step: total, per wave
   constexpr int NHS = (IH + NW - 1) / NW;        // halo DMAs per wave per chunk (one per tap step)
-  constexpr int D = WR ? 1 : IWW + 1;            // DMAs per wave per tap step
+  constexpr int D = IWW + 1;                     // DMAs per wave per tap step
   static_assert(TH % WM == 0 && TM >= 1 && TN >= 1 && IW % NW == 0 && IWW >= 1, "tile");
   static_assert(NHS <= 7, "the next chunk's halo must be issued >= 2 tap steps before it is read");
   static_assert(HSZ + (TM + 1) * HP * RB < 65536, "halo fragment offsets must fit the ds_read immediate");
@@ -234,7 +229,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
   // read while this one's MFMAs issue
   auto tap_mfma = [&](auto HSc, auto Tc, auto&& after) {
     constexpr int hs = decltype(HSc)::value, t = decltype(Tc)::value;
-    constexpr int ky = t / 3, kx = t % 3, ws = WR ? t : t % 3;
+    constexpr int ky = t / 3, kx = t % 3, ws = t % 3;
     bf16x8r_t fa[2][TM], fb[2][TN];
     auto rd = [&](auto Sc, int b) {
       constexpr int s = decltype(Sc)::value;
@@ -321,7 +316,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
 #pragma unroll
         for (int u = 0; u < D; ++u) {
           if (u == k || (k == KS - 1 && u > k)) {
-            if (!WR && u < IWW) issue_w1(cw, tw, (t + 2) % 3, u);
+            if (u < IWW) issue_w1(cw, tw, (t + 2) % 3, u);
             else issue_h(cn, t < NHS ? t : NHS - 1, t < NHS ? hs ^ 1 : -1, wr);
           }
         }
@@ -343,13 +338,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
     // prologue: chunk kc0's halo, the weights of its taps 0 and 1
 #pragma unroll
     for (int k = 0; k < NHS; ++k) issue_h(kc0, k, 0, false);
-    if constexpr (WR) {
-#pragma unroll
-      for (int t = 0; t < 9; ++t) issue_w(kc0, t, t);
-    } else {
-      issue_w(kc0, 0, 0);
-      issue_w(kc0, 1, 1);
-    }
+    issue_w(kc0, 0, 0);
+    issue_w(kc0, 1, 1);
     vm_wait<0>();
     if constexpr (XTF) {
       __syncthreads();  // the halo (and the BN table) visible to every wave
@@ -407,10 +397,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
 }
 
 // the LDS image of a launch: the ring, plus the BN table of source 0 (XTF)
-template <int TH, int BN, int CK, int NWS = 3>
+template <int TH, int BN, int CK>
 static size_t ring_smem(const IgemmArgs& a, bool xtf) {
   const Gather& g = a.a;
-  return RingGeo<TH, BN, CK, NWS>::smem + (xtf ? 8 * (size_t)(g.c_split < g.Cg ? g.c_split : g.Cg) : 0);
+  return RingGeo<TH, BN, CK>::smem + (xtf ? 8 * (size_t)(g.c_split < g.Cg ? g.c_split : g.Cg) : 0);
 }
 
 static int ring_num_cus() {
@@ -434,7 +424,7 @@ static hipError_t go_ring(const IgemmArgs& a, hipStream_t s) {
                         reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 1, MINW, 0, PT>),
                         reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 0, MINW, 1, PT>),
                         reinterpret_cast<const void*>(&k_conv3_ring<TH, BN, WM, WN, CK, 1, MINW, 1, PT>)};
-  const size_t smem = ring_smem<TH, BN, CK, PT == 2 ? 9 : 3>(a, xtf);
+  const size_t smem = ring_smem<TH, BN, CK>(a, xtf);
   if (!attr[v]) {  // the largest image any launch of this variant can ask for
     hipError_t e = hipFuncSetAttribute(fns[v], hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     if (e != hipSuccess) return e;

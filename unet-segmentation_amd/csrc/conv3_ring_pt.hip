@@ -1,6 +1,4 @@
-// Ring tiles 83, 84, the weights-resident 89 (PT = 2: single-chunk GEMMs, all
-// 9 tap slabs in LDS for the workgroup's lifetime, only the halo ring
-// streamed) and the persistent 88 (k_conv3_ring PT = 1, the geometry
+// Ring tiles 83, 84 and the persistent 88 (k_conv3_ring PT = 1, the geometry
 // of 84: each workgroup walks pixel tiles with the next tile's halo and first
 // weights in flight during this tile's last chunk and epilogue), a second
 // translation unit so the ring instantiations compile in two halves in
@@ -17,7 +15,6 @@ hipError_t go_conv3_ring_pt(const IgemmArgs& a, hipStream_t s, int tile) {
     case 83: return go_ring<4, 128, 2, 2, 32, 2, 0>(a, s);
     case 84: return go_ring<8, 64, 8, 1, 64, 2, 0>(a, s);
     case 88: return go_ring<8, 64, 8, 1, 64, 2, 1>(a, s);
-    case 89: return go_ring<4, 64, 4, 2, 64, 1, 2>(a, s);
     default: return hipErrorInvalidValue;
   }
 }

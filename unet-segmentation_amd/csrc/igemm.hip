@@ -1170,7 +1170,6 @@ static TileInfo tile_info(int id) {
     case 84: return {256, 64, 576, 1};
     // 84 persistent (k_conv3_ring PT): whole K per workgroup
     case 88: return {256, 64, 576, 1};
-    case 89: return {128, 64, 576, 1};  // weights resident (PT 2), single chunk
     // Winograd F(2x2, 3x3) (winograd.hip): no K split
     case 70: case 71: case 74: return {256, 64, 9, 2};
     case 72: return {32, 32, 16, 1};
@@ -1187,7 +1186,7 @@ static TileInfo tile_info(int id) {
 
 static bool is_halo_tile(int tile) { return (tile >= 31 && tile <= 36) || (tile >= 41 && tile <= 44); }
 static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 68); }
-static bool is_ring_tile(int tile) { return (tile >= 81 && tile <= 84) || tile == 88 || tile == 89; }
+static bool is_ring_tile(int tile) { return (tile >= 81 && tile <= 84) || tile == 88; }
 static bool is_bf16_tile(int tile) {
   return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile);
 }
@@ -1309,7 +1308,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 31: case 32: case 33: case 34: case 35: case 36:
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
     case 63: case 65: case 66: case 67: case 68: return go_conv3_dma_tile(a, s, tile);
-    case 81: case 82: case 83: case 84: case 88: case 89: return go_conv3_ring_tile(a, s, tile);
+    case 81: case 82: case 83: case 84: case 88: return go_conv3_ring_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);
     case 71: return launch_wino(a, s, 4);
     case 74: return launch_wino(a, s, 6);

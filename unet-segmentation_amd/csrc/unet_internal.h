@@ -157,7 +157,7 @@ hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);
 bool conv3_ring_tile_shape(int tile, int& th, int& bn, int& ck);
 bool conv3_ring_fits(const IgemmArgs& a, int tile);
 hipError_t go_conv3_ring_tile(const IgemmArgs& a, hipStream_t s, int tile);
-hipError_t go_conv3_ring_pt(const IgemmArgs& a, hipStream_t s, int tile);  // conv3_ring_pt.hip (83, 84, 88, 89)
+hipError_t go_conv3_ring_pt(const IgemmArgs& a, hipStream_t s, int tile);  // conv3_ring_pt.hip (83, 84, 88)
 int num_cus();
 
 // Timing-ablation switches (UNET_WG_ABL, UNET_WF_ABL, UNET_WF64_ABL: kernel
