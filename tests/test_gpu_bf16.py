@@ -430,6 +430,8 @@ def gemm_mode(request, lib):
                                        "norm+tile31", "norm+heuristic", "tile81", "tile82", "tile83", "tile84",
                                        "tile88", "norm+tile88",
                                        "tile81+split3", "heuristic+wtile26", "heuristic+wtile27",
+                                       "heuristic+wtile126", "heuristic+wtile130", "heuristic+wtile132",
+                                       "heuristic+wtile110", "heuristic+wtile112",
                                        "heuristic+wtile28", "heuristic+wtile29", "heuristic+wtile30",
                                        "heuristic+wtile31", "heuristic+wtile32", "heuristic+wtile33",
                                        "norm+heuristic+wtile26"],

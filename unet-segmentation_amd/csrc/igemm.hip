@@ -1045,7 +1045,10 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
     if (more) commit(cur ^ 1);
     __syncthreads();
   }
-  // accumulate the tile into out (fp32 atomics; the output is small next to the reduction)
+  // accumulate the tile into out (fp32 atomics; the output is small next to the
+  // reduction), or (slab mode, batch 1) store this split's partial for
+  // launch_slab_reduce
+  float* const plane = args.slab ? args.slab + (size_t)blockIdx.z * args.Mo * args.No : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1054,7 +1057,8 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
       for (int r = 0; r < 16; ++r) {
         const int row = i0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = j0 + wn * TN * 32 + j * 32 + li;
-        atomicAdd(args.out + zb * args.batch_out + (size_t)row * args.No + col, acc[i][j][r]);
+        if (plane) plane[(size_t)row * args.No + col] = acc[i][j][r];
+        else atomicAdd(args.out + zb * args.batch_out + (size_t)row * args.No + col, acc[i][j][r]);
       }
 }
 
@@ -1414,6 +1418,13 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   int tile = c.tile;
   if (tile < 0 && a.bf16) {
     if (g_tune_wgrad >= 10 && wgrad_tile_fits(a, g_tune_wgrad)) tile = g_tune_wgrad;  // forced (tests)
+    else if (g_tune_wgrad >= 126 && g_tune_wgrad <= 133 && wgrad_tile_fits(a, g_tune_wgrad - 100)) {
+      tile = g_tune_wgrad - 100;  // forced ring tile in slab mode (tests)
+      c.split = 11;
+    } else if (g_tune_wgrad >= 110 && g_tune_wgrad <= 114 && wgrad_tile_fits(a, g_tune_wgrad - 100)) {
+      c.tile = tile = g_tune_wgrad - 100;  // forced pixel-column tile in slab mode, 2 per CU (tests)
+      c.split = 102;
+    }
     else if (wgrad3_fits(a)) tile = 20;
     else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 10;
     else if (a.No % 128 == 0) tile = 12;
@@ -1439,7 +1450,10 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   int bm, bn;
   wgrad_tile(tile, bm, bn);
   const int tiles = (a.Mo / bm) * (a.No / bn) * a.batch;
-  // split the pixel reduction so that the grid has ~`per_cu` workgroups per CU
+  // split the pixel reduction so that the grid has ~`per_cu` workgroups per CU;
+  // codes >= 100: slab mode (plain-store split partials + one reduction pass)
+  const bool slab_mode = c.tile >= 0 && c.split >= 100;
+  if (slab_mode) c.split -= 100;
   const int per_cu = c.tile >= 0 ? (c.split > 0 ? c.split : 8) : (g_tune_wgrad >= 2 ? g_tune_wgrad : 8);
   const int target = per_cu * num_cus();
   int splits = (target + tiles - 1) / tiles;
@@ -1451,16 +1465,26 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   pps = (pps + kq - 1) / kq * kq;
   splits = (a.P + pps - 1) / pps;
   a.pix_per_split = pps;
+  const size_t plane = (size_t)a.Mo * a.No;
+  if (!(slab_mode && a.batch == 1 && splits > 1 && plane % 4 == 0 && a.slab &&
+        (size_t)splits * plane * sizeof(float) <= a.slab_bytes))
+    a.slab = nullptr;
   dim3 grid(a.Mo / bm, a.No / bn, splits * a.batch);
-  if (tile >= 10) return go_wgrad_bf16(a, s, tile, grid);
-  switch (tile) {
-    case 0: hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
-    case 1: hipLaunchKernelGGL((k_wgrad<128, 192, 2, 2>), grid, dim3(256), 0, s, a); break;
-    case 2: hipLaunchKernelGGL((k_wgrad<64, 192, 2, 2>), grid, dim3(256), 0, s, a); break;
-    case 3: hipLaunchKernelGGL((k_wgrad<64, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL((k_wgrad<64, 64, 2, 2>), grid, dim3(256), 0, s, a); break;
+  hipError_t e = hipSuccess;
+  if (tile >= 10) {
+    e = go_wgrad_bf16(a, s, tile, grid);
+  } else {
+    switch (tile) {
+      case 0: hipLaunchKernelGGL((k_wgrad<128, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
+      case 1: hipLaunchKernelGGL((k_wgrad<128, 192, 2, 2>), grid, dim3(256), 0, s, a); break;
+      case 2: hipLaunchKernelGGL((k_wgrad<64, 192, 2, 2>), grid, dim3(256), 0, s, a); break;
+      case 3: hipLaunchKernelGGL((k_wgrad<64, 128, 2, 2>), grid, dim3(256), 0, s, a); break;
+      default: hipLaunchKernelGGL((k_wgrad<64, 64, 2, 2>), grid, dim3(256), 0, s, a); break;
+    }
+    e = hipGetLastError();
   }
-  return hipGetLastError();
+  if (e != hipSuccess || !a.slab) return e;
+  return launch_slab_reduce(a.slab, splits, plane, a.out, s);
 }
 
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad_v(a, s, GemmChoice{}); }

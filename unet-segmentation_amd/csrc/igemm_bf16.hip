@@ -742,7 +742,9 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
     if (more) commit(cur ^ 1);
     __syncthreads();
   }
-  // accumulate the tile into out (fp32 atomics; the output is small next to the reduction)
+  // accumulate the tile into out (fp32 atomics; the output is small next to the
+  // reduction), or (slab mode) store this split's partial for launch_slab_reduce
+  float* const plane = args.slab ? args.slab + (size_t)blockIdx.z * args.Mo * args.No : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -751,7 +753,8 @@ __global__ __launch_bounds__(WM * WN * 64, 2) void k_wgrad_bf(const WgradArgs ar
       for (int r = 0; r < 16; ++r) {
         const int row = i0 + wm * TM * 32 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
         const int col = j0 + wn * TN * 32 + j * 32 + li;
-        atomicAdd(args.out + (size_t)row * args.No + col, acc[i][j][r]);
+        if (plane) plane[(size_t)row * args.No + col] = acc[i][j][r];
+        else atomicAdd(args.out + (size_t)row * args.No + col, acc[i][j][r]);
       }
 }
 

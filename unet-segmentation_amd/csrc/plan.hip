@@ -125,6 +125,7 @@ struct unet_plan {
   Buf slab;          // split-K partial tiles (igemm sites the tuner splits)
   Buf wino;          // Winograd F(2x2, 3x3) / F(4x4, 3x3) scratch (fp32 plans; U, M, V of one GEMM)
   Buf wino_w;        // the weight-gradient twin (U, Vd, Mw; backward part of the workspace)
+  Buf wslab;         // split partials of the slab-mode weight gradients (side stream)
   Buf tune_scratch;  // atomic targets of the autotuner's trial launches
   size_t ws_bytes = 0;
   size_t fwd_ws_bytes = 0;  // prefix of the workspace a forward uses (no backward buffers)
@@ -274,7 +275,7 @@ constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 // Version of the GEMM variant tables (tile ids and their kernels): part of every
 // tuning key, so a database written by a build with another tile set is never
 // replayed (its lines simply miss).  Bump whenever a tile id changes meaning.
-constexpr int kTileTableVersion = 9;
+constexpr int kTileTableVersion = 10;
 
 std::string igemm_key(const IgemmArgs& a) {
   char b[240], small[16] = "";
@@ -355,6 +356,10 @@ std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
     }
     if (t >= 24 && t <= 33) {  // wide halo-tiled / LDS-DMA ring: one resident workgroup per CU
       for (int per_cu : {1, 2}) v.push_back({t, per_cu});
+      // ring (26-33) in slab mode: split partials by plain stores + one
+      // reduction pass instead of per-element fp32 atomics
+      if (t >= 26 && a.slab)
+        for (int per_cu : {11, 12}) v.push_back({t, per_cu});
       continue;
     }
     if (t >= 20) {  // halo-tiled: workgroups per CU (2 resident)
@@ -362,8 +367,11 @@ std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
       continue;
     }
     // pixel-split column tiles: fewer splits trade fill for fewer fp32
-    // atomics per output (the short-pixel convT weight gradients)
+    // atomics per output (the short-pixel convT weight gradients); codes
+    // 101-104: the same splits in slab mode (plain-store partials + reduction)
     for (int per_cu : {1, 2, 4, 8, 16}) v.push_back({t, per_cu});
+    if (a.slab && a.batch == 1)
+      for (int per_cu : {101, 102, 104}) v.push_back({t, per_cu});
   }
   return v;
 }
@@ -524,6 +532,10 @@ hipError_t run_wgrad(const Ctx& c, WgradArgs a) {
   if (c.p->wino_w.bytes) {  // fp32 training plans: the Winograd weight-gradient scratch (side stream)
     a.wino_ws = c.f(c.p->wino_w);
     a.wino_ws_bytes = c.p->wino_w.bytes;
+  }
+  if (c.p->wslab.bytes) {  // partial planes of the slab-mode weight gradients (side stream)
+    a.slab = c.f(c.p->wslab);
+    a.slab_bytes = c.p->wslab.bytes;
   }
   const GemmChoice ch = choose_wgrad(c, a);
   if (c.p->timing) c.p->xfl += wgrad_exec_flops(a, ch);
@@ -1235,6 +1247,11 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
     }
     p->wino_w = al.take(wmx);
   }
+  // slab-mode weight gradients (ring tiles 26-33 with per_cu codes 11 / 12,
+  // pixel-column tiles with codes 101-104): one [Mo][No] fp32 plane per pixel
+  // split instead of fp32 atomics; sized for 2 per CU x the largest ring
+  // channel block (128 x 9 x 64); a launch that needs more uses the atomics
+  p->wslab = al.take((size_t)2 * num_cus() * 128 * 9 * 64 * sizeof(float));
   p->ws_bytes = al.top;
   return p;
 }

@@ -107,6 +107,12 @@ struct WgradArgs {
   int P;             // pixels
   int pix_per_split;
   float* out;        // [Mo][No] fp32, accumulated with atomics (zeroed by caller)
+  // optional split-partial slab (bf16 ring weight gradients, wgrad per_cu codes
+  // >= 10): each pixel split stores its [Mo][No] partial with plain stores and
+  // one reduction pass adds them into out -- instead of per_cu x CUs x block
+  // fp32 atomics per launch (~9.4 M for every ring launch at 1 per CU)
+  float* slab = nullptr;
+  size_t slab_bytes = 0;
   int bf16 = 0;      // 1: operands rounded to bf16 when staged (bf16 tiles 10-14)
   int split = 0;     // 1 (with bf16): operands as hi/lo bf16 pairs (UNET_PREC_BF16X3)
   // batched (fp32 tiles 0-4): blockIdx.z = b * splits + split; operand b's
@@ -188,6 +194,8 @@ hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_c
 // ring of pixel tiles (wgrad tiles 26-33, wgrad3_ring.hip)
 bool wgrad3_ring_fits(const WgradArgs& a, int tile);
 hipError_t go_wgrad3_ring(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
+// out[e] += sum_z slab[z][e], e < plane (the slab-mode weight gradients' reduction)
+hipError_t launch_slab_reduce(const float* slab, int splits, size_t plane, float* out, hipStream_t s);
 // wide halo-tiled 3x3 weight gradient with a two-stage ring (wgrad tiles 24, 25)
 bool wgrad3w_fits(const WgradArgs& a, int tile);
 hipError_t go_wgrad3w_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu);

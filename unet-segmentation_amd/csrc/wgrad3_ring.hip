@@ -405,9 +405,12 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
   }
   vm_wait<0>();  // the tail's re-issued DMAs land before the workgroup exits
 
-  // accumulate into out[co][tap * Ci + ci] (fp32 atomics, one per element per workgroup)
+  // accumulate into out[co][tap * Ci + ci]: fp32 atomics, one per element per
+  // workgroup, or (slab mode) this split's partial into its slab plane with
+  // plain stores, summed into out by k_wr_reduce
   const int h = lane >> 5, li = lane & 31;
   const int t0 = tg * 5, nt = SLIDE ? 9 : tg ? 4 : 5;
+  float* const plane = args.slab ? args.slab + (size_t)blockIdx.z * args.Mo * args.No : nullptr;
 #pragma unroll
   for (int i = 0; i < TMC1; ++i)
 #pragma unroll
@@ -417,10 +420,32 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
         for (int r = 0; r < 16; ++r) {
           const int row = i0 + cg * 32 * TMC1 + i * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
           const int col = (t0 + j) * Ci + cb + ct * 32 + li;
-          atomicAdd(args.out + (size_t)row * args.No + col, acc[i][j][r]);
+          if (plane) plane[(size_t)row * args.No + col] = acc[i][j][r];
+          else atomicAdd(args.out + (size_t)row * args.No + col, acc[i][j][r]);
         }
       }
     }
+}
+
+// out[e] += sum over the splits of slab[z][e] (slab-mode weight gradients)
+__global__ __launch_bounds__(256) void k_wr_reduce(const float* __restrict__ slab, int splits, long long n4,
+                                                   float* __restrict__ out) {
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
+    float4 acc = reinterpret_cast<const float4*>(out)[i];
+    for (int z = 0; z < splits; ++z) {
+      const float4 v = reinterpret_cast<const float4*>(slab)[(size_t)z * n4 + i];
+      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    }
+    reinterpret_cast<float4*>(out)[i] = acc;
+  }
+}
+
+hipError_t launch_slab_reduce(const float* slab, int splits, size_t plane, float* out, hipStream_t s) {
+  if (plane % 4 != 0 || splits < 1) return hipErrorInvalidValue;
+  const long long n4 = (long long)(plane / 4);
+  hipLaunchKernelGGL(k_wr_reduce, dim3((unsigned)std::min<long long>((n4 + 255) / 256, 2048)), dim3(256), 0, s,
+                     slab, splits, n4, out);
+  return hipGetLastError();
 }
 
 // wgrad tiles 26-29 (igemm.hip wgrad_tile_fits / launch_wgrad_v):
@@ -447,14 +472,23 @@ bool wgrad3_ring_fits(const WgradArgs& a, int tile) {
 }
 
 template <int TH, int TW, int BCO, int BCI, int TMC>
-static hipError_t go_wr(const WgradArgs& a, hipStream_t s, int per_cu) {
+static hipError_t go_wr(const WgradArgs& a0, hipStream_t s, int per_cu) {
   using Gm = WRGeo<TH, TW, BCO, BCI>;
   static bool attr[2] = {false, false};
-  const Gather& g = a.gb;
+  const Gather& g = a0.gb;
+  // per_cu >= 10: slab mode (per_cu - 10 workgroups per CU), when the plan's
+  // slab holds every split's plane (else the atomics)
+  const bool slab_mode = per_cu >= 10;
+  if (slab_mode) per_cu -= 10;
   const int tiles = g.nimg * ((g.Hg + TH - 1) / TH) * ((g.Wg + TW - 1) / TW);
-  const int blocks = (a.Mo / BCO) * (g.Cg / BCI);
+  const int blocks = (a0.Mo / BCO) * (g.Cg / BCI);
   int splits = (per_cu * num_cus() + blocks - 1) / blocks;
   splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
+  WgradArgs a = a0;
+  const size_t plane = (size_t)a.Mo * a.No;
+  const bool use_slab = slab_mode && a.slab && (size_t)splits * plane * sizeof(float) <= a.slab_bytes &&
+                        splits > 1 && plane % 4 == 0;
+  if (!use_slab) a.slab = nullptr;
   const dim3 grid(a.Mo / BCO, g.Cg / BCI, splits);
   // X transform per launch: the sources of the two concat halves may differ
   // (relu(bn(skip)) vs the plain convT output), so a block picks its kernel by
@@ -473,13 +507,18 @@ static hipError_t go_wr(const WgradArgs& a, hipStream_t s, int per_cu) {
     else hipLaunchKernelGGL((k_wgrad3_ring<TH, TW, BCO, BCI, TMC, 0>), gr, dim3(512), Gm::smem, s, a, cblk0);
     return hipGetLastError();
   };
-  if (!two || t0 == t1) return launch(t0, 0, grid);
-  // concat with one transformed half (relu(bn(skip)) and the plain convT
-  // output): the column blocks of each source as a launch of its own
-  const int nb0 = g.c_split / BCI;
-  const hipError_t e = launch(t0, 0, dim3(a.Mo / BCO, nb0, splits));
-  if (e != hipSuccess) return e;
-  return launch(t1, nb0, dim3(a.Mo / BCO, g.Cg / BCI - nb0, splits));
+  hipError_t e;
+  if (!two || t0 == t1) {
+    e = launch(t0, 0, grid);
+  } else {
+    // concat with one transformed half (relu(bn(skip)) and the plain convT
+    // output): the column blocks of each source as a launch of its own
+    const int nb0 = g.c_split / BCI;
+    e = launch(t0, 0, dim3(a.Mo / BCO, nb0, splits));
+    if (e == hipSuccess) e = launch(t1, nb0, dim3(a.Mo / BCO, g.Cg / BCI - nb0, splits));
+  }
+  if (e != hipSuccess || !a.slab) return e;
+  return launch_slab_reduce(a.slab, splits, plane, a.out, s);
 }
 
 hipError_t go_wgrad3_ring(const WgradArgs& a, hipStream_t s, int tile, int per_cu) {
