@@ -1449,26 +1449,20 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   if (tile == 23) return go_wgrad3_f32<4, 32>(a, s, c.split > 0 ? c.split : 4);
   int bm, bn;
   wgrad_tile(tile, bm, bn);
-  const int tiles = (a.Mo / bm) * (a.No / bn) * a.batch;
   // split the pixel reduction so that the grid has ~`per_cu` workgroups per CU;
   // codes >= 100: slab mode (plain-store split partials + one reduction pass)
   const bool slab_mode = c.tile >= 0 && c.split >= 100;
   if (slab_mode) c.split -= 100;
   const int per_cu = c.tile >= 0 ? (c.split > 0 ? c.split : 8) : (g_tune_wgrad >= 2 ? g_tune_wgrad : 8);
-  const int target = per_cu * num_cus();
-  int splits = (target + tiles - 1) / tiles;
-  int max_splits = (a.P + 255) / 256;
-  if (splits > max_splits) splits = max_splits;
-  if (splits < 1) splits = 1;
-  int pps = (a.P + splits - 1) / splits;
-  const int kq = tile >= 10 ? 32 : 16;  // pixels per K-step
-  pps = (pps + kq - 1) / kq * kq;
-  splits = (a.P + pps - 1) / pps;
+  int pps = 0;
+  const int splits = wgrad_splits(a, tile, per_cu, pps);
   a.pix_per_split = pps;
   const size_t plane = (size_t)a.Mo * a.No;
-  if (!(slab_mode && a.batch == 1 && splits > 1 && plane % 4 == 0 && a.slab &&
-        (size_t)splits * plane * sizeof(float) <= a.slab_bytes))
-    a.slab = nullptr;
+  // slab mode: one split writes its planes straight into out (plain stores),
+  // more go through the slab and an assigning reduction; either way every
+  // output element is written, so out needs no zeroing
+  if (!(slab_mode && wgrad_slab_fits(a, splits))) a.slab = nullptr;
+  else if (splits == 1) a.slab = a.out;
   dim3 grid(a.Mo / bm, a.No / bn, splits * a.batch);
   hipError_t e = hipSuccess;
   if (tile >= 10) {
@@ -1483,8 +1477,29 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     }
     e = hipGetLastError();
   }
-  if (e != hipSuccess || !a.slab) return e;
-  return launch_slab_reduce(a.slab, splits, plane, a.out, s);
+  if (e != hipSuccess || !a.slab || a.slab == a.out) return e;
+  return launch_slab_reduce(a.slab, splits, a.batch, plane, a.batch_out, a.out, s);
+}
+
+int wgrad_splits(const WgradArgs& a, int tile, int per_cu, int& pps) {
+  int bm, bn;
+  wgrad_tile(tile, bm, bn);
+  const int tiles = (a.Mo / bm) * (a.No / bn) * a.batch;
+  const int target = per_cu * num_cus();
+  int splits = (target + tiles - 1) / tiles;
+  const int max_splits = (a.P + 255) / 256;
+  if (splits > max_splits) splits = max_splits;
+  if (splits < 1) splits = 1;
+  pps = (a.P + splits - 1) / splits;
+  const int kq = tile >= 10 ? 32 : 16;  // pixels per K-step
+  pps = (pps + kq - 1) / kq * kq;
+  return (a.P + pps - 1) / pps;
+}
+
+bool wgrad_slab_fits(const WgradArgs& a, int splits) {
+  const size_t plane = (size_t)a.Mo * a.No;
+  if (!a.slab || plane % 4 != 0 || (a.batch > 1 && a.batch_out != (long long)plane)) return false;
+  return splits == 1 || (size_t)splits * a.batch * plane * sizeof(float) <= a.slab_bytes;
 }
 
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad_v(a, s, GemmChoice{}); }

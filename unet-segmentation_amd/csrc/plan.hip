@@ -349,9 +349,13 @@ std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
     if (!wgrad_tile_fits(a, t) || tune_skipped(t)) continue;
     if (t == 71 || t == 74) {  // Winograd: point-GEMM tile (k_wgrad 0-4) x workgroups per CU
       // (each pixel split adds a full points x Co x Ci slab by fp32 atomics:
-      // 1-2 per CU cut that traffic on the deep, few-tile layers)
+      // 1-2 per CU cut that traffic on the deep, few-tile layers); + 1000:
+      // slab mode (plain-store partials, no accumulator memset)
       for (int inner : {0, 1, 2, 3, 4})
         for (int per_cu : {1, 2, 4, 8, 16}) v.push_back({t, per_cu + 100 * (inner + 1)});
+      if (a.slab)
+        for (int inner : {0, 3, 4})
+          for (int per_cu : {1, 2, 4}) v.push_back({t, 1000 + per_cu + 100 * (inner + 1)});
       continue;
     }
     if (t >= 24 && t <= 33) {  // wide halo-tiled / LDS-DMA ring: one resident workgroup per CU

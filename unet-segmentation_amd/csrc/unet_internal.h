@@ -194,8 +194,14 @@ hipError_t go_wgrad3_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_c
 // ring of pixel tiles (wgrad tiles 26-33, wgrad3_ring.hip)
 bool wgrad3_ring_fits(const WgradArgs& a, int tile);
 hipError_t go_wgrad3_ring(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
-// out[e] += sum_z slab[z][e], e < plane (the slab-mode weight gradients' reduction)
-hipError_t launch_slab_reduce(const float* slab, int splits, size_t plane, float* out, hipStream_t s);
+// out[b][e] = sum_z slab[b * splits + z][e], e < plane (the slab-mode weight
+// gradients' reduction; out planes batch_out floats apart)
+hipError_t launch_slab_reduce(const float* slab, int splits, int batch, size_t plane, long long batch_out, float* out,
+                              hipStream_t s);
+// pixel splits of a pixel-column weight-gradient tile (and the pixels per split)
+int wgrad_splits(const WgradArgs& a, int tile, int per_cu, int& pps);
+// whether slab mode can hold `splits` partial planes (1 split: stores into out)
+bool wgrad_slab_fits(const WgradArgs& a, int splits);
 // wide halo-tiled 3x3 weight gradient with a two-stage ring (wgrad tiles 24, 25)
 bool wgrad3w_fits(const WgradArgs& a, int tile);
 hipError_t go_wgrad3w_bf16(const WgradArgs& a, hipStream_t s, int tile, int per_cu);

@@ -427,24 +427,30 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
     }
 }
 
-// out[e] += sum over the splits of slab[z][e] (slab-mode weight gradients)
-__global__ __launch_bounds__(256) void k_wr_reduce(const float* __restrict__ slab, int splits, long long n4,
-                                                   float* __restrict__ out) {
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < n4; i += (long long)gridDim.x * 256) {
-    float4 acc = reinterpret_cast<const float4*>(out)[i];
-    for (int z = 0; z < splits; ++z) {
-      const float4 v = reinterpret_cast<const float4*>(slab)[(size_t)z * n4 + i];
+// out[b][e] = sum over the splits of slab[b * splits + z][e] (slab-mode weight
+// gradients: every element of every plane is written by the splits, so the
+// sum is assigned -- out needs no zeroing)
+__global__ __launch_bounds__(256) void k_wr_reduce(const float* __restrict__ slab, int splits, int batch,
+                                                   long long n4, long long out4, float* __restrict__ out) {
+  const long long total = (long long)batch * n4;
+  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
+    const long long b = i / n4, e = i - b * n4;
+    const float4* src = reinterpret_cast<const float4*>(slab) + (size_t)b * splits * n4 + e;
+    float4 acc = src[0];
+    for (int z = 1; z < splits; ++z) {
+      const float4 v = src[(size_t)z * n4];
       acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
     }
-    reinterpret_cast<float4*>(out)[i] = acc;
+    reinterpret_cast<float4*>(out)[b * out4 + e] = acc;
   }
 }
 
-hipError_t launch_slab_reduce(const float* slab, int splits, size_t plane, float* out, hipStream_t s) {
-  if (plane % 4 != 0 || splits < 1) return hipErrorInvalidValue;
-  const long long n4 = (long long)(plane / 4);
-  hipLaunchKernelGGL(k_wr_reduce, dim3((unsigned)std::min<long long>((n4 + 255) / 256, 2048)), dim3(256), 0, s,
-                     slab, splits, n4, out);
+hipError_t launch_slab_reduce(const float* slab, int splits, int batch, size_t plane, long long batch_out, float* out,
+                              hipStream_t s) {
+  if (plane % 4 != 0 || splits < 1 || batch < 1 || (batch > 1 && batch_out % 4 != 0)) return hipErrorInvalidValue;
+  const long long n4 = (long long)(plane / 4), tot = n4 * batch;
+  hipLaunchKernelGGL(k_wr_reduce, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)), dim3(256), 0, s,
+                     slab, splits, batch, n4, batch > 1 ? batch_out / 4 : n4, out);
   return hipGetLastError();
 }
 
@@ -518,7 +524,7 @@ static hipError_t go_wr(const WgradArgs& a0, hipStream_t s, int per_cu) {
     if (e == hipSuccess) e = launch(t1, nb0, dim3(a.Mo / BCO, g.Cg / BCI - nb0, splits));
   }
   if (e != hipSuccess || !a.slab) return e;
-  return launch_slab_reduce(a.slab, splits, plane, a.out, s);
+  return launch_slab_reduce(a.slab, splits, 1, plane, 0, a.out, s);
 }
 
 hipError_t go_wgrad3_ring(const WgradArgs& a, hipStream_t s, int tile, int per_cu) {

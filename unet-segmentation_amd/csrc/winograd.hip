@@ -2055,6 +2055,9 @@ bool wino_wgrad_applies(const WgradArgs& a, int mt) {
 // GEMMs' pixel split, + 100 * (1 + k_wgrad tile id) to force their tile
 // (autotuner candidates)
 hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int mt) {
+  // code = [1000: slab mode] + [100 * (point-GEMM tile + 1)] + workgroups per CU
+  const bool slab = per_cu >= 1000;
+  per_cu %= 1000;
   const int forced = per_cu >= 100 ? per_cu / 100 - 1 : -1;
   per_cu %= 100;
   if (per_cu <= 0) per_cu = 8;
@@ -2080,9 +2083,8 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
     hipLaunchKernelGGL(k_wino6_dy<2>, dim3((unsigned)((nd / 2 + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg,
                        gb.Wg, Th, Tw, T, Co, Vd);  // Co % 64 == 0 (wino_wgrad_applies)
   }
-  hipError_t e = hipMemsetAsync(Mw, 0, (size_t)P * Co * Ci * 4, s);
+  hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  if ((e = hipGetLastError()) != hipSuccess) return e;
   {
     // the P point GEMMs Mw[p] = Vd[p]^T U[p] as one batched k_wgrad launch
     WgradArgs q;
@@ -2114,7 +2116,14 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
     q.batch_out = (long long)Co * Ci;
     int tile = (Co % 128 == 0 && Ci % 128 == 0) ? 0 : (Ci % 128 == 0 ? 3 : 4);
     if (forced >= 0 && wgrad_tile_fits(q, forced)) tile = forced;
-    if ((e = launch_wgrad_v(q, s, GemmChoice{tile, per_cu})) != hipSuccess) return e;
+    // slab mode (plain-store partials, every Mw element assigned) needs no
+    // zeroed accumulator; the atomics do (0.8 GB of memsets per fp32 step)
+    q.slab = a.slab;
+    q.slab_bytes = a.slab_bytes;
+    int pps = 0;
+    const bool use_slab = slab && wgrad_slab_fits(q, wgrad_splits(q, tile, per_cu, pps));
+    if (!use_slab && (e = hipMemsetAsync(Mw, 0, (size_t)P * Co * Ci * 4, s)) != hipSuccess) return e;
+    if ((e = launch_wgrad_v(q, s, GemmChoice{tile, use_slab ? per_cu + 100 : per_cu})) != hipSuccess) return e;
   }
   const long long no = (long long)Co * Ci;
   if (mt == 4)
