@@ -432,16 +432,35 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
 // sum is assigned -- out needs no zeroing)
 __global__ __launch_bounds__(256) void k_wr_reduce(const float* __restrict__ slab, int splits, int batch,
                                                    long long n4, long long out4, float* __restrict__ out) {
+  // (the planes of a small layer are few float4s but many: 8 independent
+  // loads in flight per thread, not one chained load per split -- a 64 x 576
+  // plane over 256 splits is 36 workgroups of 256-deep load chains otherwise)
   const long long total = (long long)batch * n4;
   for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
     const long long b = i / n4, e = i - b * n4;
     const float4* src = reinterpret_cast<const float4*>(slab) + (size_t)b * splits * n4 + e;
-    float4 acc = src[0];
-    for (int z = 1; z < splits; ++z) {
-      const float4 v = src[(size_t)z * n4];
-      acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+    float4 acc[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+    int z = 0;
+    for (; z + 8 <= splits; z += 8) {
+      float4 v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(z + u) * n4];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+      }
     }
-    reinterpret_cast<float4*>(out)[b * out4 + e] = acc;
+    for (; z < splits; ++z) {
+      const float4 v = src[(size_t)z * n4];
+      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    }
+#pragma unroll
+    for (int u = 1; u < 8; ++u) {
+      acc[0].x += acc[u].x; acc[0].y += acc[u].y; acc[0].z += acc[u].z; acc[0].w += acc[u].w;
+    }
+    reinterpret_cast<float4*>(out)[b * out4 + e] = acc[0];
   }
 }
 
