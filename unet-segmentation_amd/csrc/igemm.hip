@@ -1199,9 +1199,14 @@ static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 // A tile applies when the shape divides and the packed B operand is in the
 // tile's precision (fp32 `b` for tiles 1-14, bf16 `bh` for 21-26).
 bool igemm_tile_fits(const IgemmArgs& a, int tile) {
-  // every 3x3 forward conv feeds a BatchNorm (stats); the input gradients do not
-  if (wino_tile_m(tile) > (a.e.stats ? g_wino_max : g_wino_dgrad_max)) return false;
-  if (a.e.stats && wino_tile_m(tile) >= 4 && a.a.Cg < g_wino4_fwd_min_cg && a.a.Cg > g_wino4_fwd_small_cg)
+  // every 3x3 forward conv feeds a BatchNorm (stats); the input gradients do
+  // not.  An eval forward (BN folded into the weights: ReLU epilogue, no
+  // statistics -- no other GEMM of the plan has a ReLU epilogue) is held to the
+  // forward caps too, so eval logits see the same arithmetic as the training
+  // forward's parity checks
+  const bool fwd = a.e.stats != nullptr || a.e.relu;
+  if (wino_tile_m(tile) > (fwd ? g_wino_max : g_wino_dgrad_max)) return false;
+  if (fwd && wino_tile_m(tile) >= 4 && a.a.Cg < g_wino4_fwd_min_cg && a.a.Cg > g_wino4_fwd_small_cg)
     return false;
   const TileInfo t = tile_info(tile);
   const bool prec_ok = is_bf16_tile(tile) ? a.bh != nullptr && (a.bl == nullptr || bf16_tile_splits(tile))
