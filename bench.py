@@ -227,7 +227,7 @@ def run_farm(args, dtype, device, iters=20, warmup=3):
     return {"value": round(1 / med, 3), "unit": "images/s", "ms_per_image": round(med * 1e3, 3),
             "tiles_per_s": round(len(geo) / med, 1), "dtype": dtype,
             "config": {"workload": "overlap-tile inference 1024x1024x1 (configs[3]), 512^2 tiles -> 324^2, "
-                                   f"{len(geo)} tiles, batch 8, eval mode, mask output, 1 GPU (replicas: N GPUs = N x)",
+                                   f"{len(geo)} tiles, batch 8, eval mode, mask output, measured on 1 GPU (the farm deals tiles to per-GPU replicas with no exchange; multi-GPU farm throughput is not measured here)",
                        "mask_shape": list(mask.shape)}}
 
 
