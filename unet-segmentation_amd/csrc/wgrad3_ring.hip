@@ -430,37 +430,55 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
 // out[b][e] = sum over the splits of slab[b * splits + z][e] (slab-mode weight
 // gradients: every element of every plane is written by the splits, so the
 // sum is assigned -- out needs no zeroing)
+// The planes of a small layer are few float4s but many (a 64 x 576 plane over
+// 512 splits: 9216 float4s): the 2^ls threads of an element each take every
+// 2^ls-th split with 8 independent loads in flight, then combine through LDS,
+// so such a plane still spreads over hundreds of workgroups instead of 36
+// workgroups of 512-deep load chains.
 __global__ __launch_bounds__(256) void k_wr_reduce(const float* __restrict__ slab, int splits, int batch,
-                                                   long long n4, long long out4, float* __restrict__ out) {
-  // (the planes of a small layer are few float4s but many: 8 independent
-  // loads in flight per thread, not one chained load per split -- a 64 x 576
-  // plane over 256 splits is 36 workgroups of 256-deep load chains otherwise)
+                                                   long long n4, long long out4, int ls, float* __restrict__ out) {
+  __shared__ float4 red[256];
+  const int E = 256 >> ls, el = threadIdx.x & (E - 1), sl = threadIdx.x >> (8 - ls), S = 1 << ls;
   const long long total = (long long)batch * n4;
-  for (long long i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (long long)gridDim.x * 256) {
-    const long long b = i / n4, e = i - b * n4;
-    const float4* src = reinterpret_cast<const float4*>(slab) + (size_t)b * splits * n4 + e;
+  for (long long i0 = (long long)blockIdx.x * E; i0 < total; i0 += (long long)gridDim.x * E) {
+    const long long i = i0 + el;
     float4 acc[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) acc[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-    int z = 0;
-    for (; z + 8 <= splits; z += 8) {
-      float4 v[8];
+    if (i < total) {
+      const long long b = i / n4, e = i - b * n4;
+      const float4* src = reinterpret_cast<const float4*>(slab) + (size_t)b * splits * n4 + e;
+      int z = sl;
+      for (; z + 7 * S < splits; z += 8 * S) {
+        float4 v[8];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(z + u) * n4];
+        for (int u = 0; u < 8; ++u) v[u] = src[(size_t)(z + u * S) * n4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+        for (int u = 0; u < 8; ++u) {
+          acc[u].x += v[u].x; acc[u].y += v[u].y; acc[u].z += v[u].z; acc[u].w += v[u].w;
+        }
+      }
+      for (; z < splits; z += S) {
+        const float4 v = src[(size_t)z * n4];
+        acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+      }
+#pragma unroll
+      for (int u = 1; u < 8; ++u) {
+        acc[0].x += acc[u].x; acc[0].y += acc[u].y; acc[0].z += acc[u].z; acc[0].w += acc[u].w;
       }
     }
-    for (; z < splits; ++z) {
-      const float4 v = src[(size_t)z * n4];
-      acc[0].x += v.x; acc[0].y += v.y; acc[0].z += v.z; acc[0].w += v.w;
+    red[threadIdx.x] = acc[0];
+    __syncthreads();
+    if (sl == 0 && i < total) {
+      float4 t = red[el];
+      for (int q = 1; q < S; ++q) {
+        const float4 v = red[q * E + el];
+        t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+      }
+      const long long b = i / n4, e = i - b * n4;
+      reinterpret_cast<float4*>(out)[b * out4 + e] = t;
     }
-#pragma unroll
-    for (int u = 1; u < 8; ++u) {
-      acc[0].x += acc[u].x; acc[0].y += acc[u].y; acc[0].z += acc[u].z; acc[0].w += acc[u].w;
-    }
-    reinterpret_cast<float4*>(out)[b * out4 + e] = acc[0];
+    __syncthreads();
   }
 }
 
@@ -468,8 +486,13 @@ hipError_t launch_slab_reduce(const float* slab, int splits, int batch, size_t p
                               hipStream_t s) {
   if (plane % 4 != 0 || splits < 1 || batch < 1 || (batch > 1 && batch_out % 4 != 0)) return hipErrorInvalidValue;
   const long long n4 = (long long)(plane / 4), tot = n4 * batch;
-  hipLaunchKernelGGL(k_wr_reduce, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)), dim3(256), 0, s,
-                     slab, splits, batch, n4, batch > 1 ? batch_out / 4 : n4, out);
+  // split slices per element: enough threads for ~2 workgroups of 256 per CU,
+  // at least 8 splits per thread, at most 16 slices
+  int ls = 0;
+  while (ls < 4 && (tot << ls) < 2ll * 256 * num_cus() && (splits >> (ls + 1)) >= 8) ++ls;
+  const long long E = 256 >> ls;
+  hipLaunchKernelGGL(k_wr_reduce, dim3((unsigned)std::min<long long>((tot + E - 1) / E, 8192)), dim3(256), 0, s,
+                     slab, splits, batch, n4, batch > 1 ? batch_out / 4 : n4, ls, out);
   return hipGetLastError();
 }
 
