@@ -53,10 +53,12 @@ typedef struct unet_plan unet_plan;
 
 /* Create a plan; returns NULL (and sets unet_last_error) for sizes the valid
  * U-Net cannot take (models/unet_model.py:189: out = in - 184 for clean sizes)
- * and for c_in outside 1..16 or n_classes outside 1..32 (the reference's
+ * and for c_in or n_classes outside 1..4096 (the reference's
  * UNet(n_channels, n_classes), models/unet_model.py:66-85, takes any counts;
- * the first conv's direct kernel and the register-blocked head / loss bound
- * them here).  unet_plan_create() is unet_plan_create_ex(..., UNET_PREC_FP32). */
+ * the bound only keeps the per-plan buffers in reason: the first conv stages
+ * its input channels in chunks of 16, the head / loss run register-blocked up
+ * to 32 classes and with a run-time class loop above).
+ * unet_plan_create() is unet_plan_create_ex(..., UNET_PREC_FP32). */
 unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes);
 
 /* Arithmetic of the implicit-GEMM convolutions (the 17 3x3 convs after the
@@ -74,7 +76,7 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes);
  *                  fp32 accumulation; the dropped lo*lo' is <= 2^-16 of the
  *                  product).  Storage as in UNET_PREC_FP32; tested against the
  *                  fp64 oracle at the fp32 tolerances.
- * Everything else -- the first conv (Ci <= 16), the 1x1 head, BatchNorm, the
+ * Everything else -- the first conv (any Ci), the 1x1 head, BatchNorm, the
  * loss, gradients and the optimizer -- is fp32 in all three; UNET_PREC_BF16
  * plans also store the GEMM-only tensors and the raw conv outputs in bf16. */
 enum { UNET_PREC_FP32 = 0, UNET_PREC_BF16 = 1, UNET_PREC_BF16X3 = 2 };
@@ -380,6 +382,40 @@ int unet_bn_train_bwd(const float* x, const float* dy, int n, int h, int w, int 
                       const float* gamma, const float* save_mean, const float* save_invstd,
                       float* dx, float* dgamma, float* dbeta, void* ws, unet_stream_t stream);
 size_t unet_bn_ws_bytes(int c);
+
+/* Building blocks of the reference submodules' own forwards (DoubleConv / Down
+ * / Up / OutConv.forward, models/unet_model.py:20-21, 32-33, 50-54, 62-63) and
+ * of the op-by-op network path the drop-in takes for a backward through an
+ * eval-mode forward.  NHWC tensors unless marked NCHW. */
+/* nn.BatchNorm2d (+ the following nn.ReLU when relu != 0): training = batch
+ * statistics over (N,H,W), running_mean / running_var updated with `momentum`
+ * (unbiased variance), *nbt += 1 (nbt may be NULL); eval = the running
+ * statistics.  save_mean / save_invstd receive the statistics used.  c a
+ * multiple of 4 dividing 1024. */
+size_t unet_bn_relu_ws_bytes(int n, int h, int w, int c);
+int unet_bn_relu_fwd(const float* x, int n, int h, int w, int c, const float* gamma, const float* beta,
+                     float* running_mean, float* running_var, int64_t* nbt, float momentum, float eps,
+                     int training, int relu, float* y, float* save_mean, float* save_invstd, void* ws,
+                     unet_stream_t stream);
+/* Its backward: y = the forward's output (the ReLU mask), dx, dgamma, dbeta;
+ * eval mode treats the statistics as constants (dx = gamma * invstd * dz). */
+int unet_bn_relu_bwd(const float* x, const float* y, const float* dy, int n, int h, int w, int c,
+                     const float* gamma, const float* save_mean, const float* save_invstd, int training,
+                     int relu, float* dx, float* dgamma, float* dbeta, void* ws, unet_stream_t stream);
+/* The first conv (any Ci -> 64, 3x3 valid, + bias) from an NCHW input; y NHWC.
+ * Backward: dW (OIHW), db, and dx (NCHW; NULL = not needed). */
+size_t unet_conv_first_ws_bytes(int n, int ci, int h, int w);
+int unet_conv_first_fwd(const float* x_nchw, int n, int ci, int h, int w, const float* wt, const float* bias,
+                        float* y, unet_stream_t stream);
+int unet_conv_first_bwd(const float* x_nchw, const float* dy, int n, int ci, int h, int w, const float* wt,
+                        float* dx_nchw, float* dw, float* db, void* ws, unet_stream_t stream);
+/* OutConv's 1x1 conv (64 -> k channels, + bias): logits NCHW; backward dx
+ * (NHWC, NULL = not needed), dW (k, 64), db. */
+size_t unet_conv1x1_ws_bytes(int k);
+int unet_conv1x1_fwd(const float* x, int n, int h, int w, int c, const float* wt, const float* bias, int k,
+                     float* logits_nchw, unet_stream_t stream);
+int unet_conv1x1_bwd(const float* x, const float* dlogits_nchw, int n, int h, int w, int c, const float* wt, int k,
+                     float* dx, float* dw, float* db, void* ws, unet_stream_t stream);
 
 #ifdef __cplusplus
 }

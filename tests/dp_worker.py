@@ -7,7 +7,9 @@ gloo (RCCL needs one GPU per rank; the all-reduce call pattern is the same).
     python tests/dp_worker.py <out.npz> <overlap 0|1> <steps> [comm fp32|bf16] [precision fp32|bf16]
                               [batch] [size]
     env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT;
-         UNET_DP_TUNE_DB=<path>: replay that GEMM tuning database (the bench's)
+         UNET_DP_TUNE_DB=<path>: replay that GEMM tuning database (the bench's);
+         UNET_DP_BACKEND=nccl: RCCL (one GPU per rank: world 1 on the test box),
+         UNET_DP_FORCE=1: issue the collectives at world 1 too (Trainer force_collectives)
 """
 import os
 import sys
@@ -39,7 +41,12 @@ def main():
     size = int(sys.argv[7]) if len(sys.argv) > 7 else SIZE
     rank, world = int(os.environ["RANK"]), int(os.environ["WORLD_SIZE"])
     torch.cuda.set_device(0)
-    dist.init_process_group("gloo")
+    backend = os.environ.get("UNET_DP_BACKEND", "gloo")
+    if backend == "nccl":
+        dist.init_process_group("nccl", device_id=torch.device("cuda", 0))
+    else:
+        dist.init_process_group("gloo")
+    force = os.environ.get("UNET_DP_FORCE") == "1"
     from unet_amd import UNet, _lib
     from unet_amd.train import Trainer
     db = os.environ.get("UNET_DP_TUNE_DB")
@@ -51,7 +58,7 @@ def main():
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
     m = m.cuda().train()
     tr = Trainer(m, batch, size, size, lr=1e-4, momentum=0.99, process_group=dist.group.WORLD, overlap=overlap,
-                 comm_dtype=comm, precision=precision)
+                 comm_dtype=comm, precision=precision, force_collectives=force)
     tr.defer_join = os.environ.get("UNET_DP_DEFER", "1") != "0"
     x, t, w = (torch.from_numpy(a).cuda() for a in shard(rank, batch, size))
     res = {}
@@ -65,6 +72,8 @@ def main():
         tr.optimizer_step()
     torch.cuda.synchronize()
     res["params"] = tr.flat.flat.cpu().numpy().copy()
+    res["backend"] = np.array(dist.get_backend())
+    res["issued"] = np.array(tr.reducer.issued + tr.reducer_whole.issued)
     res["buffers_before_sync"] = np.concatenate([b.double().cpu().numpy().ravel() for b in m.buffers()])
     tr.sync_buffers()
     res["buffers"] = np.concatenate([b.double().cpu().numpy().ravel() for b in m.buffers()])

@@ -168,17 +168,17 @@ def test_host_sanitizer_selftest():
 
 def test_plan_takes_reference_channel_and_class_counts():
     """UNet(n_channels, n_classes) takes any counts in the reference
-    (models/unet_model.py:66-85); the plan takes 1..16 input channels and 1..32
-    classes (the first conv's direct kernel, the register-blocked head / loss)."""
+    (models/unet_model.py:66-85); the plan bounds both at 4096 only to keep
+    its per-plan buffers in reason."""
     from unet_amd import UNet
     from unet_amd.plan import Plan
     _lib()
-    for c, k in ((5, 5), (16, 32), (3, 9)):
+    for c, k in ((5, 5), (16, 32), (3, 9), (17, 2), (1, 33), (64, 150)):
         p = Plan(1, c, 188, 188, k)
         assert (p.out_h, p.out_w) == (4, 4)
         m = UNet(c, k)
         assert m.outc.conv.weight.shape == (k, 64, 1, 1) and m.inc.double_conv[0].weight.shape[1] == c
-    for c, k in ((17, 2), (1, 33)):
+    for c, k in ((0, 2), (1, 0), (4097, 2), (1, 4097)):
         with pytest.raises(ValueError):
             Plan(1, c, 188, 188, k)
         with pytest.raises(ValueError):

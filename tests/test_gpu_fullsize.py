@@ -32,6 +32,8 @@ pytestmark = pytest.mark.gpu
 torch = pytest.importorskip("torch")
 HERE = os.path.dirname(os.path.abspath(__file__))
 G = os.path.join(HERE, "golden")
+# per-tensor cap of the bf16 sampled-entry rel-L2 against the bf16 oracle
+SAMPLE_CAP = 0.5
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -116,7 +118,7 @@ def check_bf16_vs_reference(z, zb, lg, loss, grads, tag, zf=None):
         lflip = float(np.abs(zf["logits_sample"] - zb["logits_sample"]).max())
         assert lt <= 3 * lflip, (tag, lt, lflip)
     worst = worst_b = 0.0
-    ratios, worst_s = [], (0.0, "")
+    ratios, worst_s, worst_abs = [], (0.0, ""), (0.0, "")
     for name, g in grads.items():
         r = float(z[f"gnorm/{name}"])
         if O.bn_cancelled(name):
@@ -149,22 +151,26 @@ def check_bf16_vs_reference(z, zb, lg, loss, grads, tag, zf=None):
             # coefficients and with them every entry of the channel coherently,
             # so single entries carry 10-80 % (median 27 %) rel-L2 of that noise
             # (zf vs zb); the GPU's sample is one more draw of it: within 3 x the
-            # tensor's own noise (at least 5 %), and never above 1.2 -- a
-            # sign-flipped (~2) or permuted / uncorrelated (~1.4) slice fails
+            # tensor's own noise (at least 5 %), and never above 0.5 (VERDICT
+            # r04: the earlier cap of 1.2 sat close to an uncorrelated slice's
+            # ~1.4; a sign-flipped slice reads ~2)
             idx = z[f"gidx/{name}"]
             vb, vf = zb[f"gbf16val/{name}"], zf[f"gbf16val/{name}"]
             nb = max(np.linalg.norm(vb), 1e-30)
             es, fs = np.linalg.norm(g.ravel()[idx] - vb) / nb, np.linalg.norm(vf - vb) / nb
+            bar = min(SAMPLE_CAP, max(3 * fs, 0.05))
             ratios.append(es / max(fs, 0.05))
-            if es / min(1.2, max(3 * fs, 0.05)) > worst_s[0]:
-                worst_s = (es / min(1.2, max(3 * fs, 0.05)), name)
-            assert es <= min(1.2, max(3 * fs, 0.05)), (tag, name, es, fs)
+            if es / bar > worst_s[0]:
+                worst_s = (es / bar, name)
+            worst_abs = max(worst_abs, (es, name))
+            assert es <= bar, (tag, name, es, fs)
     if ratios:
         # statistically the GPU is one more draw of the oracle's own boundary
         # noise: its typical sample error sits at ~1x that noise, not above 2x
         assert float(np.median(ratios)) <= 2.0, (tag, float(np.median(ratios)))
         print(f"{tag}: sampled gradient entries vs bf16 oracle: median err / own noise {np.median(ratios):.2f}, "
-              f"worst err / bar {worst_s[0]:.2f} ({worst_s[1]})")
+              f"worst err / bar {worst_s[0]:.2f} ({worst_s[1]}), largest sampled rel-L2 {worst_abs[0]:.3f} "
+              f"({worst_abs[1]}; cap {SAMPLE_CAP})")
     print(f"{tag}: loss rel {lo:.2e} (bf16 oracle {abs(bf_loss - ref_loss) / abs(ref_loss):.2e}), "
           f"mask agreement {agree:.5f} (bf16 oracle {bf_agree:.5f}; vs bf16 oracle {agree_bf:.5f}), "
           f"logits vs bf16 oracle max {lt:.3f}, worst grad-norm err / tol {worst:.2f} (vs bf16 oracle {worst_b:.2f})")
@@ -223,14 +229,17 @@ def _torch_reference(params, x, tgt, wmap, dtype):
     return lg.detach().double().numpy(), float(loss.item()), grads
 
 
-def test_fp32_512_every_logit_and_gradient_vs_reference_fp64():
-    """configs[1]'s image size, batch 2, fp32 (autotuned mix): ALL 2 x 2 x 324^2
-    logits and ALL 31 M gradient entries against the reference's arithmetic in
-    fp64.  The fp64 run is the torch-CPU restatement, checked first against the
-    reference-made digests of the same step (train_n2_512.npz: logit sample,
-    loss, gradient norms and sampled entries to 1e-9 relative); its fp32 twin
-    gives each tensor's fp32 floor."""
-    z = np.load(os.path.join(G, "train_n2_512.npz"), allow_pickle=False)
+@pytest.mark.parametrize("fixture,path", [("train_n2_512", "dropin"), ("train_n8_512", "trainer")])
+def test_fp32_512_every_logit_and_gradient_vs_reference_fp64(fixture, path):
+    """configs[1]'s image size, fp32: ALL logits and ALL 31 M gradient entries
+    against the reference's arithmetic in fp64 -- at batch 2 through the
+    autograd drop-in, and at the bench's own batch 8 through the bench's
+    Trainer with its tuned batch-8 kernel mix.  The
+    fp64 run is the torch-CPU restatement, checked first against the
+    reference-made digests of the same step (train_n{2,8}_512.npz: logit
+    sample, loss, gradient norms and sampled entries to 1e-9 relative); its
+    fp32 twin gives each tensor's fp32 floor."""
+    z = np.load(os.path.join(G, f"{fixture}.npz"), allow_pickle=False)
     seed, n, h = int(z["x_seed"]), int(z["n"]), int(z["h"])
     params = O.hash_init(1, 2, seed=seed, bn_random=True)
     x, tgt, wmap = F.make_inputs(seed, n, 1, h)
@@ -247,23 +256,27 @@ def test_fp32_512_every_logit_and_gradient_vs_reference_fp64():
         np.testing.assert_allclose(g[z[f"gidx/{name}"]], z[f"gval/{name}"], rtol=1e-8, atol=1e-14 * ref, err_msg=name)
     _, _, r32 = _torch_reference(params, x, tgt, wmap, torch.float32)
 
-    from unet_amd import WeightedCrossEntropyLoss
-    m = make_model(params)
-    m.train()
-    logits = m(torch.from_numpy(x).cuda())
-    loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
-    loss.backward()
-    lg = logits.detach().double().cpu().numpy()
+    if path == "trainer":
+        lg, lossv, grads, _ = trainer_step(params, x, tgt, wmap, "fp32")
+    else:
+        from unet_amd import WeightedCrossEntropyLoss
+        m = make_model(params)
+        m.train()
+        logits = m(torch.from_numpy(x).cuda())
+        loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+        loss.backward()
+        lg, lossv = logits.detach().double().cpu().numpy(), loss.item()
+        grads = {k: p.grad.double().cpu().numpy() for k, p in m.named_parameters()}
     assert lg.shape == rl.shape
     lerr = np.abs(lg - rl).max()
     assert lerr <= 1e-3, lerr
-    assert abs(loss.item() - rloss) <= 1e-4 * abs(rloss)
+    assert abs(lossv - rloss) <= 1e-4 * abs(rloss)
     sure = np.abs(rl[:, 1] - rl[:, 0]) > 1e-3
     np.testing.assert_array_equal((lg[:, 1] > lg[:, 0])[sure], (rl[:, 1] > rl[:, 0])[sure])
     worst, worst_name = 0.0, ""
-    for name, p in m.named_parameters():
-        g = p.grad.double().cpu().numpy()
+    for name, g in grads.items():
         r = rg[name]
+        g = g.reshape(r.shape)
         if O.bn_cancelled(name):
             assert np.abs(g).max() <= 1e-3 * np.abs(rg[name.replace(".bias", ".weight")]).max(), name
             continue
@@ -274,5 +287,5 @@ def test_fp32_512_every_logit_and_gradient_vs_reference_fp64():
         if e / tol > worst:
             worst, worst_name = e / tol, name
         assert e <= tol, (name, e, floor)
-    print(f"512^2 batch 2, every element: logits max |err| {lerr:.2e}, {int((~sure).sum())} low-margin pixels, "
-          f"worst gradient rel-L2 / tol {worst:.2f} ({worst_name})")
+    print(f"512^2 batch {n} ({path}), every element: logits max |err| {lerr:.2e}, {int((~sure).sum())} low-margin "
+          f"pixels, worst gradient rel-L2 / tol {worst:.2f} ({worst_name})")

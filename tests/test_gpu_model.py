@@ -445,13 +445,16 @@ def test_side_stream_weight_grads_match_serial():
         assert np.abs(got[name] - g).max() <= 1e-5 * scale + 1e-12, name
 
 
-@pytest.mark.parametrize("c,k", [(2, 3), (4, 4), (3, 2), (5, 5), (1, 9), (16, 2), (1, 17), (3, 32)])
+@pytest.mark.parametrize("c,k", [(2, 3), (4, 4), (3, 2), (5, 5), (1, 9), (16, 2), (1, 17), (3, 32), (20, 2),
+                                 (1, 33), (17, 70)])
 def test_channel_and_class_counts_vs_oracle(c, k, bench_tuning):
-    """n_channels 2-5 and 16 (the first conv's direct kernel, runtime-Ci form
-    above 4; forward and weight gradient in passes of 4 channels) and n_classes
-    3-9, 17 and 32 (head, weighted CE over K classes; above 16 classes the head
-    forward runs in passes of 16, the plan's limits are 16 channels / 32
-    classes) -- the reference's constructor arguments
+    """n_channels 2-5, 16, 17 and 20 (the first conv's direct kernel, runtime-Ci
+    form above 4 staged in chunks of 16 channels; weight gradient in passes of 4
+    channels) and n_classes 3-9, 17, 32, 33 and 70 (head, weighted CE over K
+    classes; above 16 classes the head forward runs in passes of 16, above 32
+    the head backward's input gradient and the loss loop over the classes at
+    run time and its weight gradient runs in slices of 32) -- the reference's
+    constructor arguments
     (models/unet_model.py:66-85) beyond the 1 -> 2 of scripts/train.py -- with
     the autotuned GEMM mix (the committed tuning database where it has the
     shape).  At 2 x 188 some gradients are sensitive at the 1 % level to ~1e-6
@@ -784,3 +787,43 @@ def test_trainer_hipgraph_replay_matches_eager():
         upd = np.abs(b - s0.cpu().numpy()).max()
         assert np.abs(a - b).max() <= 1e-4 * upd + 1e-7 * np.abs(b).max()
     assert ng == ne == [int(b.item()) + 1 for b in nbt0]
+
+
+@pytest.mark.parametrize("precision,concurrent", [("fp32", 1), ("bf16", 0)])
+def test_trainer_hipgraph_replay_label_flag(precision, concurrent):
+    """The loss kernel's out-of-range-label flag through hipGraph replays
+    (a replayed bf16 step with valid targets raised
+    "Target 0 is out of bounds").  Valid targets: many replays, each step's
+    check before the replay and check_targets() at the end stay silent.  An
+    out-of-range label written into the same (captured) target tensor: the
+    next replay raises IndexError carrying that label; valid again: silent."""
+    from unet_amd import UNet, _lib
+    from unet_amd.train import Trainer
+    lib = _lib.load()
+    lib.unet_set_tuning(b"concurrent", concurrent)
+    try:
+        params = O.hash_init(1, 2, seed=78, bn_random=True)
+        x, t, w = (torch.from_numpy(a).cuda() for a in F.make_inputs(78, 2, 1, 188))
+        m = UNet(1, 2)
+        m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+        m = m.cuda().train()
+        tr = Trainer(m, 2, 188, 188, lr=1e-4, momentum=0.99, precision=precision, graph=True)
+        for _ in range(2):
+            tr.step(x, t, w)
+        assert tr._graph is not None, tr.graph_error
+        for _ in range(24):
+            tr.step(x, t, w)          # replay; checks the earlier steps' flags first
+        tr.check_targets()
+        keep = int(t[1, 5, 7])
+        t[1, 5, 7] = 7                # out of range for K = 2, in the captured tensor
+        tr.step(x, t, w)
+        with pytest.raises(IndexError, match="Target 7 is out of bounds"):
+            tr.check_targets()
+        t[1, 5, 7] = keep
+        for _ in range(4):
+            tr.step(x, t, w)
+        tr.check_targets()
+        assert np.isfinite(float(tr.loss))
+        print(f"{precision} concurrent={concurrent}: label-flag slots read before landing: {tr.labels.premature}")
+    finally:
+        lib.unet_set_tuning(b"concurrent", 1)

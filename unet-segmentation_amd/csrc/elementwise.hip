@@ -242,9 +242,10 @@ __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ 
 }
 
 // n_channels > 4 (models/unet_model.py:66 takes any count): the same direct
-// conv with the input-channel count at run time (<= kFirstMaxCi), the 64 x Ci
-// x 9 weights in LDS instead of registers.  Not on the benchmarked path.
-constexpr int kFirstMaxCi = 16;
+// conv with the input-channel count at run time, staged through LDS in chunks
+// of kFirstChunk channels (tile + 64 x chunk x 9 weights), the 16 pixel
+// accumulators of a thread carried across chunks.  Not on the benchmarked path.
+constexpr int kFirstChunk = 16;
 template <int H16>
 __global__ __launch_bounds__(256) void k_conv_first_fwd_gen(const float* __restrict__ x, int ci_n, int h, int w,
                                                             const float* __restrict__ wt,
@@ -252,42 +253,55 @@ __global__ __launch_bounds__(256) void k_conv_first_fwd_gen(const float* __restr
                                                             double* __restrict__ stats, int relu) {
   const int ho = h - 2, wo = w - 2;
   const int x0 = blockIdx.x * 64, row = blockIdx.y, n = blockIdx.z;
-  __shared__ float tile[kFirstMaxCi][3][66];
-  __shared__ float wl[kFirstMaxCi * 9][64];
+  __shared__ float tile[kFirstChunk][3][66];
+  __shared__ float wl[kFirstChunk * 9][64];
   const int tid = threadIdx.x;
-  for (int i = tid; i < ci_n * 3 * 66; i += 256) {
-    const int ci = i / 198, rem = i - ci * 198, r = rem / 66, cx = rem - r * 66;
-    const int gx = min(x0 + cx, w - 1);
-    tile[ci][r][cx] = x[((size_t)(n * ci_n + ci) * h + row + r) * w + gx];
-  }
-  for (int i = tid; i < ci_n * 9 * 64; i += 256) {
-    const int c = i / (ci_n * 9), k = i - c * (ci_n * 9);
-    wl[k][c] = wt[i];
-  }
   const int c = tid & 63, q = tid >> 6;
+  float acc[16];
   const float b = bias[c];
-  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = b;
+  for (int c0 = 0; c0 < ci_n; c0 += kFirstChunk) {
+    const int cn = min(kFirstChunk, ci_n - c0);
+    __syncthreads();
+    for (int i = tid; i < cn * 3 * 66; i += 256) {
+      const int ci = i / 198, rem = i - ci * 198, r = rem / 66, cx = rem - r * 66;
+      const int gx = min(x0 + cx, w - 1);
+      tile[ci][r][cx] = x[((size_t)(n * ci_n + c0 + ci) * h + row + r) * w + gx];
+    }
+    for (int i = tid; i < cn * 9 * 64; i += 256) {
+      const int cc = i / (cn * 9), k = i - cc * (cn * 9);
+      wl[k][cc] = wt[(size_t)cc * ci_n * 9 + c0 * 9 + k];
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int j = 0; j < 16; ++j) {
+      const int px = q + 4 * j;
+      float a = acc[j];
+      for (int ci = 0; ci < cn; ++ci)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) a = fmaf(tile[ci][ky][px + kx], wl[(ci * 3 + ky) * 3 + kx][c], a);
+      acc[j] = a;
+    }
+  }
   float s1 = 0.f, s2 = 0.f;
+#pragma unroll
   for (int j = 0; j < 16; ++j) {
-    const int px = q + 4 * j;
-    const int gx = x0 + px;
-    float acc = b;
-    for (int ci = 0; ci < ci_n; ++ci)
-#pragma unroll
-      for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-        for (int kx = 0; kx < 3; ++kx) acc = fmaf(tile[ci][ky][px + kx], wl[(ci * 3 + ky) * 3 + kx][c], acc);
-    if (relu) acc = fmaxf(acc, 0.f);  // eval with BatchNorm folded into wt / bias
+    const int gx = x0 + q + 4 * j;
+    float a = acc[j];
+    if (relu) a = fmaxf(a, 0.f);  // eval with BatchNorm folded into wt / bias
     if (gx < wo) {
       const size_t yi = ((size_t)(n * ho + row) * wo + gx) * 64 + c;
       if (H16) {
-        acc = round_bf(acc);
-        reinterpret_cast<uint16_t*>(y)[yi] = bf16_of(acc);
+        a = round_bf(a);
+        reinterpret_cast<uint16_t*>(y)[yi] = bf16_of(a);
       } else {
-        y[yi] = acc;
+        y[yi] = a;
       }
-      s1 += acc;
-      s2 += acc * acc;
+      s1 += a;
+      s2 += a * a;
     }
   }
   if (stats == nullptr) return;
@@ -322,10 +336,56 @@ static void conv_first_go(dim3 grid, int ci, const float* x, int h, int w, const
 hipError_t launch_conv_first_fwd(const float* x, int n, int ci, int h, int w, const float* wt,
                                  const float* bias, int co, float* y, double* stats, hipStream_t s, int out_h16,
                                  int relu) {
-  if (co != 64 || ci < 1 || ci > kFirstMaxCi || h < 3 || w < 3) return hipErrorInvalidValue;
+  if (co != 64 || ci < 1 || h < 3 || w < 3) return hipErrorInvalidValue;
   dim3 grid(cdiv(w - 2, 64), h - 2, n);
   if (out_h16) conv_first_go<1>(grid, ci, x, h, w, wt, bias, y, stats, relu, s);
   else conv_first_go<0>(grid, ci, x, h, w, wt, bias, y, stats, relu, s);
+  return hipGetLastError();
+}
+
+// inc.c0 input gradient (the per-op path, unet_conv_first_bwd; the network
+// never needs it): dx[n][ci][y][x] = sum_{co, ky, kx} dY[n][y-ky][x-kx][co] *
+// W[co][ci][ky][kx] over the valid output positions.  Thread = one input pixel
+// of one channel; 64-channel dY rows read as float4.
+__global__ __launch_bounds__(256) void k_conv_first_dgrad(const float* __restrict__ dy, int n, int ci_n, int h,
+                                                          int w, const float* __restrict__ wt,
+                                                          float* __restrict__ dx) {
+  const int ho = h - 2, wo = w - 2;
+  const long long total = (long long)n * ci_n * h * w;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < total;
+       i += (long long)gridDim.x * blockDim.x) {
+    const int xx = (int)(i % w);
+    long long t = i / w;
+    const int yy = (int)(t % h);
+    t /= h;
+    const int ci = (int)(t % ci_n), nn = (int)(t / ci_n);
+    float acc = 0.f;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int oy = yy - ky;
+      if (oy < 0 || oy >= ho) continue;
+      for (int kx = 0; kx < 3; ++kx) {
+        const int ox = xx - kx;
+        if (ox < 0 || ox >= wo) continue;
+        const float* g = dy + ((size_t)(nn * ho + oy) * wo + ox) * 64;
+        const float* wk = wt + (size_t)ci * 9 + ky * 3 + kx;
+        for (int co = 0; co < 64; co += 4) {
+          const float4 gv = ld4(g + co);
+          acc = fmaf(gv.x, wk[(size_t)(co + 0) * ci_n * 9], acc);
+          acc = fmaf(gv.y, wk[(size_t)(co + 1) * ci_n * 9], acc);
+          acc = fmaf(gv.z, wk[(size_t)(co + 2) * ci_n * 9], acc);
+          acc = fmaf(gv.w, wk[(size_t)(co + 3) * ci_n * 9], acc);
+        }
+      }
+    }
+    dx[i] = acc;
+  }
+}
+
+hipError_t launch_conv_first_dgrad(const float* dy, int n, int ci, int h, int w, const float* wt, float* dx,
+                                   hipStream_t s) {
+  if (ci < 1 || h < 3 || w < 3) return hipErrorInvalidValue;
+  const long long total = (long long)n * ci * h * w;
+  hipLaunchKernelGGL(k_conv_first_dgrad, dim3(grid_cap(total, 256, 8192)), dim3(256), 0, s, dy, n, ci, h, w, wt, dx);
   return hipGetLastError();
 }
 
@@ -388,7 +448,7 @@ static hipError_t first_wgrad_run(int ci, const float* x, int n, int h, int w, c
 
 hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, const Src& dy, int co,
                                    float* dw, float* slabs, hipStream_t s) {
-  if (co != 64 || ci < 1 || ci > kFirstMaxCi) return hipErrorInvalidValue;
+  if (co != 64 || ci < 1) return hipErrorInvalidValue;
   return first_wgrad_run<0, 0>(ci, x, n, h, w, dy, dw, slabs, nullptr, nullptr, s);
 }
 
@@ -397,7 +457,7 @@ hipError_t launch_conv_first_wgrad(const float* x, int n, int ci, int h, int w, 
 hipError_t launch_conv_first_wgrad_bn(const float* x, int n, int ci, int h, int w, const float* dz, const float* y,
                                       int y_h16, const float* coef, int co, float* dw, float* slabs, hipStream_t s,
                                       int dz_h16) {
-  if (co != 64 || ci < 1 || ci > kFirstMaxCi) return hipErrorInvalidValue;
+  if (co != 64 || ci < 1) return hipErrorInvalidValue;
   Src d;
   d.ptr = dz;
   d.H = h - 2;
@@ -474,14 +534,17 @@ __global__ void k_bn_eval_prepare(int C, const float* gamma, const float* beta, 
 //      = k0*dz' + k1*(y - mean) + k2,  k0 = g*is, k1 = -g*is^2*B2/M, k2 = -g*is*B1/M.
 // The conv bias that precedes the BN gets sum_p dY = k0*B1 + k2*M (+ k1*0),
 // which is zero up to rounding (BN-cancelled biases).
+// eval != 0: BatchNorm in eval mode (running statistics are constants): dY =
+// gamma*invstd*dz', k1 = k2 = 0.
 __global__ __launch_bounds__(256) void k_bnb_finalize(const double* __restrict__ st, int C, double M,
                                                       const float* gamma, const float* mean, const float* invstd,
-                                                      float* dgamma, float* dbeta, float* dbias, float* coef) {
+                                                      float* dgamma, float* dbeta, float* dbias, float* coef,
+                                                      int eval) {
   double b1, b2;
   int c;
   if (!group_sum(st, C, b1, b2, c)) return;
   const double gi = (double)gamma[c] * (double)invstd[c];
-  const double k0 = gi, k1 = -gi * (double)invstd[c] * b2 / M, k2 = -gi * b1 / M;
+  const double k0 = gi, k1 = eval ? 0.0 : -gi * (double)invstd[c] * b2 / M, k2 = eval ? 0.0 : -gi * b1 / M;
   if (dgamma) dgamma[c] = (float)b2;
   if (dbeta) dbeta[c] = (float)b1;
   if (dbias) dbias[c] = (float)(k0 * b1 + k2 * M);
@@ -609,9 +672,9 @@ hipError_t launch_bn_eval_prepare(int c, const float* gamma, const float* beta, 
 }
 hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const float* gamma, const float* mean,
                                const float* invstd, float* dgamma, float* dbeta, float* dbias, float* coef,
-                               hipStream_t s) {
+                               hipStream_t s, int eval) {
   hipLaunchKernelGGL(k_bnb_finalize, dim3(cdiv(c, 64)), dim3(256), 0, s, bstats, c, count, gamma, mean, invstd,
-                     dgamma, dbeta, dbias, coef);
+                     dgamma, dbeta, dbias, coef, eval);
   return hipGetLastError();
 }
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h, int w, int c,
@@ -960,19 +1023,25 @@ __global__ __launch_bounds__(256) void k_head_fwd(Src s, int n, int h, int w, co
 }
 
 // head backward: dz = W^T dl masked by ReLU'(bn(y)) (+ BN-bwd stats), dW, db.
-template <int K, int Y16>  // class capacity (kn <= K classes, as k_head_fwd); Y16: y stored bf16
+// Classes koff .. koff + kn - 1 of ktot; DZ = 0 (more than kMaxClasses classes):
+// only this class slice's dW / db, dz comes from k_head_bwd_dz.  TF = 0 (the
+// per-op 1x1 conv, unet_conv1x1_bwd): the input is read as is -- no BN+ReLU
+// transform, no mask, no statistics.
+template <int K, int Y16, int DZ = 1, int TF = 1>  // class capacity (kn <= K, as k_head_fwd); Y16: y stored bf16
 __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict__ dl, int n, int h, int w,
                                                   const float* __restrict__ wt, const float* __restrict__ mean,
                                                   const float* __restrict__ invstd, float* __restrict__ dz,
                                                   double* __restrict__ bstats, double* __restrict__ acc_out,
-                                                  int dz16, int kn) {
+                                                  int dz16, int kn, int koff, int ktot) {
   const int tid = threadIdx.x, sub = tid & 15;
   const int pixels = n * h * w;  // < 2^31 (launch_head_bwd)
   const int c = sub * 4;
   float4 wk[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) wk[k] = k < kn ? ld4(wt + k * 64 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
-  const float4 sc = ld4(s.scale + c), sf = ld4(s.shift + c), mu = ld4(mean + c), is = ld4(invstd + c);
+  for (int k = 0; k < K; ++k) wk[k] = k < kn ? ld4(wt + (koff + k) * 64 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 one = make_float4(1.f, 1.f, 1.f, 1.f), zero = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 sc = TF ? ld4(s.scale + c) : one, sf = TF ? ld4(s.shift + c) : zero;
+  const float4 mu = TF ? ld4(mean + c) : zero, is = TF ? ld4(invstd + c) : one;
   float dwa[K][4], dba[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) {
@@ -1001,7 +1070,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
       yv[u] = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + ii))
                   : ld4(s.ptr + ii);
 #pragma unroll
-      for (int k = 0; k < K; ++k) g[u][k] = dl[((size_t)nn * kn + min(k, kn - 1)) * hw + r];
+      for (int k = 0; k < K; ++k) g[u][k] = dl[((size_t)nn * ktot + koff + min(k, kn - 1)) * hw + r];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -1009,8 +1078,10 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
       if (p >= pixels) continue;
 #pragma unroll
       for (int k = 0; k < K; ++k) g[u][k] = k < kn ? g[u][k] : 0.f;
-      const float zx = fmaf(yv[u].x, sc.x, sf.x), zy = fmaf(yv[u].y, sc.y, sf.y), zz = fmaf(yv[u].z, sc.z, sf.z),
-                  zw = fmaf(yv[u].w, sc.w, sf.w);
+      const float zx = TF ? fmaf(yv[u].x, sc.x, sf.x) : yv[u].x, zy = TF ? fmaf(yv[u].y, sc.y, sf.y) : yv[u].y,
+                  zz = TF ? fmaf(yv[u].z, sc.z, sf.z) : yv[u].z, zw = TF ? fmaf(yv[u].w, sc.w, sf.w) : yv[u].w;
+      const float ax = TF ? fmaxf(zx, 0.f) : zx, ay = TF ? fmaxf(zy, 0.f) : zy, az = TF ? fmaxf(zz, 0.f) : zz,
+                  aw = TF ? fmaxf(zw, 0.f) : zw;
       float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int k = 0; k < K; ++k) {
@@ -1018,11 +1089,16 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
         d.y = fmaf(wk[k].y, g[u][k], d.y);
         d.z = fmaf(wk[k].z, g[u][k], d.z);
         d.w = fmaf(wk[k].w, g[u][k], d.w);
-        dwa[k][0] += g[u][k] * fmaxf(zx, 0.f);
-        dwa[k][1] += g[u][k] * fmaxf(zy, 0.f);
-        dwa[k][2] += g[u][k] * fmaxf(zz, 0.f);
-        dwa[k][3] += g[u][k] * fmaxf(zw, 0.f);
+        dwa[k][0] += g[u][k] * ax;
+        dwa[k][1] += g[u][k] * ay;
+        dwa[k][2] += g[u][k] * az;
+        dwa[k][3] += g[u][k] * aw;
         dba[k] += g[u][k];
+      }
+      if (!DZ) continue;
+      if (!TF) {
+        st4(dz + (size_t)p * 64 + c, d);
+        continue;
       }
       d.x = zx > 0.f ? d.x : 0.f;
       d.y = zy > 0.f ? d.y : 0.f;
@@ -1045,7 +1121,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
         st4(dz + (size_t)p * 64 + c, d);
     }
   }
-  reduce_pairs_to_global(sa, sb, 16, 64, bstats + (size_t)(blockIdx.x % kStatGroups) * 64 * 2);
+  if (DZ && TF) reduce_pairs_to_global(sa, sb, 16, 64, bstats + (size_t)(blockIdx.x % kStatGroups) * 64 * 2);
   __syncthreads();
   __shared__ float red[256][4];
 #pragma unroll
@@ -1060,7 +1136,7 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
 #pragma unroll
         for (int j = 0; j < 4; ++j) t[j] += red[rr][j];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) atomicAdd(acc_out + k * 64 + tid * 4 + j, (double)t[j]);
+      for (int j = 0; j < 4; ++j) atomicAdd(acc_out + (koff + k) * 64 + tid * 4 + j, (double)t[j]);
     }
     __syncthreads();
     red[tid][0] = (sub == 0) ? dba[k] : 0.f;
@@ -1068,10 +1144,71 @@ __global__ __launch_bounds__(256) void k_head_bwd(Src s, const float* __restrict
     if (tid == 0) {
       float t = 0.f;
       for (int rr = 0; rr < 256; rr += 16) t += red[rr][0];
-      atomicAdd(acc_out + kn * 64 + k, (double)t);
+      atomicAdd(acc_out + ktot * 64 + koff + k, (double)t);
     }
     __syncthreads();
   }
+}
+
+// head backward input gradient for more than kMaxClasses classes: the class
+// loop at run time, W rows read through the cache (same arithmetic order as
+// k_head_bwd's d: fmaf over k ascending); ReLU mask, bf16 rounding and the
+// BN-backward statistics as there.
+template <int Y16, int TF = 1>
+__global__ __launch_bounds__(256) void k_head_bwd_dz(Src s, const float* __restrict__ dl, int n, int h, int w,
+                                                     const float* __restrict__ wt, const float* __restrict__ mean,
+                                                     const float* __restrict__ invstd, float* __restrict__ dz,
+                                                     double* __restrict__ bstats, int dz16, int kn) {
+  const int tid = threadIdx.x, sub = tid & 15;
+  const int pixels = n * h * w;
+  const int c = sub * 4;
+  const float4 one = make_float4(1.f, 1.f, 1.f, 1.f), zero = make_float4(0.f, 0.f, 0.f, 0.f);
+  const float4 sc = TF ? ld4(s.scale + c) : one, sf = TF ? ld4(s.shift + c) : zero;
+  const float4 mu = TF ? ld4(mean + c) : zero, is = TF ? ld4(invstd + c) : one;
+  float sa[4] = {0, 0, 0, 0}, sb[4] = {0, 0, 0, 0};
+  const int hw = h * w;
+  for (int p = blockIdx.x * 16 + (tid >> 4); p < pixels; p += gridDim.x * 16) {
+    const int nn = p / hw, r = p - nn * hw;
+    const int y = r / w, x = r - y * w;
+    const size_t ii = ((size_t)(nn * s.H + y + s.oy) * s.W + x + s.ox) * 64 + c;
+    const float4 yv = Y16 ? bf16x4_to_f4(*reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(s.ptr) + ii))
+                          : ld4(s.ptr + ii);
+    float4 d = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int k = 0; k < kn; ++k) {
+      const float g = dl[((size_t)nn * kn + k) * hw + r];
+      const float4 wk = ld4(wt + k * 64 + c);
+      d.x = fmaf(wk.x, g, d.x);
+      d.y = fmaf(wk.y, g, d.y);
+      d.z = fmaf(wk.z, g, d.z);
+      d.w = fmaf(wk.w, g, d.w);
+    }
+    if (!TF) {
+      st4(dz + (size_t)p * 64 + c, d);
+      continue;
+    }
+    const float zx = fmaf(yv.x, sc.x, sf.x), zy = fmaf(yv.y, sc.y, sf.y), zz = fmaf(yv.z, sc.z, sf.z),
+                zw = fmaf(yv.w, sc.w, sf.w);
+    d.x = zx > 0.f ? d.x : 0.f;
+    d.y = zy > 0.f ? d.y : 0.f;
+    d.z = zz > 0.f ? d.z : 0.f;
+    d.w = zw > 0.f ? d.w : 0.f;
+    if (dz16) {
+      d.x = round_bf(d.x);
+      d.y = round_bf(d.y);
+      d.z = round_bf(d.z);
+      d.w = round_bf(d.w);
+    }
+    sa[0] += d.x; sa[1] += d.y; sa[2] += d.z; sa[3] += d.w;
+    sb[0] += d.x * (yv.x - mu.x) * is.x;
+    sb[1] += d.y * (yv.y - mu.y) * is.y;
+    sb[2] += d.z * (yv.z - mu.z) * is.z;
+    sb[3] += d.w * (yv.w - mu.w) * is.w;
+    if (dz16)
+      reinterpret_cast<uint2*>(dz)[((size_t)p * 64 + c) / 4] = make_uint2(bf16pack(d.x, d.y), bf16pack(d.z, d.w));
+    else
+      st4(dz + (size_t)p * 64 + c, d);
+  }
+  if (TF) reduce_pairs_to_global(sa, sb, 16, 64, bstats + (size_t)(blockIdx.x % kStatGroups) * 64 * 2);
 }
 
 __global__ void k_d2f(const double* __restrict__ a, int n, float* __restrict__ o) {
@@ -1079,14 +1216,16 @@ __global__ void k_d2f(const double* __restrict__ a, int n, float* __restrict__ o
   if (i < n) o[i] = (float)a[i];
 }
 
-// largest class count (models/unet_model.py:66 takes any; the register-blocked
-// head backward and loss hold K values per thread)
+// largest class count of the register-blocked head backward and loss (K values
+// per thread); models/unet_model.py:66 takes any count: above it the head
+// backward runs k_head_bwd_dz + class slices of k_head_bwd<32, *, 0>, the loss
+// k_wce_gen (run-time class loop)
 constexpr int kMaxClasses = 32;
 static int class_capacity(int k) { return k <= 4 ? k : k <= 8 ? 8 : k <= 16 ? 16 : 32; }
 
 hipError_t launch_head_fwd(const Src& s, int n, int h, int w, int c, const float* wt, const float* bias, int k,
                            float* logits, hipStream_t st) {
-  if (c != 64 || k < 1 || k > kMaxClasses) return hipErrorInvalidValue;
+  if (c != 64 || k < 1) return hipErrorInvalidValue;
   const long long pixels = (long long)n * h * w;
   dim3 grid(grid_cap(pixels, 16 * 4, 8192));
   for (int k0 = 0; k0 < k; k0 += 16) {
@@ -1107,7 +1246,7 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
                            const float* yraw, const float* mean, const float* invstd, float* dz, double* bstats,
                            float* dw, float* db, double* acc, hipStream_t st, int dz_h16) {
   (void)yraw;
-  if (c != 64 || k < 1 || k > kMaxClasses) return hipErrorInvalidValue;
+  if (c != 64 || k < 1) return hipErrorInvalidValue;
   const long long pixels = (long long)n * h * w;
   // 512 blocks: the per-block fp64 atomics (BN statistics, dW, db) bound this
   // kernel at larger grids (measured: 256 blocks 199 us, 512 146 us, 2048 236 us)
@@ -1115,14 +1254,34 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
   hipError_t me = hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
   if (me != hipSuccess) return me;
   if (pixels >= (1LL << 31)) return hipErrorInvalidValue;
+  if (k > kMaxClasses) {
+    if (s.h16)
+      hipLaunchKernelGGL((k_head_bwd_dz<1>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats,
+                         dz_h16, k);
+    else
+      hipLaunchKernelGGL((k_head_bwd_dz<0>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats,
+                         dz_h16, k);
+    for (int k0 = 0; k0 < k; k0 += kMaxClasses) {
+      const int kn = k - k0 < kMaxClasses ? k - k0 : kMaxClasses;
+      if (s.h16)
+        hipLaunchKernelGGL((k_head_bwd<kMaxClasses, 1, 0>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd,
+                           dz, bstats, acc, dz_h16, kn, k0, k);
+      else
+        hipLaunchKernelGGL((k_head_bwd<kMaxClasses, 0, 0>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd,
+                           dz, bstats, acc, dz_h16, kn, k0, k);
+    }
+    hipLaunchKernelGGL(k_d2f, dim3(cdiv(k * 64, 256)), dim3(256), 0, st, acc, k * 64, dw);
+    hipLaunchKernelGGL(k_d2f, dim3(cdiv(k, 256)), dim3(256), 0, st, acc + k * 64, k, db);
+    return hipGetLastError();
+  }
 #define HEAD_BWD(KK)                                                                                            \
   do {                                                                                                          \
     if (s.h16)                                                                                                  \
       hipLaunchKernelGGL((k_head_bwd<KK, 1>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, \
-                         acc, dz_h16, k);                                                                       \
+                         acc, dz_h16, k, 0, k);                                                                 \
     else                                                                                                        \
       hipLaunchKernelGGL((k_head_bwd<KK, 0>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, mean, invstd, dz, bstats, \
-                         acc, dz_h16, k);                                                                       \
+                         acc, dz_h16, k, 0, k);                                                                 \
   } while (0)
   switch (class_capacity(k)) {
     case 1: HEAD_BWD(1); break;
@@ -1136,6 +1295,34 @@ hipError_t launch_head_bwd(const Src& s, const float* dl, int n, int h, int w, i
 #undef HEAD_BWD
   hipLaunchKernelGGL(k_d2f, dim3(cdiv(k * 64, 256)), dim3(256), 0, st, acc, k * 64, dw);
   hipLaunchKernelGGL(k_d2f, dim3(1), dim3(64), 0, st, acc + k * 64, k, db);
+  return hipGetLastError();
+}
+
+// 1x1 conv backward on a plain (already activated) fp32 NHWC input, any class
+// count (the per-op unet_conv1x1_bwd): dx = W^T dl, dW, db (acc: k*64 + k doubles)
+hipError_t launch_head_bwd_plain(const float* x, const float* dl, int n, int h, int w, const float* wt, int k,
+                                 float* dx, float* dw, float* db, double* acc, hipStream_t st) {
+  if (k < 1) return hipErrorInvalidValue;
+  const long long pixels = (long long)n * h * w;
+  if (pixels >= (1LL << 31)) return hipErrorInvalidValue;
+  Src s;
+  s.ptr = x;
+  s.H = h;
+  s.W = w;
+  s.C = 64;
+  dim3 grid(grid_cap(pixels, 16 * 8, 512));
+  hipError_t me = hipMemsetAsync(acc, 0, sizeof(double) * (k * 64 + k), st);
+  if (me != hipSuccess) return me;
+  if (dx)
+    hipLaunchKernelGGL((k_head_bwd_dz<0, 0>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, nullptr, nullptr, dx,
+                       nullptr, 0, k);
+  for (int k0 = 0; k0 < k; k0 += kMaxClasses) {
+    const int kn = k - k0 < kMaxClasses ? k - k0 : kMaxClasses;
+    hipLaunchKernelGGL((k_head_bwd<kMaxClasses, 0, 0, 0>), grid, dim3(256), 0, st, s, dl, n, h, w, wt, nullptr,
+                       nullptr, nullptr, nullptr, acc, 0, kn, k0, k);
+  }
+  hipLaunchKernelGGL(k_d2f, dim3(cdiv(k * 64, 256)), dim3(256), 0, st, acc, k * 64, dw);
+  hipLaunchKernelGGL(k_d2f, dim3(cdiv(k, 256)), dim3(256), 0, st, acc + k * 64, k, db);
   return hipGetLastError();
 }
 
@@ -1197,16 +1384,71 @@ __global__ __launch_bounds__(256) void k_wce(const float* __restrict__ lg, const
   if (threadIdx.x == 0) atomicAdd(acc, (double)(red[0] + red[1] + red[2] + red[3]));
 }
 
+// more than kMaxClasses classes: the same arithmetic with the class loop at run
+// time (the logits of a pixel are read twice: max / sum, then the gradient)
+__global__ __launch_bounds__(256) void k_wce_gen(const float* __restrict__ lg, const int64_t* __restrict__ t,
+                                                 const float* __restrict__ wm, int n, int h, int w, int64_t ts0,
+                                                 int64_t ts1, int64_t ts2, int64_t ws0, int64_t ws1, int64_t ws2,
+                                                 float* __restrict__ dl, float gscale, double* __restrict__ acc,
+                                                 int kn) {
+  const long long hw = (long long)h * w, total = (long long)n * hw;
+  const double inv = 1.0 / (double)total;
+  float local = 0.f;
+  for (long long p = blockIdx.x * (long long)blockDim.x + threadIdx.x; p < total;
+       p += (long long)gridDim.x * blockDim.x) {
+    const int nn = (int)(p / hw);
+    const long long r = p - nn * hw;
+    const int yy = (int)(r / w), xx = (int)(r % w);
+    const float* l = lg + (size_t)nn * kn * hw + r;
+    const int64_t tg = t[nn * ts0 + yy * ts1 + xx * ts2];
+    const float wt = wm[nn * ws0 + yy * ws1 + xx * ws2];
+    float mx = l[0];
+    for (int k = 1; k < kn; ++k) mx = fmaxf(mx, l[(size_t)k * hw]);
+    float se = 0.f, lt = 0.f;
+    for (int k = 0; k < kn; ++k) {
+      const float v = l[(size_t)k * hw];
+      se += __expf(v - mx);
+      if (k == tg) lt = v;
+    }
+    const float lse = mx + __logf(se);
+    const bool valid = (tg >= 0 && tg < kn);
+    if (!valid && tg != -100) {
+      acc[1] = 1.0;
+      acc[2] = (double)tg;
+    }
+    if (valid) local += wt * (lse - lt);
+    const float sc = valid ? (float)((double)wt * inv) * gscale : 0.f;
+    const float rs = 1.f / se;
+    for (int k = 0; k < kn; ++k)
+      dl[((size_t)nn * kn + k) * hw + r] = sc * (__expf(l[(size_t)k * hw] - mx) * rs - (k == tg ? 1.f : 0.f));
+  }
+  for (int o = 32; o >= 1; o >>= 1) local += __shfl_xor(local, o);
+  __shared__ float red[4];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = local;
+  __syncthreads();
+  if (threadIdx.x == 0) atomicAdd(acc, (double)(red[0] + red[1] + red[2] + red[3]));
+}
+
 __global__ void k_wce_final(const double* acc, double count, float* loss) { *loss = (float)(acc[0] / count); }
+
+// Clears the sum, the bad-label flag and the bad label.  A kernel rather than a
+// hipMemsetAsync, so that a captured step (Trainer(graph=True)) holds a kernel
+// node ordered on the same queue as k_wce, not a memset node.
+__global__ void k_wce_init(double* acc) {
+  if (threadIdx.x < 3) acc[threadIdx.x] = 0.0;
+}
 
 hipError_t launch_wce(const float* logits, const int64_t* t, const float* wm, int n, int k, int h, int w,
                       const int64_t* ts, const int64_t* wsd, float* loss, float* dlogits, float gscale, double* acc,
                       hipStream_t s) {
-  if (k < 1 || k > kMaxClasses) return hipErrorInvalidValue;
+  if (k < 1) return hipErrorInvalidValue;
   const long long total = (long long)n * h * w;
   dim3 grid(grid_cap(total, 256 * 4, 2048));
-  hipError_t me = hipMemsetAsync(acc, 0, 3 * sizeof(double), s);  // sum, bad-label flag, bad label
-  if (me != hipSuccess) return me;
+  hipLaunchKernelGGL(k_wce_init, dim3(1), dim3(64), 0, s, acc);
+  if (k > kMaxClasses)
+    hipLaunchKernelGGL(k_wce_gen, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1],
+                       wsd[2], dlogits, gscale, acc, k);
+  else
   switch (class_capacity(k)) {
     case 1: hipLaunchKernelGGL(k_wce<1>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;
     case 2: hipLaunchKernelGGL(k_wce<2>, grid, dim3(256), 0, s, logits, t, wm, n, h, w, ts[0], ts[1], ts[2], wsd[0], wsd[1], wsd[2], dlogits, gscale, acc, k); break;

@@ -2,6 +2,7 @@
 // caller buffers, built from the same kernels the network plan schedules.
 // They exist for op-level parity tests and for callers that compose their own
 // graph; the training path uses unet_plan_*.
+#include <algorithm>
 #include <cerrno>
 #include <string>
 
@@ -42,6 +43,27 @@ hipError_t op_b_to_bf16(IgemmArgs& a, size_t n, void* scratch, hipStream_t s) {
   a.bl = bl;
   a.b = nullptr;
   return e;
+}
+}  // namespace
+
+namespace {
+// dz = dy where the (ReLU) output y > 0, else 0 (torch's threshold_backward on
+// the output, nn.ReLU(inplace=True) of models/unet_model.py:13, 17)
+__global__ void k_relu_mask(const float* __restrict__ dy, const float* __restrict__ y, long long n4,
+                            float* __restrict__ dz) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += (long long)gridDim.x * blockDim.x) {
+    const float4 g = reinterpret_cast<const float4*>(dy)[i], v = reinterpret_cast<const float4*>(y)[i];
+    reinterpret_cast<float4*>(dz)[i] =
+        make_float4(v.x > 0.f ? g.x : 0.f, v.y > 0.f ? g.y : 0.f, v.z > 0.f ? g.z : 0.f, v.w > 0.f ? g.w : 0.f);
+  }
+}
+
+// eval-mode BatchNorm statistics: the running ones (invstd as k_bn_eval_prepare)
+__global__ void k_bn_eval_stats(int C, const float* rm, const float* rv, float eps, float* mean, float* invstd) {
+  const int c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= C) return;
+  mean[c] = rm[c];
+  invstd[c] = (float)(1.0 / sqrt((double)rv[c] + (double)eps));
 }
 }  // namespace
 
@@ -353,10 +375,120 @@ int unet_bn_train_bwd(const float* x, const float* dy, int n, int h, int w, int 
   return 0;
 }
 
+size_t unet_bn_relu_ws_bytes(int n, int h, int w, int c) {
+  return unet_bn_ws_bytes(c) + al256(sizeof(float) * (size_t)n * h * w * c);
+}
+
+int unet_bn_relu_fwd(const float* x, int n, int h, int w, int c, const float* gamma, const float* beta, float* rm,
+                     float* rv, int64_t* nbt, float momentum, float eps, int training, int relu, float* y,
+                     float* save_mean, float* save_invstd, void* ws, unet_stream_t st) {
+  if (!x || !y || !gamma || !beta || !save_mean || !save_invstd || c % 4 || 256 % (c / 4) || n < 1) return -EINVAL;
+  if (!training && (!rm || !rv)) return -EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  double* stats = reinterpret_cast<double*>(p);
+  float* scale = reinterpret_cast<float*>(p + al256(sizeof(double) * kStatGroups * 2 * c));
+  float* shift = scale + al256(sizeof(float) * c) / 4;
+  const size_t pix = (size_t)n * h * w;
+  if (training) {
+    OPCK(hipMemsetAsync(stats, 0, sizeof(double) * kStatGroups * 2 * c, s));
+    OPCK(launch_channel_stats(x, pix, c, stats, s));
+    OPCK(launch_bn_finalize(stats, c, (double)pix, gamma, beta, rm, rv, nbt, save_mean, save_invstd, scale, shift,
+                            momentum, eps, s));
+  } else {
+    OPCK(launch_bn_eval_prepare(c, gamma, beta, rm, rv, scale, shift, eps, s));
+    hipLaunchKernelGGL(k_bn_eval_stats, dim3((c + 255) / 256), dim3(256), 0, s, c, rm, rv, eps, save_mean,
+                       save_invstd);
+    OPCK(hipGetLastError());
+  }
+  OPCK(launch_affine_relu(x, pix, c, scale, shift, relu, y, s));
+  return 0;
+}
+
+int unet_bn_relu_bwd(const float* x, const float* y, const float* dy, int n, int h, int w, int c, const float* gamma,
+                     const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
+                     float* dgamma, float* dbeta, void* ws, unet_stream_t st) {
+  if (!x || !dy || !dx || !gamma || c % 4 || 256 % (c / 4) || n < 1 || (relu && !y)) return -EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  double* stats = reinterpret_cast<double*>(p);
+  float* coef = reinterpret_cast<float*>(p + al256(sizeof(double) * kStatGroups * 2 * c));
+  float* dz = reinterpret_cast<float*>(p + unet_bn_ws_bytes(c));
+  const size_t pix = (size_t)n * h * w;
+  const float* g = dy;
+  if (relu) {
+    const long long n4 = (long long)(pix * c / 4);
+    hipLaunchKernelGGL(k_relu_mask, dim3((unsigned)std::min<long long>((n4 + 255) / 256, 8192)), dim3(256), 0, s, dy,
+                       y, n4, dz);
+    OPCK(hipGetLastError());
+    g = dz;
+  }
+  OPCK(hipMemsetAsync(stats, 0, sizeof(double) * kStatGroups * 2 * c, s));
+  OPCK(launch_bn_bwd_stats(g, x, save_mean, save_invstd, pix, c, stats, s));
+  OPCK(launch_bnb_finalize(stats, c, (double)pix, gamma, save_mean, save_invstd, dgamma, dbeta, nullptr, coef, s,
+                           training ? 0 : 1));
+  OPCK(launch_bnb_apply(g, x, coef, n, h, w, c, dx, 0, s));
+  return 0;
+}
+
+size_t unet_conv_first_ws_bytes(int n, int ci, int h, int w) {
+  (void)n; (void)h; (void)w;
+  return conv_first_wgrad_ws_bytes(ci) + al256(sizeof(double) * kStatGroups * 2 * 64);
+}
+
+int unet_conv_first_fwd(const float* x, int n, int ci, int h, int w, const float* wt, const float* bias, float* y,
+                        unet_stream_t st) {
+  if (!x || !wt || !bias || !y || n < 1 || ci < 1 || h < 3 || w < 3) return -EINVAL;
+  OPCK(launch_conv_first_fwd(x, n, ci, h, w, wt, bias, 64, y, nullptr, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_conv_first_bwd(const float* x, const float* dy, int n, int ci, int h, int w, const float* wt, float* dx,
+                        float* dw, float* db, void* ws, unet_stream_t st) {
+  if (!x || !dy || !wt || !dw || !db || !ws || n < 1 || ci < 1 || h < 3 || w < 3) return -EINVAL;
+  hipStream_t s = reinterpret_cast<hipStream_t>(st);
+  char* p = reinterpret_cast<char*>(ws);
+  float* slabs = reinterpret_cast<float*>(p);
+  double* st2 = reinterpret_cast<double*>(p + conv_first_wgrad_ws_bytes(ci));
+  Src d;
+  d.ptr = dy;
+  d.H = h - 2;
+  d.W = w - 2;
+  d.C = 64;
+  OPCK(launch_conv_first_wgrad(x, n, ci, h, w, d, 64, dw, slabs, s));
+  OPCK(hipMemsetAsync(st2, 0, sizeof(double) * kStatGroups * 2 * 64, s));
+  OPCK(launch_channel_stats(dy, (size_t)n * (h - 2) * (w - 2), 64, st2, s));
+  OPCK(launch_pair_sum(st2, kStatGroups, 64, db, s));
+  if (dx) OPCK(launch_conv_first_dgrad(dy, n, ci, h, w, wt, dx, s));
+  return 0;
+}
+
+size_t unet_conv1x1_ws_bytes(int k) { return al256(sizeof(double) * ((size_t)k * 64 + k)); }
+
+int unet_conv1x1_fwd(const float* x, int n, int h, int w, int c, const float* wt, const float* bias, int k,
+                     float* logits, unet_stream_t st) {
+  if (!x || !wt || !bias || !logits || c != 64 || k < 1 || n < 1) return -EINVAL;
+  Src s0;
+  s0.ptr = x;
+  s0.H = h;
+  s0.W = w;
+  s0.C = 64;
+  OPCK(launch_head_fwd(s0, n, h, w, 64, wt, bias, k, logits, reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
+int unet_conv1x1_bwd(const float* x, const float* dl, int n, int h, int w, int c, const float* wt, int k, float* dx,
+                     float* dw, float* db, void* ws, unet_stream_t st) {
+  if (!x || !dl || !wt || !dw || !db || !ws || c != 64 || k < 1 || n < 1) return -EINVAL;
+  OPCK(launch_head_bwd_plain(x, dl, n, h, w, wt, k, dx, dw, db, reinterpret_cast<double*>(ws),
+                             reinterpret_cast<hipStream_t>(st)));
+  return 0;
+}
+
 int unet_wce_fwd_bwd(const float* logits, const int64_t* t, const float* wm, int n, int k, int h, int w,
                      const int64_t* ts, const int64_t* wsd, float* loss, float* dl, float gscale, void* ws,
                      unet_stream_t st) {
-  if (!ts || !wsd || k < 1 || k > 32) return -EINVAL;
+  if (!ts || !wsd || k < 1) return -EINVAL;
   OPCK(launch_wce(logits, t, wm, n, k, h, w, ts, wsd, loss, dl, gscale, reinterpret_cast<double*>(ws),
                   reinterpret_cast<hipStream_t>(st)));
   return 0;

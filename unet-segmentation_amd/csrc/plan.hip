@@ -1036,8 +1036,10 @@ unet_plan* unet_plan_create(int n, int c_in, int h, int w, int n_classes) {
 int unet_plan_precision(const unet_plan* p) { return p ? p->prec : -EINVAL; }
 
 unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int prec) {
-  if (n < 1 || c_in < 1 || c_in > 16 || n_classes < 1 || n_classes > 32) {
-    set_err("unet_plan_create: need n>=1, 1<=c_in<=16, 1<=n_classes<=32");
+  // models/unet_model.py:66 takes any channel / class count; the bounds here
+  // only keep the per-plan buffers (logits, head accumulators) within reason
+  if (n < 1 || c_in < 1 || c_in > kMaxInChannels || n_classes < 1 || n_classes > kMaxClassCount) {
+    set_err("unet_plan_create: need n>=1, 1<=c_in<=4096, 1<=n_classes<=4096");
     return nullptr;
   }
   if (prec != UNET_PREC_FP32 && prec != UNET_PREC_BF16 && prec != UNET_PREC_BF16X3) {
@@ -1144,7 +1146,7 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
   }
   for (int k = 0; k < 4; ++k)  // colsum groups + (tail) expanded bias table
     p->T[k].colsum = al.take(sizeof(double) * kStatGroups * p->T[k].co);
-  p->head_acc = al.take(sizeof(double) * (64 * 32 + 32));  // dW, db of up to 32 classes
+  p->head_acc = al.take(sizeof(double) * (64 * (size_t)n_classes + n_classes));  // head dW, db
   p->wce_acc = al.take(64);
   p->first_slabs = al.take(conv_first_wgrad_ws_bytes(c_in));
   p->stat_region.off = stat_start;

@@ -7,6 +7,10 @@
 
 namespace unet {
 
+// plan-creation bounds on UNet(n_channels, n_classes) (include/unet_hip.h)
+constexpr int kMaxInChannels = 4096;
+constexpr int kMaxClassCount = 4096;
+
 // A tensor in NHWC, addressed as an (H, W, C) grid per image with an (oy, ox)
 // origin: element (n, y, x, c) lives at ((n*H + y+oy)*W + x+ox)*C + c.
 // An optional per-channel affine+ReLU (BatchNorm2d train/eval + nn.ReLU,
@@ -268,7 +272,7 @@ hipError_t launch_bn_eval_prepare(int c, const float* gamma, const float* beta,
 // k[3][C] for dY = k0*dz' + k1*y + k2.
 hipError_t launch_bnb_finalize(const double* bstats, int c, double count, const float* gamma,
                                const float* mean, const float* invstd, float* dgamma,
-                               float* dbeta, float* dbias_conv, float* coef, hipStream_t s);
+                               float* dbeta, float* dbias_conv, float* coef, hipStream_t s, int eval = 0);
 // dYpad interior = coef0*dz + coef1*y + coef2; border (pad each side) = 0.
 hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, int n, int h,
                             int w, int c, float* dypad, int pad, hipStream_t s, int out_h16 = 0,
@@ -291,6 +295,12 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
 // 1x1 head (OutConv, models/unet_model.py:56-63) forward: logits NCHW.
 hipError_t launch_head_fwd(const Src& src, int n, int h, int w, int c, const float* wt,
                            const float* bias, int k, float* logits, hipStream_t s);
+// 1x1 conv backward on a plain fp32 NHWC input (64 channels): dx (nullable), dW, db
+hipError_t launch_head_bwd_plain(const float* x, const float* dl, int n, int h, int w, const float* wt, int k,
+                                 float* dx, float* dw, float* db, double* acc, hipStream_t s);
+// inc.c0 input gradient, dx NCHW (per-op path only)
+hipError_t launch_conv_first_dgrad(const float* dy, int n, int ci, int h, int w, const float* wt, float* dx,
+                                   hipStream_t s);
 // head backward: dz' (masked, + BN-bwd stats), dW (k x c), db (k) (written, not accumulated).
 hipError_t launch_head_bwd(const Src& src, const float* dlogits, int n, int h, int w, int c,
                            const float* wt, int k, const float* yraw, const float* mean,

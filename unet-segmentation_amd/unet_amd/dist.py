@@ -86,10 +86,16 @@ class GradBucketReducer:
     for everything bucket b depends on beyond the current stream (the plan's
     side-stream weight gradients, unet_plan_wait_segment); the collective is
     then issued from that stream, so later work on the current stream (the
-    next backward segment) does not wait for it."""
+    next backward segment) does not wait for it.
 
-    def __init__(self, flat, buckets, group=None, comm_dtype=None, ready=None):
+    ``force=True`` (tests only) issues the collectives at world size 1 too,
+    where they are the identity: the RCCL path (stream-ordered ``Work.wait``,
+    the side-stream issue, the bf16 shadow) then runs on a one-GPU box."""
+
+    def __init__(self, flat, buckets, group=None, comm_dtype=None, ready=None, force=False):
         self.flat = flat
+        self.force = bool(force)
+        self.issued = 0  # collectives issued so far
         self.buckets = list(buckets)
         self.group = group
         self.works = []
@@ -114,7 +120,7 @@ class GradBucketReducer:
         return sum(z - a for a, z in self.buckets) * elem
 
     def reduce(self, b):
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return
         a, z = self.buckets[b]
         if self.ready is None or not self.flat.is_cuda:
@@ -129,6 +135,7 @@ class GradBucketReducer:
             self._issue(a, z)
 
     def _issue(self, a, z):
+        self.issued += 1
         if self.shadow is None:
             self.works.append((dist.all_reduce(self.flat[a:z], group=self.group, async_op=True), a, z))
             return

@@ -87,7 +87,8 @@ class FlatBuffers:
 
 class Trainer:
     def __init__(self, model, batch, height, width, lr=1e-4, momentum=0.99, process_group=None,
-                 overlap=True, precision="fp32", comm_dtype=None, broadcast_buffers=True, graph=False):
+                 overlap=True, precision="fp32", comm_dtype=None, broadcast_buffers=True, graph=False,
+                 force_collectives=False):
         from .modules import UNet
         if not isinstance(model, UNet):
             raise TypeError("Trainer drives the MI355X UNet")
@@ -99,7 +100,9 @@ class Trainer:
         self.flat = FlatParams(model)
         self.flat_buffers = FlatBuffers(model)
         # DDP default: every step starts from rank 0's BatchNorm running statistics
-        self.broadcast_buffers = broadcast_buffers and self.world > 1
+        # force_collectives (tests only): issue the buffer broadcast and the bucket
+        # all-reduces at world size 1 too, where they are the identity
+        self.broadcast_buffers = broadcast_buffers and (self.world > 1 or (force_collectives and self.pg is not None))
         dev = self.flat.flat.device
         self.plan = Plan(batch, model.n_channels, height, width, model.n_classes, precision)
         self.ws = torch.empty(self.plan.workspace_bytes, dtype=torch.uint8, device=dev)
@@ -130,8 +133,9 @@ class Trainer:
         self.comm_dtype = torch.float32 if comm_dtype is None else comm_dtype
         comm_dtype = self.comm_dtype
         self.reducer = GradBucketReducer(self.flat.grad, buckets, process_group, comm_dtype,
-                                         ready=lambda b, st: self.plan.wait_segment(b, st))
-        self.reducer_whole = GradBucketReducer(self.flat.grad, [(0, self.flat.numel)], process_group, comm_dtype)
+                                         ready=lambda b, st: self.plan.wait_segment(b, st), force=force_collectives)
+        self.reducer_whole = GradBucketReducer(self.flat.grad, [(0, self.flat.numel)], process_group, comm_dtype,
+                                               force=force_collectives)
 
     @property
     def out_hw(self):
