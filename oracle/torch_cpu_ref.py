@@ -43,7 +43,10 @@ class TorchCpuUNet:
     in float64 on the same torch CPU kernels); the GPU parity tests use it as the
     full-tensor oracle at 512^2, where a NumPy fp64 run would take minutes."""
 
-    def __init__(self, params, n_channels=1, n_classes=2, dtype=torch.float32):
+    def __init__(self, params, n_channels=1, n_classes=2, dtype=torch.float32, training=True):
+        # training=False: BatchNorm on the running statistics (model.eval(),
+        # scripts/predict.py:70), differentiable like reference autograd's
+        self.training = training
         self.p = {}
         for k, v in params.items():
             t = torch.from_numpy(np.array(v, copy=True))
@@ -60,7 +63,7 @@ class TorchCpuUNet:
             x = F.conv2d(x, self.p[f"{pre}{conv}.weight"], self.p[f"{pre}{conv}.bias"])
             b = f"{pre}{bn}"
             x = F.batch_norm(x, self.p[f"{b}.running_mean"], self.p[f"{b}.running_var"], self.p[f"{b}.weight"],
-                             self.p[f"{b}.bias"], training=True, momentum=0.1, eps=1e-5)
+                             self.p[f"{b}.bias"], training=self.training, momentum=0.1, eps=1e-5)
             x = F.relu(x)
         return x
 

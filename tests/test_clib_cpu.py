@@ -133,8 +133,13 @@ def test_module_has_no_cpu_fallback():
     m = UNet(1, 2)
     with pytest.raises(RuntimeError, match="HIP device"):
         m(torch.zeros(1, 1, 188, 188))
-    with pytest.raises(RuntimeError, match="parameter holder"):
+    # the submodules' own forwards run on the per-op HIP blocks: no CPU path either
+    with pytest.raises(RuntimeError, match="no CPU path"):
         m.inc(torch.zeros(1, 1, 188, 188))
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        m.up1(torch.zeros(1, 1024, 4, 4), torch.zeros(1, 512, 8, 8))
+    with pytest.raises(RuntimeError, match="no CPU path"):
+        m.outc(torch.zeros(1, 64, 4, 4))
     with pytest.raises(RuntimeError):
         WeightedCrossEntropyLoss()(torch.zeros(1, 2, 4, 4), torch.zeros(1, 4, 4, dtype=torch.long),
                                    torch.ones(1, 4, 4))

@@ -1,0 +1,183 @@
+"""The reference submodules' own forwards and the backward through an
+eval-mode forward (VERDICT r04 missing items 3-4), on the per-op HIP blocks
+(unet_amd/blocks.py).
+
+References: the submodules' torch.nn contents run as the reference runs them
+(DoubleConv.forward = its nn.Sequential, models/unet_model.py:20-21; Down =
+MaxPool2d + DoubleConv, :32-33; Up.forward, :50-54; OutConv, :62-63) on CPU in
+float64, from the same weights; the whole network in eval mode against the
+torch-CPU fp64 restatement (oracle/torch_cpu_ref.py, BatchNorm on the running
+statistics).  fp32 GEMMs against fp64: outputs within 1e-4 of their scale,
+gradients within rel-L2 max(1e-3, 2 x the same reference in fp32) per tensor.
+"""
+import copy
+
+import numpy as np
+import pytest
+
+from oracle import unet_oracle as O
+from oracle import fixtures as F
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+def _model(seed, c=1, k=2):
+    from unet_amd import UNet
+    params = O.hash_init(c, k, seed=seed, bn_random=True)
+    m = UNet(c, k)
+    m.load_state_dict({kk: torch.from_numpy(np.asarray(v)) for kk, v in params.items()})
+    return m, params
+
+
+def _rel(a, b):
+    a, b = np.asarray(a, np.float64), np.asarray(b, np.float64)
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-30))
+
+
+def _run(fn, mods, inputs, g):
+    """fn(*inputs) on the given modules; returns output, input grads, param grads."""
+    ins = [t.detach().clone().requires_grad_(True) for t in inputs]
+    for m in mods:
+        m.zero_grad(set_to_none=True)
+    out = fn(*ins)
+    out.backward(g)
+    params = {n: p.grad.detach().double().cpu().numpy() for m in mods for n, p in m.named_parameters()}
+    return (out.detach().double().cpu().numpy(), [i.grad.double().cpu().numpy() for i in ins], params)
+
+
+def _bn_cancelled(name):
+    """Train mode: the biases of a conv / convT whose output feeds a
+    BatchNorm (directly or through the next conv) have analytically zero
+    gradients: compared absolutely."""
+    return name.endswith("up.bias") or name.endswith("double_conv.0.bias") or name.endswith("double_conv.3.bias")
+
+
+def _check(gpu, ref64, ref32, tag, training):
+    (o, gi, gp), (ro, rgi, rgp), (o32, gi32, gp32) = gpu, ref64, ref32
+    scale = np.abs(ro).max()
+    assert np.abs(o - ro).max() <= 1e-4 * scale, (tag, np.abs(o - ro).max(), scale)
+    worst = 0.0
+    pairs = [(f"dx{i}", a, b, c) for i, (a, b, c) in enumerate(zip(gi, rgi, gi32))]
+    for n in rgp:
+        if training and _bn_cancelled(n):
+            wscale = np.abs(rgp[n.replace(".bias", ".weight")]).max()
+            assert np.abs(gp[n]).max() <= 1e-3 * wscale, (tag, n, np.abs(gp[n]).max(), wscale)
+            continue
+        pairs.append((n, gp[n], rgp[n], gp32[n]))
+    for name, a, b, c in pairs:
+        tol = max(1e-3, 2 * _rel(c, b))
+        e = _rel(a, b)
+        worst = max(worst, e / tol)
+        assert e <= tol, (tag, name, e, tol)
+    print(f"{tag}: worst gradient rel-L2 / tol {worst:.2f}")
+
+
+@pytest.mark.parametrize("training", [True, False])
+def test_submodule_forwards_vs_reference_modules(training):
+    """model.inc / down1 / down4 / up1 / up4 / outc called on their own, in train
+    and eval mode: outputs, input gradients, parameter gradients and (train)
+    the BatchNorm running-statistics update against the same nn modules on CPU."""
+    m, _ = _model(81)
+    m.train(training)
+    g = torch.Generator().manual_seed(5)
+
+    def rnd(*shape):
+        return torch.rand(*shape, generator=g, dtype=torch.float64) * 2 - 1
+
+    cases = [
+        ("inc", lambda mm: (lambda x: mm.inc(x)), lambda mm: (lambda x: mm.inc.double_conv(x)), [rnd(2, 1, 36, 36)]),
+        ("down1", lambda mm: (lambda x: mm.down1(x)),
+         lambda mm: (lambda x: mm.down1.maxpool_conv[1].double_conv(mm.down1.maxpool_conv[0](x))),
+         [rnd(2, 64, 27, 26)]),
+        ("down4", lambda mm: (lambda x: mm.down4(x)),
+         lambda mm: (lambda x: mm.down4.maxpool_conv[1].double_conv(mm.down4.maxpool_conv[0](x))),
+         [rnd(2, 512, 14, 14)]),
+        ("up1", lambda mm: (lambda a, b: mm.up1(a, b)),
+         lambda mm: (lambda a, b: mm.up1.conv.double_conv(torch.cat([b, mm.up1.up(a)], 1))),
+         [rnd(2, 1024, 5, 5), rnd(2, 512, 10, 10)]),
+        ("up4", lambda mm: (lambda a, b: mm.up4(a, b)),
+         lambda mm: (lambda a, b: mm.up4.conv.double_conv(torch.cat([b, mm.up4.up(a)], 1))),
+         [rnd(2, 128, 9, 9), rnd(2, 64, 18, 18)]),
+        ("outc", lambda mm: (lambda x: mm.outc(x)), lambda mm: (lambda x: mm.outc.conv(x)), [rnd(2, 64, 7, 9)]),
+    ]
+    for name, ours, ref, inputs in cases:
+        sub = getattr(m, name)
+        cpu64 = copy.deepcopy(sub).double()
+        cpu32 = copy.deepcopy(sub).float()
+        gpu = copy.deepcopy(sub).cuda()
+        holder = lambda s: type("H", (), {name: s})()  # noqa: E731
+        out_shape = ref(holder(copy.deepcopy(cpu64)))(*inputs).shape
+        gout = rnd(*out_shape)
+        r64 = _run(ref(holder(cpu64)), [cpu64], inputs, gout)
+        r32 = _run(ref(holder(cpu32)), [cpu32], [t.float() for t in inputs], gout.float())
+        res = _run(ours(holder(gpu)), [gpu], [t.float().cuda() for t in inputs], gout.float().cuda())
+        _check(res, r64, r32, f"{name} ({'train' if training else 'eval'})", training)
+        if training:  # running statistics updated as nn.BatchNorm2d does
+            for (n, b), (_, rb) in zip(gpu.named_buffers(), cpu64.named_buffers()):
+                np.testing.assert_allclose(b.double().cpu().numpy(), rb.numpy(), rtol=1e-4, atol=1e-6,
+                                           err_msg=f"{name}.{n}")
+
+
+def test_eval_mode_backward_vs_reference():
+    """loss.backward() through model.eval() outputs (reference autograd allows
+    it, e.g. fine-tuning with frozen BatchNorm statistics): the plan's eval
+    forward, then the op-by-op recompute's gradients -- logits, loss, every
+    parameter gradient and the input gradient against the reference arithmetic
+    in fp64 with BatchNorm on its running statistics."""
+    from oracle import torch_cpu_ref as R
+    from unet_amd import WeightedCrossEntropyLoss
+    m, params = _model(82)
+    m = m.cuda().eval()
+    x, tgt, wmap = F.make_inputs(82, 2, 1, 188)
+    xd = torch.from_numpy(x).cuda().requires_grad_(True)
+    logits = m(xd)
+    loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+    loss.backward()
+    refs = {}
+    for dt in (torch.float64, torch.float32):
+        net = R.TorchCpuUNet(params, dtype=dt, training=False)
+        xr = torch.from_numpy(x).to(dt).requires_grad_(True)
+        lr = net.forward(xr)
+        lo = R.weighted_ce(lr, torch.from_numpy(tgt), torch.from_numpy(wmap).to(dt))
+        lo.backward()
+        refs[dt] = (lr.detach().double().numpy(), float(lo), xr.grad.double().numpy(),
+                    {k: v.grad.double().numpy() for k, v in net.p.items() if v.requires_grad})
+    rl, rloss, rdx, rg = refs[torch.float64]
+    _, _, dx32, g32 = refs[torch.float32]
+    assert np.abs(logits.detach().double().cpu().numpy() - rl).max() <= 1e-3
+    assert abs(loss.item() - rloss) <= 1e-4 * abs(rloss)
+    worst = 0.0
+    got = {k: p.grad.double().cpu().numpy() for k, p in m.named_parameters()}
+    got["input"], rg["input"], g32["input"] = xd.grad.double().cpu().numpy(), rdx, dx32
+    for k, r in rg.items():
+        tol = max(1e-3, 2 * _rel(g32[k], r))
+        e = _rel(got[k], r)
+        worst = max(worst, e / tol)
+        assert e <= tol, (k, e, tol)
+    print(f"eval-mode backward: worst gradient rel-L2 / tol {worst:.2f}")
+
+
+def test_ops_path_train_step_matches_plan():
+    """UNet.forward(x, _ops=True) -- the reference forward op by op on the
+    blocks -- against the one-plan forward in train mode: logits and, after the
+    weighted CE, every gradient (both fp32; the plan's autotuned GEMMs and the
+    blocks' direct GEMMs round differently, so the gradients agree to the fp32
+    noise of small-sample BatchNorm: rel-L2 <= 1e-2)."""
+    from unet_amd import WeightedCrossEntropyLoss
+    m, _ = _model(83)
+    m = m.cuda().train()
+    x, tgt, wmap = (torch.from_numpy(a).cuda() for a in F.make_inputs(83, 2, 1, 204))
+    res = []
+    for ops in (False, True):
+        m.zero_grad(set_to_none=True)
+        lg = m(x, _ops=ops)
+        WeightedCrossEntropyLoss()(lg, tgt, wmap).backward()
+        res.append((lg.detach().double().cpu().numpy(),
+                    {k: p.grad.double().cpu().numpy() for k, p in m.named_parameters()}))
+    (lp, gp), (lo, go) = res
+    assert np.abs(lp - lo).max() <= 1e-3
+    for k in gp:
+        if O.bn_cancelled(k):
+            continue
+        assert _rel(go[k], gp[k]) <= 1e-2, (k, _rel(go[k], gp[k]))

@@ -814,12 +814,12 @@ def test_trainer_hipgraph_replay_label_flag(precision, concurrent):
         for _ in range(24):
             tr.step(x, t, w)          # replay; checks the earlier steps' flags first
         tr.check_targets()
-        keep = int(t[1, 5, 7])
-        t[1, 5, 7] = 7                # out of range for K = 2, in the captured tensor
+        keep = int(t[1, 2, 3])
+        t[1, 2, 3] = 7                # out of range for K = 2, in the captured tensor
         tr.step(x, t, w)
         with pytest.raises(IndexError, match="Target 7 is out of bounds"):
             tr.check_targets()
-        t[1, 5, 7] = keep
+        t[1, 2, 3] = keep
         for _ in range(4):
             tr.step(x, t, w)
         tr.check_targets()

@@ -1696,6 +1696,7 @@ __global__ __launch_bounds__(256) void k_pack_all(const PackJobs jobs) {
 }
 
 hipError_t launch_pack_all(PackJobs jobs, hipStream_t s) {
+  if (jobs.n <= 0 || jobs.n > kPackJobsMax) return hipErrorInvalidValue;  // before touching j[] / first[]
   int blocks = 0;
   for (int j = 0; j < jobs.n; ++j) {
     const PackJob& J = jobs.j[j];
@@ -1703,7 +1704,6 @@ hipError_t launch_pack_all(PackJobs jobs, hipStream_t s) {
     jobs.first[j] = blocks;
     blocks += (J.ci / 32) * (J.co / 32);
   }
-  if (jobs.n <= 0 || jobs.n > kPackJobsMax) return hipErrorInvalidValue;
   jobs.first[jobs.n] = blocks;
   hipLaunchKernelGGL(k_pack_all, dim3(blocks), dim3(256), 0, s, jobs);
   return hipGetLastError();

@@ -1405,7 +1405,8 @@ static void wgrad_tile(int id, int& bm, int& bn) {
 }
 bool wgrad_tile_fits(const WgradArgs& a, int tile) {
   if (wino_tile_m(tile) > g_wino_wgrad_max) return false;
-  if (tile == 71 || tile == 74) return wino_wgrad_applies(a, tile == 71 ? 4 : 6);
+  // the Winograd weight gradients assign G^T Mw G to out: no accumulation
+  if (tile == 71 || tile == 74) return !a.accumulate && wino_wgrad_applies(a, tile == 71 ? 4 : 6);
   if (a.batch > 1 && (tile < 0 || tile > 4)) return false;  // batched: fp32 pixel-column tiles only
   if (tile == 20 || tile == 21) return wgrad3_fits(a);  // halo-tiled 3x3, all taps
   if (tile == 22 || tile == 23) return wgrad3_f32_fits(a);  // fp32 twin
@@ -1503,7 +1504,7 @@ int wgrad_splits(const WgradArgs& a, int tile, int per_cu, int& pps) {
 
 bool wgrad_slab_fits(const WgradArgs& a, int splits) {
   const size_t plane = (size_t)a.Mo * a.No;
-  if (!a.slab || plane % 4 != 0 || (a.batch > 1 && a.batch_out != (long long)plane)) return false;
+  if (!a.slab || a.accumulate || plane % 4 != 0 || (a.batch > 1 && a.batch_out != (long long)plane)) return false;
   return splits == 1 || (size_t)splits * a.batch * plane * sizeof(float) <= a.slab_bytes;
 }
 

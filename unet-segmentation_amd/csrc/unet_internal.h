@@ -110,13 +110,19 @@ struct WgradArgs {
   int Mo, No;        // output rows (ga.Cg) and cols (gb taps * gb.Cg)
   int P;             // pixels
   int pix_per_split;
-  float* out;        // [Mo][No] fp32, accumulated with atomics (zeroed by caller)
+  // [Mo][No] fp32.  Atomic modes ADD into it (the caller zeroes it first);
+  // slab modes (below) OVERWRITE it: the reduction assigns the sum of the
+  // splits, a single split stores straight into it.
+  float* out;
   // optional split-partial slab (bf16 ring weight gradients, wgrad per_cu codes
   // >= 10): each pixel split stores its [Mo][No] partial with plain stores and
-  // one reduction pass adds them into out -- instead of per_cu x CUs x block
-  // fp32 atomics per launch (~9.4 M for every ring launch at 1 per CU)
+  // one reduction pass assigns their sum to out -- instead of per_cu x CUs x
+  // block fp32 atomics per launch (~9.4 M for every ring launch at 1 per CU)
   float* slab = nullptr;
   size_t slab_bytes = 0;
+  // 1: the caller needs out += C (accumulation into earlier contents):
+  // launch_wgrad then refuses slab modes (keeps the atomics)
+  int accumulate = 0;
   int bf16 = 0;      // 1: operands rounded to bf16 when staged (bf16 tiles 10-14)
   int split = 0;     // 1 (with bf16): operands as hi/lo bf16 pairs (UNET_PREC_BF16X3)
   // batched (fp32 tiles 0-4): blockIdx.z = b * splits + split; operand b's

@@ -534,7 +534,7 @@ static hipError_t go_wr(const WgradArgs& a0, hipStream_t s, int per_cu) {
   splits = splits < 1 ? 1 : (splits > tiles ? tiles : splits);
   WgradArgs a = a0;
   const size_t plane = (size_t)a.Mo * a.No;
-  const bool use_slab = slab_mode && a.slab && (size_t)splits * plane * sizeof(float) <= a.slab_bytes &&
+  const bool use_slab = slab_mode && a.slab && !a.accumulate && (size_t)splits * plane * sizeof(float) <= a.slab_bytes &&
                         splits > 1 && plane % 4 == 0;
   if (!use_slab) a.slab = nullptr;
   const dim3 grid(a.Mo / BCO, g.Cg / BCI, splits);

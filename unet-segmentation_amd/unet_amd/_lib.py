@@ -68,6 +68,16 @@ SIGNATURES = {
     "unet_bn_train_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "unet_bn_train_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     "unet_bn_ws_bytes": (_sz, [_i]),
+    "unet_bn_relu_ws_bytes": (_sz, [_i, _i, _i, _i]),
+    "unet_bn_relu_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _f, _f, _i, _i, _vp, _vp, _vp, _vp,
+                              _vp]),
+    "unet_bn_relu_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
+    "unet_conv_first_ws_bytes": (_sz, [_i, _i, _i, _i]),
+    "unet_conv_first_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp]),
+    "unet_conv_first_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    "unet_conv1x1_ws_bytes": (_sz, [_i]),
+    "unet_conv1x1_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp]),
+    "unet_conv1x1_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
     "unet_tracker_create": (_vp, [_i, _i, ctypes.c_double, ctypes.c_double, _i]),
     "unet_tracker_destroy": (None, [_vp]),
     "unet_tracker_ws_bytes": (_sz, [_i, _i]),

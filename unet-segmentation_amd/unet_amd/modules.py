@@ -5,9 +5,12 @@ Mirrors the reference interface:
 * ``UNet(n_channels, n_classes, bilinear=False)`` -- models/unet_model.py:66-146
   (same submodule tree, so ``state_dict`` keys/shapes, ``.apply(init_weights)``
   from scripts/train.py:54-61, ``.parameters()`` for optim.SGD and
-  ``.train()/.eval()`` behave as in the reference).  The submodules are
-  parameter holders; ``UNet.forward`` runs the whole network as one HIP plan
-  (NHWC activations, MFMA implicit GEMM) inside one autograd node.
+  ``.train()/.eval()`` behave as in the reference).  ``UNet.forward`` runs the
+  whole network as one HIP plan (NHWC activations, MFMA implicit GEMM) inside
+  one autograd node.  The submodules' own forwards (``model.inc(x)``,
+  ``model.up1(x1, x2)``, ...) run op by op on the per-op HIP entry points
+  (unet_amd/blocks.py), and so does a backward through an eval-mode forward
+  (recomputed there: the plan's eval forward folds BatchNorm into the convs).
   GEMM precision: fp32 by default; bf16 operands with fp32 accumulation inside
   ``torch.autocast("cuda", dtype=torch.bfloat16)`` (the reference's convs under
   autocast) or when ``model.precision = "bf16"``; ``"bf16x3"`` = fp32-accurate
@@ -27,14 +30,8 @@ import threading
 import torch
 import torch.nn as nn
 
-from . import _lib
+from . import _lib, blocks
 from .plan import PRECISIONS, Plan
-
-
-def _param_holder_forward(self, *a, **k):
-    raise RuntimeError(
-        f"{type(self).__name__} is a parameter holder of the MI355X UNet; call UNet.forward "
-        "(the whole network runs as one HIP plan)")
 
 
 class DoubleConv(nn.Module):
@@ -51,7 +48,8 @@ class DoubleConv(nn.Module):
             nn.ReLU(inplace=True),
         )
 
-    forward = _param_holder_forward
+    def forward(self, x):
+        return blocks.double_conv(self, x)
 
 
 class Down(nn.Module):
@@ -61,7 +59,8 @@ class Down(nn.Module):
         super().__init__()
         self.maxpool_conv = nn.Sequential(nn.MaxPool2d(2), DoubleConv(in_channels, out_channels))
 
-    forward = _param_holder_forward
+    def forward(self, x):
+        return blocks.down(self, x)
 
 
 class Up(nn.Module):
@@ -77,7 +76,10 @@ class Up(nn.Module):
         self.up = nn.ConvTranspose2d(c, c // 2, kernel_size=2, stride=2)
         self.conv = DoubleConv(c // 2 + skip_channels, out_channels)
 
-    forward = _param_holder_forward
+    def forward(self, x1, x2_cropped):
+        """x1 from the previous decoder stage, x2_cropped the skip tensor already
+        cropped to the upsampled size (models/unet_model.py:50-54)."""
+        return blocks.up(self, x1, x2_cropped)
 
 
 class OutConv(nn.Module):
@@ -87,7 +89,8 @@ class OutConv(nn.Module):
         super().__init__()
         self.conv = nn.Conv2d(in_channels, out_channels, kernel_size=1)
 
-    forward = _param_holder_forward
+    def forward(self, x):
+        return blocks.out_conv(self, x)
 
 
 class _Runner:
@@ -154,14 +157,15 @@ class _UNetFunction(torch.autograd.Function):
         plan.forward(tab, x, logits, ws, train)
         ctx.plan, ctx.ws, ctx.tab, ctx.train, ctx.need_bwd = plan, ws, tab, train, need_bwd
         ctx.params = params
+        ctx.module = module if not train else None
         ctx.save_for_backward(x)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
         if not ctx.train:
-            raise RuntimeError("backward through an eval-mode UNet forward is not supported by the MI355X "
-                               "plan (train.py only differentiates train-mode forwards)")
+            dx, *grads = _eval_backward(ctx.module, ctx.saved_tensors[0], dlogits, ctx.params, ctx.needs_input_grad[0])
+            return (dx, None, None, None, *grads)
         if not ctx.need_bwd or ctx.ws is None:
             raise RuntimeError("the MI355X UNet backward needs the workspace of a forward that recorded autograd "
                                "(and it runs once per forward: use retain_graph=False)")
@@ -171,6 +175,24 @@ class _UNetFunction(torch.autograd.Function):
         ctx.plan.backward(ctx.tab, _lib.ptr_array(grads), x, dlogits, ctx.ws)
         ctx.ws = None
         return (None, None, None, None, *grads)
+
+
+def _eval_backward(module, x, dlogits, params, need_x):
+    """Backward through an eval-mode forward (BatchNorm on its running
+    statistics, as reference autograd differentiates model.eval() outputs):
+    the forward is recomputed op by op on the per-op HIP blocks with the same
+    weights (the plan's eval forward folded BatchNorm into the convs and kept
+    no activations) and differentiated there.  Returns (dx, *param grads)."""
+    names = [k for k, _ in module.named_parameters()]
+    with torch.enable_grad():
+        xr = x.detach().requires_grad_(need_x)
+        leaves = {k: p.detach().requires_grad_(True) for k, p in zip(names, params)}
+        out = torch.func.functional_call(module, leaves, (xr,), {"_ops": True}, strict=False)
+        inputs = ([xr] if need_x else []) + list(leaves.values())
+        grads = torch.autograd.grad(out, inputs, dlogits, allow_unused=True)
+    dx = grads[0] if need_x else None
+    pg = grads[1:] if need_x else grads
+    return (dx, *[g if g is not None else torch.zeros_like(p) for g, p in zip(pg, params)])
 
 
 class UNet(nn.Module):
@@ -216,10 +238,14 @@ class UNet(nn.Module):
         """(name, tensor) of all 136 state_dict entries in reference order."""
         return list(self.state_dict(keep_vars=True).items())
 
-    def forward(self, x):
+    def forward(self, x, _ops=False):
         _check_tensor(x, "input")
         if x.dim() != 4 or x.shape[1] != self.n_channels:
             raise ValueError(f"expected input (N, {self.n_channels}, H, W), got {tuple(x.shape)}")
+        if _ops:
+            # the reference's forward op by op on the per-op HIP blocks (fp32
+            # GEMMs): the eval-mode backward's recompute, and a cross-check of the plan
+            return blocks.unet_forward(self, x)
         params = tuple(self.parameters())
         return _UNetFunction.apply(x, self, bool(self.training), self.gemm_precision(), *params)
 
