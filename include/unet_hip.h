@@ -417,6 +417,14 @@ int unet_conv1x1_fwd(const float* x, int n, int h, int w, int c, const float* wt
 int unet_conv1x1_bwd(const float* x, const float* dlogits_nchw, int n, int h, int w, int c, const float* wt, int k,
                      float* dx, float* dw, float* db, void* ws, unet_stream_t stream);
 
+/* Ceilings of this device, measured (bench.py's untimed tail; BASELINE.md asks
+ * for roofline fractions against peaks measured on the box): kind 0 = dense
+ * bf16 MFMA (v_mfma_f32_32x32x16_bf16) TFLOP/s, 1 = f32 MFMA
+ * (v_mfma_f32_16x16x4_f32) TFLOP/s, 2 = HBM float4 copy GB/s (read + write),
+ * 3 = HBM read-only stream GB/s.
+ * Best of `reps` timed launches after a warm-up; allocates its own buffers. */
+int unet_peak_probe(int kind, int reps, double* result, unet_stream_t stream);
+
 #ifdef __cplusplus
 }
 #endif

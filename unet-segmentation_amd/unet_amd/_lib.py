@@ -78,6 +78,7 @@ SIGNATURES = {
     "unet_conv1x1_ws_bytes": (_sz, [_i]),
     "unet_conv1x1_fwd": (_i, [_vp, _i, _i, _i, _i, _vp, _vp, _i, _vp, _vp]),
     "unet_conv1x1_bwd": (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _i, _vp, _vp, _vp, _vp, _vp]),
+    "unet_peak_probe": (_i, [_i, _i, ctypes.POINTER(ctypes.c_double), _vp]),
     "unet_tracker_create": (_vp, [_i, _i, ctypes.c_double, ctypes.c_double, _i]),
     "unet_tracker_destroy": (None, [_vp]),
     "unet_tracker_ws_bytes": (_sz, [_i, _i]),
@@ -148,7 +149,7 @@ def stream_of(device=None):
 # csrc/Makefile SRC_HASH: sha256 over these files, in this order
 _HASHED = ["igemm.hip", "igemm_bf16.hip", "conv3_dma.hip", "conv3_ring.hip", "winograd.hip", "elementwise.hip", "elastic.hip",
            "tiling.hip", "weightmap.hip", "postproc.hip", "track.hip", "ops.hip", "plan.hip", "wgrad3_ring.hip",
-           "conv3_ring_pt.hip", "unet_internal.h", "gemm_common.h", "ring_common.h", "conv3_ring_kernel.h",
+           "conv3_ring_pt.hip", "peak.hip", "unet_internal.h", "gemm_common.h", "ring_common.h", "conv3_ring_kernel.h",
            os.path.join("..", "..", "include", "unet_hip.h")]
 
 
