@@ -64,6 +64,7 @@ HBM_PEAK_GBS = 8000.0
 # stand in only if the probe fails.
 FP32_MFMA_MEASURED_TFLOPS = 155.0
 HBM_MEASURED_GBS = 6290.0
+BOTTLENECK_LAYERS = ("down4.c0", "down4.c1", "up1.convT", "up1.c0")
 GEMM_DESC = {"fp32": "fp32", "bf16": "bf16-operand/fp32-acc",
              "bf16x3": "fp32-accurate bf16x3 split-operand (3 bf16 MFMA products, fp32 acc)"}
 PEAK = {"fp32": FP32_MFMA_PEAK_TFLOPS, "bf16": BF16_MFMA_PEAK_TFLOPS, "bf16x3": round(BF16_MFMA_PEAK_TFLOPS / 3, 1)}
@@ -326,6 +327,7 @@ def run_precision(args, dtype, device, pg, world, rank):
     trainer.plan.set_timing(False)
     tim = trainer.plan.timing()
     xfl = trainer.plan.mfma_flops()
+    sites = trainer.plan.timing_sites()
     comm = None
     if pg is not None:
         comm = {"collective": f"all_reduce(SUM) of {len(trainer.reducer.buckets)} gradient buckets, each issued as its "
@@ -389,7 +391,13 @@ def run_precision(args, dtype, device, pg, world, rank):
                        "frac": round(xfl["bottleneck"] / (bn[0] * 1e-3) / 1e12 / peak, 4) if bn[0] > 0 else None,
                        "frac_measured": round(xfl["bottleneck"] / (bn[0] * 1e-3) / 1e12 / peak_m, 4)
                        if bn[0] > 0 else None,
-                       "direct_conv_tflops": round(bn[1] / (bn[0] * 1e-3) / 1e12, 2) if bn[0] > 0 else None},
+                       "direct_conv_tflops": round(bn[1] / (bn[0] * 1e-3) / 1e12, 2) if bn[0] > 0 else None,
+                       # per launch site: ms and executed-MFMA TFLOP/s (the split of the set)
+                       "sites": {nm: [round(ms, 4), round(xf / (ms * 1e-3) / 1e12, 1) if ms > 0 else None]
+                                 for nm, ms, _, xf in sites if nm.split(" ")[0] in BOTTLENECK_LAYERS}},
+        # every GEMM launch site of the timing step: [ms, executed-MFMA TFLOP/s]
+        "gemm_sites": {nm: [round(ms, 4), round(xf / (ms * 1e-3) / 1e12, 1) if ms > 0 else None]
+                       for nm, ms, _, xf in sites},
         # SURVEY.md §8d target: >= 40 % HBM on stage 1 (inc.c0 + BN0 stats fwd;
         # BN0 backward fused into inc.c0's weight gradient)
         "stage1": {"bound": "hbm", "ms": round(st[0], 3), "launches": st[3],
@@ -501,7 +509,7 @@ def main():
                        "parallelism": f"dp{world}"},
         }
         for k in ("mean_ms_per_step", "wall_value", "step_ms_range", "roofline", "bottleneck", "stage1", "kernels",
-                  "final_loss"):
+                  "gemm_sites", "final_loss"):
             out[k] = main_res[k]
         out["lib"] = {**ident, "tune_db": os.path.relpath(args.tune_db, ROOT) if tune_db_entries > 0 else None,
                       "tune_db_entries": tune_db_entries}
@@ -512,7 +520,7 @@ def main():
                       "mean_ms_per_step": r["mean_ms_per_step"],
                       "config": f"same workload, {GEMM_DESC[d]} GEMMs (global batch {world * args.batch}"
                                 f"{'; configs[2] at N=8' if d == 'bf16' else ''})",
-                      **{k: r[k] for k in ("roofline", "bottleneck", "stage1", "kernels", "final_loss")}}
+                      **{k: r[k] for k in ("roofline", "bottleneck", "stage1", "kernels", "gemm_sites", "final_loss")}}
         if c5 is not None:
             out["c5"] = {"value": c5["value"], "unit": "images/s", "ms_per_step": c5["ms_per_step"],
                          "steps": c5["steps"], "dtype": "bf16",

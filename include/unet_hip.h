@@ -151,6 +151,10 @@ int unet_plan_timing(const unet_plan* p, double* ms, double* flops, double* byte
  * convolution's 2*M*N*K) except where a Winograd variant ran (igemm tiles
  * 70-72/74, wgrad tiles 71/74: 2 * points * tiles * Cin * Cout). */
 int unet_plan_timing_mfma_flops(const unet_plan* p, double* mfma_flops);
+/* Per GEMM launch site of the last step unet_plan_timing() collected: one line
+ * per site, "<layer> <fwd|dgrad|wgrad>\t<ms>\t<direct flops>\t<MFMA flops>".
+ * Copies up to cap bytes (NUL-terminated) into buf; returns the size needed. */
+size_t unet_plan_timing_sites(const unet_plan* p, char* buf, size_t cap);
 
 /* ------------------------------------------------------------------------
  * Loss: WeightedCrossEntropyLoss (utils/losses.py:29-57) fused fwd+bwd.

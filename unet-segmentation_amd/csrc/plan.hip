@@ -15,6 +15,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <array>
 #include <map>
 #include <mutex>
 #include <string>
@@ -135,8 +136,11 @@ struct unet_plan {
     hipEvent_t a, b;
     int cls;
     double flops, bytes, xflops;
+    int site;  // GEMM launch site (site_name), -1 = none
   };
   std::vector<Ev> evs;
+  // per GEMM launch site of the last timed step: ms, direct flops, MFMA flops
+  std::map<int, std::array<double, 3>> sites, sites_last;
   // MFMA flops the chosen GEMM variants execute (Winograd: its point GEMMs),
   // summed on the host as launches are enqueued; Timer intervals take deltas
   double xfl = 0;
@@ -176,6 +180,18 @@ struct Ctx {
 // (and up1.convT, ConvT index 0)
 inline bool bottleneck_conv(int l) { return l == 8 || l == 9 || l == 10; }
 
+// GEMM launch-site ids of the per-site timing report (unet_plan_timing_sites):
+// kind 0 = forward, 1 = input gradient, 2 = weight gradient
+inline int site_conv(int l, int kind) { return l * 4 + kind; }
+inline int site_convT(int k, int kind) { return 100 + k * 4 + kind; }
+std::string site_name(int site) {
+  static const char* kinds[3] = {"fwd", "dgrad", "wgrad"};
+  if (site >= 100) return "up" + std::to_string((site - 100) / 4 + 1) + ".convT " + kinds[site % 4];
+  const int l = site / 4;
+  std::string layer = l < 2 ? "inc" : l < 10 ? "down" + std::to_string(l / 2) : "up" + std::to_string((l - 10) / 2 + 1);
+  return layer + ".c" + std::to_string(l % 2) + " " + kinds[site % 4];
+}
+
 struct Timer {
   unet_plan* p;
   hipStream_t s;
@@ -183,8 +199,9 @@ struct Timer {
   bool ok = false;
   int cls;
   double fl, by, x0;
-  Timer(unet_plan* p_, hipStream_t s_, int c, double f, double by_, bool on = true)
-      : p(p_), s(s_), cls(c), fl(f), by(by_), x0(p_->xfl) {
+  int site;
+  Timer(unet_plan* p_, hipStream_t s_, int c, double f, double by_, bool on = true, int site_ = -1)
+      : p(p_), s(s_), cls(c), fl(f), by(by_), x0(p_->xfl), site(site_) {
     // timing is best effort (bench / tools only): a failed event leaves the
     // interval out of the report instead of failing the plan call
     if (p->timing && on) {
@@ -199,7 +216,7 @@ struct Timer {
   ~Timer() {
     if (p->timing && ok) {
       if (hipEventRecord(b, s) == hipSuccess) {
-        p->evs.push_back({a, b, cls, fl, by, p->xfl - x0});
+        p->evs.push_back({a, b, cls, fl, by, p->xfl - x0, site});
       } else {
         (void)hipEventDestroy(a);
         (void)hipEventDestroy(b);
@@ -716,7 +733,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       a.e.bias = P<float>(prm, T.pw + 1);  // bias[co], col = ab*Co + co
       a.e.shuffle_co = T.co;
       a.e.d[0] = Dst{c.f(T.u), 2 * T.h, 2 * T.w, T.co, 0, 0, p->prec == UNET_PREC_BF16};
-      Timer t(p, s, UNET_KC_CONV_FWD, 2.0 * a.M * a.N * a.K, 0);
+      Timer t(p, s, UNET_KC_CONV_FWD, 2.0 * a.M * a.N * a.K, 0, true, site_convT(k, 0));
       Timer tb(p, s, UNET_KC_BOTTLENECK, 2.0 * a.M * a.N * a.K, 0, k == 0);
       CK(run_igemm(c, a));
     }
@@ -731,7 +748,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
     a.e.d[0] = Dst{c.f(L.y), L.ho, L.wo, L.co, 0, 0, p->prec == UNET_PREC_BF16};
     a.e.stats = train ? c.d(L.stats) : nullptr;
     {
-      Timer t(p, s, UNET_KC_CONV_FWD, conv_flops(L, n), 0);
+      Timer t(p, s, UNET_KC_CONV_FWD, conv_flops(L, n), 0, true, site_conv(l, 0));
       Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
       CK(run_igemm(c, a));
     }
@@ -861,7 +878,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       w.No = 9 * L.ci;
       w.P = n * L.ho * L.wo;
       w.out = c.f(L.dwp);
-      Timer t(p, sw, UNET_KC_CONV_WGRAD, conv_flops(L, n), 0);
+      Timer t(p, sw, UNET_KC_CONV_WGRAD, conv_flops(L, n), 0, true, site_conv(l, 2));
       Timer tb(p, sw, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
       CK(run_wgrad(cw, w));
     }
@@ -890,7 +907,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       a.e.bn_mean = c.f(Q.mean);
       a.e.bn_invstd = c.f(Q.invstd);
       a.e.bstats = c.d(Q.bstats);
-      Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+      Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0, true, site_conv(l, 1));
       Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
       CK(run_igemm(c, a));
     } else if (l <= 8) {  // -> gradient of the pooled tensor, then pool backward
@@ -898,7 +915,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       Pool& pl = p->P[k];
       a.e.d[0] = Dst{c.f(pl.dp), pl.h / 2, pl.w / 2, pl.c, 0, 0, g16};
       {
-        Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+        Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0, true, site_conv(l, 1));
         Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
         CK(run_igemm(c, a));
       }
@@ -917,7 +934,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       a.e.n_split = sk.c;
       a.e.colsum1 = c.d(T.colsum);
       {
-        Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0);
+        Timer t(p, s, UNET_KC_CONV_DGRAD, conv_flops(L, n), 0, true, site_conv(l, 1));
         Timer tb(p, s, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
         CK(run_igemm(c, a));
       }
@@ -954,7 +971,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
         w.No = 4 * T.co;
         w.P = n * T.h * T.w;
         w.out = c.f(T.dwp);
-        Timer t(p, sw, UNET_KC_CONV_WGRAD, 2.0 * w.P * (double)w.Mo * w.No, 0);
+        Timer t(p, sw, UNET_KC_CONV_WGRAD, 2.0 * w.P * (double)w.Mo * w.No, 0, true, site_convT(k, 2));
         Timer tb(p, sw, UNET_KC_BOTTLENECK, 2.0 * w.P * (double)w.Mo * w.No, 0, k == 0);
         CK(run_wgrad(cw, w));
       }
@@ -987,7 +1004,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       b.e.bn_mean = c.f(Q.mean);
       b.e.bn_invstd = c.f(Q.invstd);
       b.e.bstats = c.d(Q.bstats);
-      Timer t(p, s, UNET_KC_CONV_DGRAD, 2.0 * b.M * (double)b.N * b.K, 0);
+      Timer t(p, s, UNET_KC_CONV_DGRAD, 2.0 * b.M * (double)b.N * b.K, 0, true, site_convT(k, 1));
       Timer tb(p, s, UNET_KC_BOTTLENECK, 2.0 * b.M * (double)b.N * b.K, 0, k == 0);
       CK(run_igemm(c, b));
     }
@@ -1417,6 +1434,12 @@ int unet_plan_timing(const unet_plan* pc, double* ms, double* fl, double* by, in
       p->t_by[e.cls] += e.bytes;
       p->t_xf[e.cls] += e.xflops;
       p->t_n[e.cls] += 1;
+      if (e.site >= 0) {
+        auto& v = p->sites[e.site];
+        v[0] += t;
+        v[1] += e.flops;
+        v[2] += e.xflops;
+      }
     }
     (void)hipEventDestroy(e.a);
     (void)hipEventDestroy(e.b);
@@ -1431,7 +1454,26 @@ int unet_plan_timing(const unet_plan* pc, double* ms, double* fl, double* by, in
     p->t_ms[i] = p->t_fl[i] = p->t_by[i] = p->t_xf[i] = 0;
     p->t_n[i] = 0;
   }
+  p->sites_last.swap(p->sites);
+  p->sites.clear();
   return rc;
+}
+
+size_t unet_plan_timing_sites(const unet_plan* p, char* buf, size_t cap) {
+  if (!p) return 0;
+  std::string out;
+  for (const auto& kv : p->sites_last) {
+    char line[160];
+    snprintf(line, sizeof line, "%s\t%.4f\t%.6e\t%.6e\n", site_name(kv.first).c_str(), kv.second[0], kv.second[1],
+             kv.second[2]);
+    out += line;
+  }
+  if (buf && cap) {
+    const size_t m = out.size() < cap - 1 ? out.size() : cap - 1;
+    memcpy(buf, out.data(), m);
+    buf[m] = 0;
+  }
+  return out.size() + 1;
 }
 
 int unet_plan_timing_mfma_flops(const unet_plan* p, double* xfl) {

@@ -40,6 +40,7 @@ SIGNATURES = {
     "unet_plan_set_timing": (_i, [_vp, _i]),
     "unet_plan_timing": (_i, [_vp, _vp, _vp, _vp, _vp]),
     "unet_plan_timing_mfma_flops": (_i, [_vp, _vp]),
+    "unet_plan_timing_sites": (_sz, [_vp, ctypes.c_char_p, _sz]),
     "unet_wce_fwd_bwd": (_i, [_vp, _vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _f, _vp, _vp]),
     "unet_scale_by_device_scalar": (_i, [_vp, _sz, _vp, _vp]),
     "unet_scale_by_device_scalar_out": (_i, [_vp, _vp, _sz, _vp, _vp]),

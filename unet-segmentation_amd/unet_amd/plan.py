@@ -95,3 +95,15 @@ class Plan:
         _lib.check(self.lib.unet_plan_timing_mfma_flops(self.handle, xf), "unet_plan_timing_mfma_flops")
         names = ["conv_fwd", "conv_dgrad", "conv_wgrad", "stage1", "elementwise", "bottleneck"]
         return {names[i]: xf[i] for i in range(n)}
+
+    def timing_sites(self):
+        """[(site, ms, direct flops, MFMA flops)] per GEMM launch site of the
+        step the last timing() call collected (site = "<layer> <fwd|dgrad|wgrad>")."""
+        n = self.lib.unet_plan_timing_sites(self.handle, None, 0)
+        buf = ctypes.create_string_buffer(n)
+        self.lib.unet_plan_timing_sites(self.handle, buf, n)
+        out = []
+        for ln in buf.value.decode().splitlines():
+            name, ms, fl, xf = ln.split("\t")
+            out.append((name, float(ms), float(fl), float(xf)))
+        return out
