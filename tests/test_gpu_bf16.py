@@ -434,13 +434,16 @@ def gemm_mode(request, lib):
                                        "heuristic+wtile110", "heuristic+wtile112",
                                        "heuristic+wtile28", "heuristic+wtile29", "heuristic+wtile30",
                                        "heuristic+wtile31", "heuristic+wtile32", "heuristic+wtile33",
-                                       "norm+heuristic+wtile26"],
+                                       "norm+heuristic+wtile26", "tile91", "tile92", "tile93", "tile94",
+                                       "tile95", "tile96", "tile97", "tile98", "tile99", "tile92+split2",
+                                       "tile95+split3", "tile96+split2"],
                          indirect=True)
 def test_bf16_gemm_variants_vs_bf16_oracle(gemm_mode):
     """Every bf16 tile (21-26 row gather, 31-36 halo-tiled 3x3, 63-67 LDS-DMA
     halo, 81-84 LDS-DMA halo / weight rings -- the convT GEMMs fall back to the
-    built-in tile there) and split-K on every conv / convT / dgrad GEMM of a
-    train step; the weight gradients run the bf16 wgrad tiles."""
+    built-in tile there; 91-95 the convT forward / input-gradient K rings --
+    the 3x3 GEMMs fall back there) and split-K on every conv / convT / dgrad
+    GEMM of a train step; the weight gradients run the bf16 wgrad tiles."""
     params = O.hash_init(1, 2, seed=21, bn_random=True)
     x, tgt, wmap = F.make_inputs(21, 2, 1, 188)
     check_vs_bf16_oracle(make_model(params), params, x, tgt, wmap, gemm_mode)

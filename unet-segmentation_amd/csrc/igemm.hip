@@ -1174,6 +1174,17 @@ static TileInfo tile_info(int id) {
     case 84: return {256, 64, 576, 1};
     // 84 persistent (k_conv3_ring PT): whole K per workgroup
     case 88: return {256, 64, 576, 1};
+    // bf16 convT forward / input gradient on LDS-DMA K rings (k_gemm_ring,
+    // gemm_ring.hip): 64-k stages
+    case 91: return {128, 128, 64, 1};
+    case 92: return {256, 128, 64, 1};
+    case 93: return {128, 256, 64, 1};
+    case 94: return {128, 128, 64, 1};
+    case 95: return {64, 128, 64, 1};
+    case 96: return {256, 256, 32, 1};
+    case 97: return {256, 128, 32, 1};
+    case 98: return {128, 256, 32, 1};
+    case 99: return {128, 128, 32, 1};
     // Winograd F(2x2, 3x3) (winograd.hip): no K split
     case 70: case 71: case 74: return {256, 64, 9, 2};
     case 72: return {32, 32, 16, 1};
@@ -1191,8 +1202,10 @@ static TileInfo tile_info(int id) {
 static bool is_halo_tile(int tile) { return (tile >= 31 && tile <= 36) || (tile >= 41 && tile <= 44); }
 static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 68); }
 static bool is_ring_tile(int tile) { return (tile >= 81 && tile <= 84) || tile == 88; }
+static bool is_gemm_ring_tile(int tile) { return tile >= 91 && tile <= 99; }
 static bool is_bf16_tile(int tile) {
-  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile);
+  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile) ||
+         is_gemm_ring_tile(tile);
 }
 static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 
@@ -1215,6 +1228,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
   if (is_ring_tile(tile)) return conv3_ring_fits(a, tile);
+  if (is_gemm_ring_tile(tile)) return gemm_ring_fits(a, tile);
   if (tile == 70 || tile == 71 || tile == 74) return wino_applies(a, tile == 70 ? 2 : tile == 71 ? 4 : 6);
   if (tile == 72) return wino_fused_applies(a);
   if (tile == 73) return wino_fused64_applies(a);
@@ -1318,6 +1332,8 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
     case 63: case 65: case 66: case 67: case 68: return go_conv3_dma_tile(a, s, tile);
     case 81: case 82: case 83: case 84: case 88: return go_conv3_ring_tile(a, s, tile);
+    case 91: case 92: case 93: case 94: case 95: case 96: case 97: case 98: case 99:
+      return go_gemm_ring_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);
     case 71: return launch_wino(a, s, 4);
     case 74: return launch_wino(a, s, 6);

@@ -174,6 +174,10 @@ bool conv3_ring_tile_shape(int tile, int& th, int& bn, int& ck);
 bool conv3_ring_fits(const IgemmArgs& a, int tile);
 hipError_t go_conv3_ring_tile(const IgemmArgs& a, hipStream_t s, int tile);
 hipError_t go_conv3_ring_pt(const IgemmArgs& a, hipStream_t s, int tile);  // conv3_ring_pt.hip (83, 84, 88)
+// bf16 convT forward / input gradient on LDS-DMA K rings (gemm_ring.hip), tile ids 91-99
+bool gemm_ring_tile_shape(int tile, int& bm, int& bn);
+bool gemm_ring_fits(const IgemmArgs& a, int tile);
+hipError_t go_gemm_ring_tile(const IgemmArgs& a, hipStream_t s, int tile);
 int num_cus();
 
 // Timing-ablation switches (UNET_WG_ABL, UNET_WF_ABL, UNET_WF64_ABL: kernel
