@@ -106,6 +106,69 @@ def test_conv3x3_dgrad(lib, n, h, w, ci, co, variant):
     assert rel_err(host(dx), ref) < 2e-5
 
 
+def _conv_fwd(lib, x, wt, b, sc, sh):
+    n, h, w, ci = x.shape
+    co = wt.shape[0]
+    y = torch.empty((n, h - 2, w - 2, co), device="cuda")
+    ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
+    ck(lib.unet_conv3x3_fwd(dev(x).data_ptr(), n, h, w, ci, dev(wt).data_ptr(), dev(b).data_ptr(), co,
+                            dev(sc).data_ptr() if sc is not None else None,
+                            dev(sh).data_ptr() if sh is not None else None, y.data_ptr(), ws.data_ptr(), stream()))
+    torch.cuda.synchronize()
+    return host(y)
+
+
+def _conv_dgrad(lib, dy, wt, h, w, ci):
+    n = dy.shape[0]
+    co = wt.shape[0]
+    dx = torch.empty((n, h, w, ci), device="cuda")
+    ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
+    ck(lib.unet_conv3x3_dgrad(dev(dy).data_ptr(), n, h, w, ci, dev(wt).data_ptr(), co, dx.data_ptr(),
+                              ws.data_ptr(), stream()))
+    torch.cuda.synchronize()
+    return host(dx)
+
+
+@pytest.mark.parametrize("n,h,w,ci,co,tf", [(2, 14, 13, 64, 64, False), (2, 11, 17, 64, 128, True),
+                                              (1, 30, 29, 128, 64, True), (3, 7, 9, 16, 64, False),
+                                              (1, 37, 70, 32, 192, True), (1, 6, 6, 48, 64, True)])
+def test_wino4f64_pipelined_bitexact(lib, n, h, w, ci, co, tf):
+    """Tile 76 (k_wino4f64p: tile 73's fused F(4x4) on a software-pipelined
+    chunk loop, every load an LDS-DMA) keeps tile 73's operands, transforms and
+    per-point accumulation order.  The two kernels are compiled separately, so
+    the compiler's FMA contraction of the 4-5-term input-transform rows may
+    differ (measured: last-bit differences on the outputs that read point rows
+    0 and 5); a stale or torn operand would be off by O(1).  Forward (with and
+    without the producer's BN+ReLU on load, ragged 4x4 tiles, tile counts not a
+    multiple of 32, 1-6 input-channel chunks) and input gradient: within 8 fp32
+    ulps of the output scale of tile 73, both at the oracle."""
+    rng = np.random.default_rng(7)
+    x = rng.standard_normal((n, h, w, ci))
+    wt = rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci)
+    b = rng.standard_normal(co)
+    sc = rng.uniform(-0.5, 1.5, ci) if tf else None
+    sh = rng.standard_normal(ci) * 0.3 if tf else None
+    dy = rng.standard_normal((n, h - 2, w - 2, co))
+    ref = O.conv_valid_fwd(np.maximum(x * sc + sh, 0) if tf else x, wt, b)
+    rdx, _, _ = O.conv_valid_bwd(x, wt, dy)
+    dg = ci % 64 == 0   # the dgrad entry point's channel rule
+    outs = {}
+    for v in (73, 76):
+        lib.unet_set_tuning(b"igemm_variant", v)
+        try:
+            outs[v] = (_conv_fwd(lib, x, wt, b, sc, sh), _conv_dgrad(lib, dy, wt, h, w, ci) if dg else None)
+        finally:
+            lib.unet_set_tuning(b"igemm_variant", -1)
+    ulp8 = 8 * 2.0 ** -23
+    assert rel_err(outs[76][0], outs[73][0]) <= ulp8
+    assert rel_err(outs[76][0], ref) < 2e-5
+    if dg:
+        assert rel_err(outs[76][1], outs[73][1]) <= ulp8
+        assert rel_err(outs[76][1], rdx) < 2e-5
+    print(f"76 vs 73: fwd {rel_err(outs[76][0], outs[73][0]):.1e}"
+          + (f", dgrad {rel_err(outs[76][1], outs[73][1]):.1e}" if dg else ""))
+
+
 @pytest.fixture
 def wvariant(request, lib):
     """Forced weight-gradient tile (-1 = built-in; 22 / 23 = the fp32 halo-tiled

@@ -29,7 +29,12 @@ CASES = [(1, 2, 2, 512, "fp32", "module"), (3, 2, 2, 572, "fp32", "trainer"), (3
          (1, 2, 8, 512, "fp32", "trainer"), (1, 2, 8, 512, "bf16", "trainer")]
 # tests/test_gpu_model.py::test_channel_and_class_counts_vs_oracle (bench_tuning)
 CASES += [(c, k, 2, 188, "fp32", "module") for c, k in ((2, 3), (3, 1), (4, 4), (5, 5), (1, 9), (16, 2), (1, 17),
-                                                            (3, 32))]
+                                                            (3, 32), (20, 2), (1, 33), (17, 70))]
+# tests/test_gpu_model.py's small train steps (vs the oracle, odd pooling sizes)
+# in every precision, so that those tests replay recorded choices too (VERDICT
+# r04 weak item 8: 126-189 live-tuned shapes per suite run)
+CASES += [(1, 2, n, h, p, "module") for n, h in ((2, 188), (2, 204), (1, 220), (2, 195), (1, 198))
+          for p in ("fp32", "bf16", "bf16x3")]
 
 
 def main():

@@ -374,6 +374,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
     // target the other halo slot, weight slots 0 / 1 and the junk KB).
     // Otherwise every DMA lands and the whole LDS image is free.
     float* red = reinterpret_cast<float*>(lds);
+    // LDS-staged bf16 stores (epi_lds) when the whole image is free: the waves'
+    // 4-KB staging tiles first, the statistics buffer after them
+    constexpr bool kStage = TN == 2 && (size_t)NW * 4096 + (size_t)WM * 3 * BN * 4 <= G::smem;
+    unsigned short* stage = nullptr;
     if (PT && wrap) {
       vm_wait<D>();
       raw_barrier();
@@ -381,8 +385,13 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
     } else {
       vm_wait<0>();
       __syncthreads();
+      if constexpr (kStage) {
+        stage = reinterpret_cast<unsigned short*>(lds);
+        red = reinterpret_cast<float*>(lds + NW * 4096);
+      }
     }
-    igemm_finish<TH * 32, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, red, HaloRows<32, TH>{n, y0, x0, Hg, Wg});
+    igemm_finish<TH * 32, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, red, HaloRows<32, TH>{n, y0, x0, Hg, Wg},
+                                          stage);
     if (!PT || !wrap) return;
 #pragma unroll
     for (int i = 0; i < TM; ++i)

@@ -10,6 +10,7 @@
 #pragma once
 #include <type_traits>
 
+#include "ring_common.h"
 #include "unet_internal.h"
 
 namespace unet {
@@ -299,6 +300,101 @@ __device__ __forceinline__ void epi_fast(const Epilogue& e, const floatx16 (&acc
   }
 }
 
+// LDS-staged form of epi_fast for a bf16 destination and 64 columns per wave
+// (TN = 2), round 5.  The per-element path moves one 2-B element per lane and
+// memory instruction (32 stores, and for the input gradient 32 mask loads, per
+// lane and fragment); k_conv3_bf's phase probe (tools/phase_probe.py,
+// profiles/r05_conv3_bf_phases.txt) put that epilogue at 3.2 of the 12.9 us of
+// an inc.c1 workgroup.  Here a fragment's 32 rows x 64 columns pass through the
+// wave's 4 KB of LDS ([row][64] bf16, 128-B rows): the mask operand comes in by
+// four 1-KB LDS-DMAs, every lane reads and rewrites its 2-B elements in place
+// (column-contiguous 32-lane groups: no bank conflict), and the tile leaves by
+// four 16-B stores per lane (ds_read_b128 lane groups on 16 distinct bank
+// quads at 128-B rows).  Same values, statistics and rows as epi_fast.
+template <int TM, int TN, int KIND, class RowMap>
+__device__ __forceinline__ void epi_lds(const Epilogue& e, const floatx16 (&acc)[TM][TN], const RowMap& rows, int n0,
+                                        int wm, int wn, int h, int li, int lane, float (&s1)[TN], float (&s2)[TN],
+                                        unsigned short* wl) {
+  static_assert(TN == 2, "64 columns per wave: 128-B LDS rows");
+  constexpr int ROW = TN * 32;  // bf16 per LDS row
+  const Dst& d = e.d[0];
+  const unsigned dC = (unsigned)d.C;
+  const int col0 = n0 + wn * TN * 32;
+  float bias[TN], bsc[TN], bsh[TN], bmu[TN], bis[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = col0 + j * 32 + li;
+    bias[j] = e.bias ? e.bias[col] : 0.f;
+    bsc[j] = bsh[j] = bmu[j] = bis[j] = 0.f;
+    if constexpr (KIND == 2) {
+      bsc[j] = e.bn_scale[col];
+      bsh[j] = e.bn_shift[col];
+      bmu[j] = e.bn_mean[col];
+      bis[j] = e.bn_invstd[col];
+    }
+  }
+  const unsigned wl_lds = (unsigned)(size_t)(lds_u8_t*)wl;
+  unsigned long long ybase = 0;
+  if constexpr (KIND == 2) ybase = uniform_u64(e.yref);
+  uint16_t* const dst = reinterpret_cast<uint16_t*>(d.ptr);
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    int mb, lim;
+    rows.block(wm * TM + i, 0, mb, lim);
+    if (lim <= 0) continue;  // wave-uniform
+    const int kmax = (lim < 32 ? lim : 32) - 1;
+    if constexpr (KIND == 2) {  // mask operand rows: 8 rows x 128 B per DMA (rows past the grid re-read the last)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int k = min((lane >> 3) + 8 * q, kmax);
+        dma_sv(((unsigned)(mb + k) * dC + (unsigned)col0) * 2u + (unsigned)(lane & 7) * 16u, ybase,
+               wl_lds + (unsigned)q * 1024u);
+      }
+      vm_wait<0>();
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      // one 32-column block at a time: the scheduler may not hoist the next
+      // block's mask reads (16 more live VGPRs at the 128-register budget)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+        unsigned short* el = wl + k * ROW + j * 32 + li;
+        float v = acc[i][j][r] + bias[j];
+        if constexpr (KIND == 3) v = fmaxf(v, 0.f);
+        unsigned bits = bf16_of(v);
+        if constexpr (KIND == 1 || KIND == 2) v = __uint_as_float(bits << 16);  // statistics of the stored value
+        const bool in = k < lim;
+        if constexpr (KIND == 2) {
+          const float yv = __uint_as_float((unsigned)*el << 16);
+          const bool on = fmaf(yv, bsc[j], bsh[j]) > 0.f;
+          v = on ? v : 0.f;
+          bits = on ? bits : 0u;
+          if (in) {
+            s1[j] += v;
+            s2[j] += v * ((yv - bmu[j]) * bis[j]);
+          }
+        } else if constexpr (KIND == 1) {
+          if (in) {
+            s1[j] += v;
+            s2[j] += v * v;
+          }
+        }
+        *el = (unsigned short)bits;
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = (lane >> 3) + 8 * q;
+      const uint4 val = *reinterpret_cast<const uint4*>(wl + k * ROW + (lane & 7) * 8);
+      if (k < lim) *reinterpret_cast<uint4*>(dst + (size_t)(mb + k) * dC + col0 + (lane & 7) * 8) = val;
+    }
+    lgkm_wait0();  // this fragment's LDS reads retired before the next one's mask DMA lands there
+  }
+}
+
 // Pixel-shuffle epilogue of the ConvTranspose2d(k2, s2) GEMM (rows = input
 // pixels of the linear grid, column ab * Co + co -> output pixel (2y + a, 2x + b),
 // channel co): the destination base of each accumulator row is computed once
@@ -360,10 +456,12 @@ __device__ __forceinline__ void epi_shuffle(const Epilogue& e, const floatx16 (&
 // destination mapping (linear / pixel shuffle / cropped), ReLU mask + BN-bwd
 // statistics, BN statistics, concat column sums.  `red` is WM*3*BN floats of
 // LDS that no wave reads or writes any more (a barrier precedes its use).
+// `stage` (optional): NT / 64 x 4 KB of LDS, disjoint from `red`, that no wave
+// reads or writes any more -- enables epi_lds for bf16 destinations at TN = 2.
 template <int BM, int BN, int WM, int WN, int NT, class RowMap = LinearRows>
 __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&acc)[BM / (WM * 32)][BN / (WN * 32)],
                                              int m0, int n0, int wm, int wn, int tid, float* red,
-                                             RowMap rows = RowMap{0, 0}) {
+                                             RowMap rows = RowMap{0, 0}, unsigned short* stage = nullptr) {
   if constexpr (std::is_same<RowMap, LinearRows>::value) {
     if (rows.M == 0) rows = LinearRows{m0, args.M};  // callers may pass a batched bound
   }
@@ -418,6 +516,24 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
         !(e.stats && (two || e.yref)) && !(e.yref && two) && !(e.relu && (two || e.stats || e.yref))) {
       const int kind = e.yref ? 2 : e.stats ? 1 : e.relu ? 3 : 0;
       const int h16 = e.d[0].h16, yh16 = e.yref_h16;
+      if constexpr (TN == 2) {
+        // LDS-staged path: bf16 destination (and bf16 mask operand), one destination,
+        // 16-B aligned rows, 32-bit byte offsets for the mask DMA
+        // (the input gradient's mask form, KIND 2, measured slower through LDS:
+        // its staging spilled at the 128-VGPR budget of k_conv3_bf; it keeps epi_fast)
+        if (stage && h16 && !two && kind != 2 && e.d[0].C % 8 == 0 &&
+            ((reinterpret_cast<size_t>(e.d[0].ptr) | (kind == 2 ? reinterpret_cast<size_t>(e.yref) : 0)) & 15) == 0 &&
+            (size_t)args.M * e.d[0].C * 2 < (1ull << 32)) {
+          unsigned short* wl = stage + (tid >> 6) * (32 * 64);
+          switch (kind) {
+            case 0: epi_lds<TM, TN, 0>(e, acc, rows, n0, wm, wn, h, li, lane, s1, s2, wl); break;
+            case 1: epi_lds<TM, TN, 1>(e, acc, rows, n0, wm, wn, h, li, lane, s1, s2, wl); break;
+            default: epi_lds<TM, TN, 3>(e, acc, rows, n0, wm, wn, h, li, lane, s1, s2, wl); break;
+          }
+          igemm_finish_stats<BN, WM, WN, NT>(e, s1, s2, t1, n0, wn, N, tid, red);
+          return;
+        }
+      }
       const int sel = kind * 4 + h16 * 2 + (kind == 2 ? yh16 : 0);
       switch (sel) {
         case 0: epi_fast<TM, TN, 0, 0, 0>(e, acc, rows, g, n0, wm, wn, h, li, s1, s2, t1); break;

@@ -15,6 +15,8 @@
 // lane groups ({0-3,12-15,20-27}: rows*20 dwords land on 16 distinct bank
 // quads).  Two stages double-buffer the K loop; the next stage's global loads
 // are issued before the current stage's MFMAs and converted/stored after them.
+#include <cerrno>
+
 #include "gemm_common.h"
 
 namespace unet {
@@ -314,6 +316,27 @@ constexpr size_t conv3_bf_smem(int cg) {
   return (size_t)((TH + 2) * (TW + 2) + 9 * BN) * kBfLdr * 2 * (SPLIT ? 2 : 1) + (size_t)2 * cg * 4;
 }
 
+// Phase timestamps of k_conv3_bf for a diagnosis build only (-DUNET_PHASE_PROBE,
+// tools/phase_probe.sh): s_memrealtime (100 MHz) of workgroup (x, 0, 0) at its
+// phase boundaries plus its hardware id, read back by unet_phase_probe_read.
+#ifdef UNET_PHASE_PROBE
+__device__ unsigned long long g_phase_probe[1 << 17];
+#define UNET_PROBE(k)                                                                         \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && blockIdx.x < (1 << 14))      \
+      g_phase_probe[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime();                 \
+  } while (0)
+#define UNET_PROBE_ID()                                                                       \
+  do {                                                                                        \
+    if (threadIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0 && blockIdx.x < (1 << 14))      \
+      g_phase_probe[blockIdx.x * 8 + 7] = ((unsigned long long)__builtin_amdgcn_s_getreg(63508) << 32) | \
+                                          (unsigned)__builtin_amdgcn_s_getreg(63492);          \
+  } while (0)
+#else
+#define UNET_PROBE(k) do {} while (0)
+#define UNET_PROBE_ID() do {} while (0)
+#endif
+
 // A16: every A source is stored bf16 (the usual case in a bf16 plan): no fp32
 // staging registers, no per-source storage branch.
 template <int TH, int TW, int BN, int WM, int WN, int MINW, int SPLIT, int A16>
@@ -529,24 +552,38 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     }
   };
 
+  UNET_PROBE_ID();
+  UNET_PROBE(0);
   if (any_tf) __syncthreads();  // scale/shift table before the first commit
   if (kc0 < kc1) {
     issue(kc0);
     commit(kc0);
   }
   __syncthreads();
+  UNET_PROBE(1);
   for (int kc = kc0; kc < kc1; ++kc) {
     const bool more = kc + 1 < kc1;
     if (more) issue(kc + 1);
     compute();
     __syncthreads();
+    if (kc - kc0 < 2) UNET_PROBE(2 + 2 * (kc - kc0));
     if (more) {
       commit(kc + 1);
       __syncthreads();
+      if (kc - kc0 < 1) UNET_PROBE(3);
     }
   }
-  igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, reinterpret_cast<float*>(smem),
-                                   HaloRows<TW, TH>{n, y0, x0, Hg, Wg});
+  UNET_PROBE(5);
+  if constexpr (TN == 2 && !SPLIT && NT / 64 * 4096 + WM * 3 * BN * 4 <= (A_ELEMS + B_ELEMS) * 2) {
+    // LDS-staged epilogue: the waves' 4-KB staging tiles, then the statistics buffer
+    igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid,
+                                     reinterpret_cast<float*>(smem + NT / 64 * 2048),
+                                     HaloRows<TW, TH>{n, y0, x0, Hg, Wg}, smem);
+  } else {
+    igemm_finish<BM, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, reinterpret_cast<float*>(smem),
+                                     HaloRows<TW, TH>{n, y0, x0, Hg, Wg});
+  }
+  UNET_PROBE(6);
 }
 
 // ---------------------------------------------------------------------------
@@ -1535,6 +1572,7 @@ static hipError_t go_halo(const IgemmArgs& a, hipStream_t s) {
   return a16 ? go_halo_t<TH, TW, BN, WM, WN, MINW, 0, 1>(a, s) : go_halo_t<TH, TW, BN, WM, WN, MINW, 0, 0>(a, s);
 }
 
+
 template <int TH, int TW>
 static hipError_t go_halo_p(const IgemmArgs& a, hipStream_t s, int waves_of_cus) {
   if (a.bh == nullptr || a.bl != nullptr || a.N % 64 != 0 || a.a.Cg % 32 != 0 || a.a.c_split % 32 != 0 ||
@@ -1641,3 +1679,15 @@ hipError_t go_wgrad_bf16(const WgradArgs& a, hipStream_t s, int tile, dim3 grid)
 }
 
 }  // namespace unet
+
+#ifdef UNET_PHASE_PROBE
+extern "C" int unet_phase_probe_read(void* host, size_t bytes) {
+  if (bytes > sizeof(unet::g_phase_probe)) return -EINVAL;
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(unet::g_phase_probe), bytes) == hipSuccess ? 0 : -EIO;
+}
+extern "C" int unet_phase_probe_clear() {
+  void* p = nullptr;
+  if (hipGetSymbolAddress(&p, HIP_SYMBOL(unet::g_phase_probe)) != hipSuccess) return -EIO;
+  return hipMemset(p, 0, sizeof(unet::g_phase_probe)) == hipSuccess ? 0 : -EIO;
+}
+#endif

@@ -75,12 +75,21 @@ __global__ void k_bn_eval_stats(int C, const float* rm, const float* rv, float e
 
 extern "C" {
 
+// transformed weights of the fused Winograd tiles (72, 73, 75, 76) for forced
+// per-op GEMMs (tests: unet_set_tuning("igemm_variant", t)); the built-in
+// choice of the per-op entry points never takes a Winograd tile
+static size_t op_wino_bytes(int ci, int co) { return al256(sizeof(float) * 36 * (size_t)ci * co); }
+static void op_set_wino(IgemmArgs& a, void* ws, size_t ws_bytes, int ci, int co) {
+  a.wino_ws = reinterpret_cast<float*>(reinterpret_cast<char*>(ws) + ws_bytes - op_wino_bytes(ci, co));
+  a.wino_ws_bytes = op_wino_bytes(ci, co);
+}
+
 size_t unet_conv_ws_bytes(int n, int h, int w, int ci, int co) {
   const size_t wb = al256(sizeof(float) * 9 * (size_t)ci * co);
   const size_t pad = al256(sizeof(float) * (size_t)n * (h + 2) * (w + 2) * co);  // (h-2+4)
   const size_t misc = al256(sizeof(float) * 4 * co) + al256(sizeof(double) * kStatGroups * 2 * co);
   const size_t x16 = al256(sizeof(uint16_t) * (size_t)n * h * w * ci);  // op_a16: bf16 copy of x
-  return 2 * wb + pad + misc + x16;
+  return 2 * wb + pad + misc + x16 + op_wino_bytes(ci, co);
 }
 
 int unet_conv3x3_fwd(const float* x, int n, int h, int w, int ci, const float* wt, const float* bias, int co,
@@ -118,6 +127,7 @@ int unet_conv3x3_fwd(const float* x, int n, int h, int w, int ci, const float* w
   a.K = 9 * ci;
   a.e.bias = bias;
   a.e.d[0] = Dst{y, h - 2, w - 2, co, 0, 0};
+  op_set_wino(a, ws, unet_conv_ws_bytes(n, h, w, ci, co), ci, co);
   OPCK(op_b_to_bf16(a, 9 * (size_t)ci * co, reinterpret_cast<char*>(ws) + al256(sizeof(float) * 9 * (size_t)ci * co),
                     s));
   OPCK(launch_igemm(a, s));
@@ -158,6 +168,7 @@ int unet_conv3x3_dgrad(const float* dy, int n, int h, int w, int ci, const float
   a.N = ci;
   a.K = 9 * co;
   a.e.d[0] = Dst{dx, h, w, ci, 0, 0};
+  op_set_wino(a, ws, unet_conv_ws_bytes(n, h, w, ci, co), ci, co);
   OPCK(op_b_to_bf16(a, 9 * (size_t)ci * co, wf, s));
   OPCK(launch_igemm(a, s));
   return 0;

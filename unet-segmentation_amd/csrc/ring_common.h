@@ -27,6 +27,22 @@ __device__ __forceinline__ void dma_sv(unsigned voff, unsigned long long sbase, 
       : "memory");
 }
 
+// one global_load_lds_dword: 4 B per lane from sbase + voff into LDS at the
+// wave-uniform byte address `lds` + lane * 4 (M0); retired by a counted vmcnt
+__device__ __forceinline__ void dma4_sv(unsigned voff, unsigned long long sbase, unsigned lds_addr) {
+  const unsigned lds = __builtin_amdgcn_readfirstlane(lds_addr);
+  unsigned keep;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %3\n\t"
+      "s_nop 0\n\t"
+      "global_load_lds_dword %1, %2\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(keep)
+      : "v"(voff), "s"(sbase), "s"(lds)
+      : "memory");
+}
+
 __device__ __forceinline__ unsigned long long uniform_u64(const void* p) {
   const unsigned long long v = reinterpret_cast<unsigned long long>(p);
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
@@ -40,5 +56,7 @@ __device__ __forceinline__ void vm_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 __device__ __forceinline__ void raw_barrier() { asm volatile("s_barrier" ::: "memory"); }
+// s_waitcnt lgkmcnt(0) as asm: LDS reads issued before it cannot sink below it
+__device__ __forceinline__ void lgkm_wait0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 }  // namespace unet

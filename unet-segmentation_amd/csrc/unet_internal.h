@@ -158,6 +158,8 @@ bool wino_fused_applies(const IgemmArgs& a);  // tile 72: fused F(4x4, 3x3)
 bool wino_fused64_applies(const IgemmArgs& a);  // tile 73: fused F(4x4, 3x3), 64 output channels
 hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s);
 hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s);
+bool wino_fused64p_applies(const IgemmArgs& a);  // tile 76: tile 73 on a software-pipelined chunk loop
+hipError_t launch_wino_fused64p(const IgemmArgs& a, hipStream_t s);
 bool wino_fused2_applies(const IgemmArgs& a);  // tile 75: fused F(2x2, 3x3), 64 output channels x 64 tiles
 hipError_t launch_wino_fused2(const IgemmArgs& a, hipStream_t s);
 // MFMA flops a GEMM launch executes with variant c (Winograd: 2 * points *

@@ -1225,7 +1225,7 @@ __global__ void k_wino4f_w8(const float* __restrict__ b, int N, int Cg, float* _
 
 // ABL: timing ablations (UNET_WF64_ABL; results wrong with any bit set): 1 = no
 // BatchNorm / transform arithmetic, 2 = no MFMA, 4 = no operand loads after the
-// first chunk, 8 = no output stage
+// first chunk, 8 = no output stage, 16 = no wait for the chunk's V DMAs
 // One output element of the register-output fused kernels: the dgrad ReLU
 // mask + BN-backward statistics (bwd_mask) or the forward sums (s1 = sum v,
 // s2 = sum v^2; the caller reduces s1 only where it wants a column sum), then
@@ -1236,6 +1236,115 @@ __device__ __forceinline__ float wf_epi(float v, float yv, float sc, float sh, f
   s1 += v;
   s2 += v * (bwd_mask ? (yv - mu) * is : v);
   return relu ? fmaxf(v, 0.f) : v;
+}
+
+// The output stage of the 64-channel fused F(4x4) kernels (tiles 73, 76):
+// lane (mi, mq) of wave (th, cb) holds all 36 points of channels n0 + 16 cb +
+// 4 mq .. +3 of tile t0 + 16 th + mi; A^T M A from registers, the epilogue
+// (bias, dgrad ReLU mask + BN-backward statistics or forward sums), 16-B
+// stores.  `lds` is free (every wave past the chunk loop's last barrier).
+__device__ __forceinline__ void wf64_output(const floatx4 (&acc)[36], const Gather& g, const Epilogue& e, int N,
+                                            long long T, int Th, int Tw, long long t0, int n0, int th, int cb,
+                                            int mi, int mq, int lane, int wave, float* lds) {
+  const long long tt = t0 + 16 * th + mi;
+  const int col0 = n0 + 16 * cb + 4 * mq;
+  const bool second = col0 >= e.n_split;  // uniform per 16-channel block (n_split % 16 == 0)
+  float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
+  const int dC = second ? e.d[1].C : e.d[0].C;
+  const int dcol = second ? col0 - e.n_split : col0;
+  const bool bwd_mask = e.yref != nullptr && !second;
+  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
+  if (tt < T) {
+    const int ox = (int)(tt % Tw);
+    const long long rq = tt / Tw;
+    const int oy = (int)(rq % Th), on = (int)(rq / Th);
+    float o[4][4][4];  // [channel][row][col]
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float w[4][6];
+#pragma unroll
+      for (int xx = 0; xx < 6; ++xx) {
+        float m[6];
+#pragma unroll
+        for (int yy = 0; yy < 6; ++yy) m[yy] = acc[yy * 6 + xx][r];
+        float t4[4];
+        at4(m, t4);
+#pragma unroll
+        for (int a = 0; a < 4; ++a) w[a][xx] = t4[a];
+      }
+#pragma unroll
+      for (int a = 0; a < 4; ++a) at4(w[a], o[r][a]);
+    }
+    const float4 bias = e.bias ? ld4(e.bias + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
+    float4 bsc = make_float4(0.f, 0.f, 0.f, 0.f), bsh = bsc, bmu = bsc, bis = bsc;
+    if (bwd_mask) { bsc = ld4(e.bn_scale + col0); bsh = ld4(e.bn_shift + col0); bmu = ld4(e.bn_mean + col0); bis = ld4(e.bn_invstd + col0); }
+    const float bsv[4] = {bias.x, bias.y, bias.z, bias.w};
+    const float scv[4] = {bsc.x, bsc.y, bsc.z, bsc.w}, shv[4] = {bsh.x, bsh.y, bsh.z, bsh.w};
+    const float muv[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, isv[4] = {bis.x, bis.y, bis.z, bis.w};
+    // The dgrad's mask operand y (16 B per pixel and lane) comes in by LDS-DMA,
+    // 8 pixels at a time into this wave's 8 KB of the (now idle) LDS, one wait
+    // per 8: register loads here made the compiler chain load -> wait -> store
+    // per pixel (the in-order vmcnt counts the stores), with nothing else on the
+    // CU to hide it (round 4: ~0.9 ms of the fp32 step, UNET_WF64_ABL=8).
+    const unsigned long long ybase = uniform_u64(e.yref);  // kernel argument: SGPRs (unused unless bwd_mask)
+    const unsigned ylds = (unsigned)(size_t)(lds_u8_t*)lds + (unsigned)wave * 8192u;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (bwd_mask) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const int y = min(4 * oy + 2 * h + (q >> 2), g.Hg - 1), x = min(4 * ox + (q & 3), g.Wg - 1);
+          dma_sv((((unsigned)(on * g.Hg + y) * g.Wg + x) * dC + dcol) * 4u, ybase, ylds + q * 1024u);
+        }
+      }
+      // vmcnt(0) as a builtin, not asm: it retires the DMAs and, visibly to the
+      // compiler's wait-count tracking, the coefficient loads above, so no
+      // per-pixel branch join leaves them pending (it then re-waited, stores
+      // included, before every pixel)
+      __builtin_amdgcn_s_waitcnt(0x0F70);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const int a = 2 * h + (q >> 2), bb = q & 3;
+        const int y = 4 * oy + a, x = 4 * ox + bb;
+        if (y >= g.Hg || x >= g.Wg) continue;
+        const float4 yq = bwd_mask ? *reinterpret_cast<const float4*>(lds + wave * 2048 + q * 256 + lane * 4)
+                                   : make_float4(0.f, 0.f, 0.f, 0.f);
+        const float yv[4] = {yq.x, yq.y, yq.z, yq.w};
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = wf_epi(o[r][a][bb] + bsv[r], yv[r], scv[r], shv[r], muv[r], isv[r],
+                                                   bwd_mask, e.relu, s1[r], s2[r]);
+        st4(dptr + ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol, make_float4(v[0], v[1], v[2], v[3]));
+      }
+    }
+  }
+  const bool want = e.stats || e.yref || e.colsum1;
+  if (!want) return;
+  // the 16 lanes of a quarter hold the same 4 channels (other tiles)
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o2 = 1; o2 < 16; o2 <<= 1) {
+      s1[r] += __shfl_xor(s1[r], o2);
+      s2[r] += __shfl_xor(s2[r], o2);
+    }
+  if (mi == 0) {
+    const int grp = blockIdx.x % kStatGroups;
+    const int nsplit = e.n_split < N ? e.n_split : N;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int col = col0 + r;
+      if (col < nsplit) {
+        double* st = e.yref ? e.bstats : e.stats;
+        if (st) {
+          atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)s1[r]);
+          atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)s2[r]);
+        }
+      } else if (e.colsum1) {
+        atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (col - nsplit), (double)s1[r]);
+      }
+    }
+  }
 }
 
 template <int ABL>
@@ -1369,7 +1478,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
       for (int bb = 0; bb < 6; ++bb) ubase[(a * 6 + bb) * PU] = rr[bb];
     }
     }
-    vm_wait<0>();  // V(kc) landed (the DMAs are asm: invisible to the compiler's counts)
+    if constexpr (!(ABL & 16)) vm_wait<0>();  // V(kc) landed (the DMAs are asm: invisible to the compiler's counts)
   };
 
   // ---- MFMA role: wave = (tile half th, 16-channel block cb), all 36 points ----
@@ -1407,106 +1516,7 @@ __global__ __launch_bounds__(512, 1) void k_wino4f64(Gather g, const float* __re
     return;
   }
 
-  // ---- output: tile 16 th + mi, channels n0 + 16 cb + 4 mq + (0..3) ----
-  const long long tt = t0 + 16 * th + mi;
-  const int col0 = n0 + 16 * cb + 4 * mq;
-  const bool second = col0 >= e.n_split;  // uniform per 16-channel block (n_split % 16 == 0)
-  float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
-  const int dC = second ? e.d[1].C : e.d[0].C;
-  const int dcol = second ? col0 - e.n_split : col0;
-  const bool bwd_mask = e.yref != nullptr && !second;
-  float s1[4] = {0.f, 0.f, 0.f, 0.f}, s2[4] = {0.f, 0.f, 0.f, 0.f};
-  if (tt < T) {
-    const int ox = (int)(tt % Tw);
-    const long long rq = tt / Tw;
-    const int oy = (int)(rq % Th), on = (int)(rq / Th);
-    float o[4][4][4];  // [channel][row][col]
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      float w[4][6];
-#pragma unroll
-      for (int xx = 0; xx < 6; ++xx) {
-        float m[6];
-#pragma unroll
-        for (int yy = 0; yy < 6; ++yy) m[yy] = acc[yy * 6 + xx][r];
-        float t4[4];
-        at4(m, t4);
-#pragma unroll
-        for (int a = 0; a < 4; ++a) w[a][xx] = t4[a];
-      }
-#pragma unroll
-      for (int a = 0; a < 4; ++a) at4(w[a], o[r][a]);
-    }
-    const float4 bias = e.bias ? ld4(e.bias + col0) : make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 bsc = make_float4(0.f, 0.f, 0.f, 0.f), bsh = bsc, bmu = bsc, bis = bsc;
-    if (bwd_mask) { bsc = ld4(e.bn_scale + col0); bsh = ld4(e.bn_shift + col0); bmu = ld4(e.bn_mean + col0); bis = ld4(e.bn_invstd + col0); }
-    const float bsv[4] = {bias.x, bias.y, bias.z, bias.w};
-    const float scv[4] = {bsc.x, bsc.y, bsc.z, bsc.w}, shv[4] = {bsh.x, bsh.y, bsh.z, bsh.w};
-    const float muv[4] = {bmu.x, bmu.y, bmu.z, bmu.w}, isv[4] = {bis.x, bis.y, bis.z, bis.w};
-    // The dgrad's mask operand y (16 B per pixel and lane) comes in by LDS-DMA,
-    // 8 pixels at a time into this wave's 8 KB of the (now idle) LDS, one wait
-    // per 8: register loads here made the compiler chain load -> wait -> store
-    // per pixel (the in-order vmcnt counts the stores), with nothing else on the
-    // CU to hide it (round 4: ~0.9 ms of the fp32 step, UNET_WF64_ABL=8).
-    const unsigned long long ybase = uniform_u64(e.yref);  // kernel argument: SGPRs (unused unless bwd_mask)
-    const unsigned ylds = (unsigned)(size_t)(lds_u8_t*)lds + (unsigned)wave * 8192u;
-#pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      if (bwd_mask) {
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          const int y = min(4 * oy + 2 * h + (q >> 2), g.Hg - 1), x = min(4 * ox + (q & 3), g.Wg - 1);
-          dma_sv((((unsigned)(on * g.Hg + y) * g.Wg + x) * dC + dcol) * 4u, ybase, ylds + q * 1024u);
-        }
-      }
-      // vmcnt(0) as a builtin, not asm: it retires the DMAs and, visibly to the
-      // compiler's wait-count tracking, the coefficient loads above, so no
-      // per-pixel branch join leaves them pending (it then re-waited, stores
-      // included, before every pixel)
-      __builtin_amdgcn_s_waitcnt(0x0F70);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const int a = 2 * h + (q >> 2), bb = q & 3;
-        const int y = 4 * oy + a, x = 4 * ox + bb;
-        if (y >= g.Hg || x >= g.Wg) continue;
-        const float4 yq = bwd_mask ? *reinterpret_cast<const float4*>(lds + wave * 2048 + q * 256 + lane * 4)
-                                   : make_float4(0.f, 0.f, 0.f, 0.f);
-        const float yv[4] = {yq.x, yq.y, yq.z, yq.w};
-        float v[4];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = wf_epi(o[r][a][bb] + bsv[r], yv[r], scv[r], shv[r], muv[r], isv[r],
-                                                   bwd_mask, e.relu, s1[r], s2[r]);
-        st4(dptr + ((size_t)(on * g.Hg + y) * g.Wg + x) * dC + dcol, make_float4(v[0], v[1], v[2], v[3]));
-      }
-    }
-  }
-  const bool want = e.stats || e.yref || e.colsum1;
-  if (!want) return;
-  // the 16 lanes of a quarter hold the same 4 channels (other tiles)
-#pragma unroll
-  for (int r = 0; r < 4; ++r)
-#pragma unroll
-    for (int o2 = 1; o2 < 16; o2 <<= 1) {
-      s1[r] += __shfl_xor(s1[r], o2);
-      s2[r] += __shfl_xor(s2[r], o2);
-    }
-  if (mi == 0) {
-    const int grp = blockIdx.x % kStatGroups;
-    const int nsplit = e.n_split < N ? e.n_split : N;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int col = col0 + r;
-      if (col < nsplit) {
-        double* st = e.yref ? e.bstats : e.stats;
-        if (st) {
-          atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 0, (double)s1[r]);
-          atomicAdd(st + ((size_t)grp * nsplit + col) * 2 + 1, (double)s2[r]);
-        }
-      } else if (e.colsum1) {
-        atomicAdd(e.colsum1 + (size_t)grp * (N - nsplit) + (col - nsplit), (double)s1[r]);
-      }
-    }
-  }
+  wf64_output(acc, g, e, N, T, Th, Tw, t0, n0, th, cb, mi, mq, lane, wave, lds);
 }
 
 bool wino_fused64_applies(const IgemmArgs& a) {
@@ -1529,7 +1539,7 @@ hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s) {
   switch (abl) {
 #define WF64(A) \
   case A: hipLaunchKernelGGL(k_wino4f64<A>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e); break;
-    WF64(1) WF64(2) WF64(4) WF64(8) WF64(6) WF64(3)
+    WF64(1) WF64(2) WF64(4) WF64(8) WF64(6) WF64(3) WF64(16) WF64(20) WF64(18) WF64(7) WF64(15)
 #undef WF64
     default: hipLaunchKernelGGL(k_wino4f64<0>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
   }
@@ -1537,6 +1547,237 @@ hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s) {
 }
 
 
+
+// ---------------------------------------------------------------------------
+// k_wino4f64p: tile 76 = tile 73's arithmetic (the same operands, the same
+// per-point accumulation order: bit-identical outputs) on a software-pipelined
+// chunk loop.  Round-5 ablations of tile 73 (fp32 bench, 12 launch sites,
+// profiles/r05_wino4f64_ablation.txt): without its MFMAs the two GEMM classes
+// lose 2.18 ms, without the patch loads 0.67 ms, without the transform
+// arithmetic 0.12 ms, without all of those and the output stage 4.07 of the
+// kernel's ~5.7 ms.  Tile 73 fills its LDS between two barriers while no MFMA
+// runs: V (74 KB per chunk from L2) is DMA'd during the transform, the patch
+// loads are retired by a full vmcnt, so the L2 -> LDS transfer of every chunk
+// is serialised with its MFMAs.  Here every global -> LDS transfer is an
+// LDS-DMA retired by counted vmcnt waits (no compiler-tracked load in the loop):
+//   * the 18 patch values of a thread land in a per-wave raw area (dword DMA,
+//     lane-contiguous rows) one chunk ahead; the BatchNorm scale / shift of
+//     every input channel sits in an LDS table;
+//   * V is split into half A (points 0-15, 32 KB) and half B (points 16-35,
+//     40 KB), each refilled for the next chunk as soon as the MFMAs of its
+//     points are done: 4 + 5 pieces of 1 KB per wave and chunk;
+//   * per chunk: commit (raw -> BN+ReLU -> B^T d B -> U), barrier, MFMAs of
+//     points 0-15, barrier, V(next) half A, MFMAs of points 16-35, barrier,
+//     V(next) half B.
+// Per wave and chunk the DMAs are issued in the order raw(k+1) [18], VA(k+1)
+// [4], VB(k+1) [5], so the waits are constant: raw(k) before the commit
+// (vmcnt 9), VA(k) before the first barrier (23), VB(k) before the second (18).
+// The last chunk re-issues its own transfers (same counts; never read).
+// LDS: U 38 KB + V 72 KB + raw 36 KB + BN table 8 KB = 153 KB, one workgroup
+// per CU as tile 73.
+// ---------------------------------------------------------------------------
+constexpr int kWf64pMaxCg = 1024;
+
+__global__ __launch_bounds__(512, 1) void k_wino4f64p(Gather g, const float* __restrict__ V, int N, long long T,
+                                                      int Th, int Tw, int NB, Epilogue e) {
+  constexpr int PU = 32 * 8 + 8, PV = 64 * 8;
+  constexpr int PA = 16;  // points of V half A
+  constexpr int U_F = 36 * PU, VA_F = PA * PV, VB_F = (36 - PA) * PV, RAW_F = 8 * 18 * 64;
+  __shared__ __attribute__((aligned(16))) float lds[U_F + VA_F + VB_F + RAW_F + 2 * kWf64pMaxCg];
+  float* Us = lds;
+  float* VAs = lds + U_F;
+  float* VBs = VAs + VA_F;
+  float* raws = VBs + VB_F;
+  float* ss = raws + RAW_F;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  long long bid = blockIdx.x;
+  const long long G = gridDim.x;
+  if ((G & 7) == 0) bid = (bid & 7) * (G >> 3) + (bid >> 3);  // an XCD's workgroups share tiles
+  const int nb = (int)(bid % NB);
+  const long long t0 = (bid / NB) * 32;
+  const int n0 = nb * 64;
+  const int Cg = g.Cg, nk = Cg >> 3;
+
+  // ---- loader role: patch (tile lt, channel lc), column half hf (tile 73) ----
+  const int hf = (lane >> 4) & 1;
+  const int pt = wave * 32 + (lane & 15) + ((lane >> 5) << 4);
+  const int lt = pt >> 3, lc = pt & 7;
+  const long long t = t0 + lt;
+  int img = 0, ty = 0, tx = 0;
+  if (t < T) {
+    tx = (int)(t % Tw);
+    const long long r = t / Tw;
+    ty = (int)(r % Th);
+    img = (int)(r / Th);
+  }
+  const int vrows = t < T ? min(6, g.Hg + 2 - 4 * ty) : 0;
+  const int vcols = t < T ? min(6, g.Wg + 2 - 4 * tx) : 0;
+  const bool wfull = __all(vrows == 6 && vcols == 6);
+  float* const ubase = Us + (3 * hf) * 6 * PU + lt * 8 + wf8_slot(lt, lc & 3) + (lc >> 2);
+
+  // the consumer BatchNorm+ReLU table (scale | shift) of the concatenated channels
+  const bool tf0 = g.s[0].scale != nullptr, tf1 = g.c_split < Cg && g.s[1].scale != nullptr;
+  if (tf0 || tf1) {
+    for (int c = tid; c < Cg; c += 512) {
+      const bool sec = c >= g.c_split;
+      const float* scp = sec ? g.s[1].scale : g.s[0].scale;
+      const float* shp = sec ? g.s[1].shift : g.s[0].shift;
+      const int cl = sec ? c - g.c_split : c;
+      ss[c] = scp ? scp[cl] : 1.f;
+      ss[kWf64pMaxCg + c] = scp ? shp[cl] : 0.f;
+    }
+  }
+
+  const unsigned raw_lds = (unsigned)(size_t)(lds_u8_t*)raws + (unsigned)wave * (18u * 256u);
+  auto issue_raw = [&](int kc) {  // 18 dword DMAs: raw[yy][xx] -> raw area row yy * 3 + xx
+    const bool second = kc * 8 >= g.c_split;  // c_split % 8 == 0: uniform source
+    const unsigned long long sb = uniform_u64(second ? g.s[1].ptr : g.s[0].ptr);
+    const int sH = second ? g.s[1].H : g.s[0].H, sW = second ? g.s[1].W : g.s[0].W;
+    const int sC = second ? g.s[1].C : g.s[0].C;
+    const int soy = second ? g.s[1].oy : g.s[0].oy, sox = second ? g.s[1].ox : g.s[0].ox;
+    const int cl = kc * 8 - (second ? g.c_split : 0) + lc;
+    const unsigned o0 = ((unsigned)((img * sH + 4 * ty + soy) * sW + 4 * tx + sox) * sC + cl) * 4u;
+    const unsigned rs = (unsigned)sW * sC * 4u, cs = (unsigned)sC * 4u;
+    if (wfull) {
+      const unsigned oh = o0 + 3u * hf * cs;
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 3; ++xx) dma4_sv(oh + (yy * rs + xx * cs), sb, raw_lds + (yy * 3 + xx) * 256u);
+    } else {  // clamp to the last in-window row / column (zeroed in commit)
+      const unsigned lr = (unsigned)max(vrows - 1, 0), lcn = (unsigned)max(vcols - 1, 0);
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy)
+#pragma unroll
+        for (int xx = 0; xx < 3; ++xx)
+          dma4_sv(o0 + (min((unsigned)yy, lr) * rs + min((unsigned)(3 * hf + xx), lcn) * cs), sb,
+                  raw_lds + (yy * 3 + xx) * 256u);
+    }
+  };
+  // V (k_wino4f_w8 layout [Cg/8][36][N][8]: 2 KB per point for 64 columns):
+  // half A = points 0-15 as 32 pieces of 1 KB, 4 per wave; half B = points
+  // 16-35, 40 pieces, 5 per wave
+  const unsigned long long vbase = uniform_u64(V);
+  const unsigned va_lds = (unsigned)(size_t)(lds_u8_t*)VAs, vb_lds = (unsigned)(size_t)(lds_u8_t*)VBs;
+  auto issue_v = [&](int kc, int half) {
+    const int np = half ? 5 : 4, p0 = half ? PA : 0;
+    const unsigned dst = half ? vb_lds : va_lds;
+#pragma unroll
+    for (int j = 0; j < 5; ++j) {
+      if (j < np) {
+        const int pc = wave + 8 * j;  // piece: point p0 + (pc >> 1), 1-KB half pc & 1
+        dma_sv((unsigned)((((size_t)kc * 36 + p0 + (pc >> 1)) * N + n0) * 32) + (unsigned)((pc & 1) * 1024 + lane * 16),
+               vbase, dst + (unsigned)((pc >> 1) * PV * 4 + (pc & 1) * 1024));
+      }
+    }
+  };
+  auto commit = [&](int kc) {
+    vm_wait<9>();  // raw(kc) landed (VA(kc), VB(kc) may still be in flight)
+    float raw[18];
+#pragma unroll
+    for (int q = 0; q < 18; ++q) raw[q] = raws[wave * (18 * 64) + q * 64 + lane];
+    lgkm_wait0();  // the raw area is read before its refill is issued
+    issue_raw(kc + 1 < nk ? kc + 1 : kc);
+    const bool second = kc * 8 >= g.c_split;
+    const bool tf = second ? tf1 : tf0;
+    if (tf) {
+      const float sc = ss[kc * 8 + lc], sh = ss[kWf64pMaxCg + kc * 8 + lc];
+#pragma unroll
+      for (int q = 0; q < 18; ++q) raw[q] = fmaxf(fmaf(raw[q], sc, sh), 0.f);
+    }
+    if (!wfull) {
+#pragma unroll
+      for (int q = 0; q < 18; ++q) raw[q] = (q / 3 < vrows && 3 * hf + q % 3 < vcols) ? raw[q] : 0.f;
+    }
+#pragma unroll
+    for (int xx = 0; xx < 3; ++xx) {  // columns in place: raw[a][xx] = (B^T d)[a][3 hf + xx]
+      float d[6];
+#pragma unroll
+      for (int yy = 0; yy < 6; ++yy) d[yy] = raw[yy * 3 + xx];
+      float rr[6];
+      bt6(d, rr);
+#pragma unroll
+      for (int a = 0; a < 6; ++a) raw[a * 3 + xx] = rr[a];
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+      const auto sw = __builtin_amdgcn_permlane16_swap(__float_as_uint(raw[k]), __float_as_uint(raw[9 + k]),
+                                                       false, false);
+      raw[k] = __uint_as_float(sw[0]);
+      raw[9 + k] = __uint_as_float(sw[1]);
+    }
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+      const float d[6] = {raw[a * 3 + 0], raw[a * 3 + 1], raw[a * 3 + 2],
+                          raw[9 + a * 3 + 0], raw[9 + a * 3 + 1], raw[9 + a * 3 + 2]};
+      float rr[6];
+      bt6(d, rr);
+#pragma unroll
+      for (int bb = 0; bb < 6; ++bb) ubase[(a * 6 + bb) * PU] = rr[bb];
+    }
+  };
+
+  // ---- MFMA role: wave = (tile half th, 16-channel block cb), all 36 points (tile 73) ----
+  const int th = wave & 1, cb = wave >> 1;
+  const int mi = lane & 15, mq = lane >> 4;
+  const int aoff = (16 * th + mi) * 8 + wf8_slot(16 * th + mi, mq);
+  const int boff = (16 * cb + mi) * 8 + wf8_slot(mi, mq);
+  floatx4 acc[36];
+#pragma unroll
+  for (int p = 0; p < 36; ++p) acc[p] = (floatx4){0.f, 0.f, 0.f, 0.f};
+
+  __syncthreads();  // BN table
+  issue_raw(0);
+  issue_v(0, 0);
+  issue_v(0, 1);
+  for (int kc = 0; kc < nk; ++kc) {
+    const int kn = kc + 1 < nk ? kc + 1 : kc;
+    commit(kc);
+    vm_wait<23>();  // VA(kc) landed (VB(kc) and raw(kc + 1) may be in flight)
+    lgkm_wait0();   // U stores
+    raw_barrier();
+#pragma unroll
+    for (int p = 0; p < PA; ++p) {
+      const float2 a = *reinterpret_cast<const float2*>(Us + p * PU + aoff);
+      const float2 b = *reinterpret_cast<const float2*>(VAs + p * PV + boff);
+      acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.x, a.x, acc[p], 0, 0, 0);
+      acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.y, a.y, acc[p], 0, 0, 0);
+    }
+    vm_wait<18>();  // VB(kc) landed (raw(kc + 1) may be in flight)
+    lgkm_wait0();
+    raw_barrier();  // every wave is past its half-A reads
+    issue_v(kn, 0);
+#pragma unroll
+    for (int p = PA; p < 36; ++p) {
+      const float2 a = *reinterpret_cast<const float2*>(Us + p * PU + aoff);
+      const float2 b = *reinterpret_cast<const float2*>(VBs + (p - PA) * PV + boff);
+      acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.x, a.x, acc[p], 0, 0, 0);
+      acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.y, a.y, acc[p], 0, 0, 0);
+    }
+    lgkm_wait0();
+    raw_barrier();  // every wave is past its U and half-B reads
+    issue_v(kn, 1);
+  }
+  vm_wait<0>();  // the last chunk's re-issued transfers, before the output stage reuses the LDS
+  __syncthreads();
+  wf64_output(acc, g, e, N, T, Th, Tw, t0, n0, th, cb, mi, mq, lane, wave, lds);
+}
+
+bool wino_fused64p_applies(const IgemmArgs& a) { return wino_fused64_applies(a) && a.a.Cg <= kWf64pMaxCg; }
+
+hipError_t launch_wino_fused64p(const IgemmArgs& a, hipStream_t s) {
+  if (!wino_fused64p_applies(a)) return hipErrorInvalidValue;
+  const Gather& g = a.a;
+  const int Th = (g.Hg + 3) / 4, Tw = (g.Wg + 3) / 4;
+  const long long T = (long long)g.nimg * Th * Tw;
+  float* V = reinterpret_cast<float*>(a.wino_ws);
+  const long long nw = (long long)a.N * g.Cg;
+  const int NB = a.N / 64;
+  const long long G = (T + 31) / 32 * NB;
+  hipLaunchKernelGGL(k_wino4f_w8, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
+  hipLaunchKernelGGL(k_wino4f64p, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  return hipGetLastError();
+}
 
 // ---------------------------------------------------------------------------
 // k_wino2f64: fused Winograd F(2x2, 3x3), 64 output channels x 64 tiles per
