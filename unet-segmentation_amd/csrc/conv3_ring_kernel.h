@@ -390,8 +390,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
         red = reinterpret_cast<float*>(lds + NW * 4096);
       }
     }
-    igemm_finish<TH * 32, BN, WM, WN, NT>(args, acc, 0, n0, wm, wn, tid, red, HaloRows<32, TH>{n, y0, x0, Hg, Wg},
-                                          stage);
+    igemm_finish<TH * 32, BN, WM, WN, NT, HaloRows<32, TH>, 1>(args, acc, 0, n0, wm, wn, tid, red,
+                                                                HaloRows<32, TH>{n, y0, x0, Hg, Wg}, stage);
     if (!PT || !wrap) return;
 #pragma unroll
     for (int i = 0; i < TM; ++i)

@@ -458,7 +458,9 @@ __device__ __forceinline__ void epi_shuffle(const Epilogue& e, const floatx16 (&
 // LDS that no wave reads or writes any more (a barrier precedes its use).
 // `stage` (optional): NT / 64 x 4 KB of LDS, disjoint from `red`, that no wave
 // reads or writes any more -- enables epi_lds for bf16 destinations at TN = 2.
-template <int BM, int BN, int WM, int WN, int NT, class RowMap = LinearRows>
+// KSTAGE2: also stage the input gradient's masked form (KIND 2; callers with the
+// register budget for it -- k_conv3_bf's 128 VGPRs spilled).
+template <int BM, int BN, int WM, int WN, int NT, class RowMap = LinearRows, int KSTAGE2 = 0>
 __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&acc)[BM / (WM * 32)][BN / (WN * 32)],
                                              int m0, int n0, int wm, int wn, int tid, float* red,
                                              RowMap rows = RowMap{0, 0}, unsigned short* stage = nullptr) {
@@ -519,15 +521,18 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
       if constexpr (TN == 2) {
         // LDS-staged path: bf16 destination (and bf16 mask operand), one destination,
         // 16-B aligned rows, 32-bit byte offsets for the mask DMA
-        // (the input gradient's mask form, KIND 2, measured slower through LDS:
-        // its staging spilled at the 128-VGPR budget of k_conv3_bf; it keeps epi_fast)
-        if (stage && h16 && !two && kind != 2 && e.d[0].C % 8 == 0 &&
+        // (the input gradient's mask form, KIND 2, only with KSTAGE2: in
+        // k_conv3_bf its staging spilled at the 128-VGPR budget and ran slower)
+        if (stage && h16 && !two && (kind != 2 || (KSTAGE2 && yh16)) && e.d[0].C % 8 == 0 &&
             ((reinterpret_cast<size_t>(e.d[0].ptr) | (kind == 2 ? reinterpret_cast<size_t>(e.yref) : 0)) & 15) == 0 &&
             (size_t)args.M * e.d[0].C * 2 < (1ull << 32)) {
           unsigned short* wl = stage + (tid >> 6) * (32 * 64);
           switch (kind) {
             case 0: epi_lds<TM, TN, 0>(e, acc, rows, n0, wm, wn, h, li, lane, s1, s2, wl); break;
             case 1: epi_lds<TM, TN, 1>(e, acc, rows, n0, wm, wn, h, li, lane, s1, s2, wl); break;
+            case 2:
+              if constexpr (KSTAGE2) epi_lds<TM, TN, 2>(e, acc, rows, n0, wm, wn, h, li, lane, s1, s2, wl);
+              break;
             default: epi_lds<TM, TN, 3>(e, acc, rows, n0, wm, wn, h, li, lane, s1, s2, wl); break;
           }
           igemm_finish_stats<BN, WM, WN, NT>(e, s1, s2, t1, n0, wn, N, tid, red);
