@@ -9,7 +9,7 @@ set -o pipefail
 out=$1; shift
 export TMPDIR=/tmp
 mkdir -p "$out"
-B="bench.py --no-cpu-baseline --no-iou --no-extras --extra-dtypes= --steps 2 --warmup 1"
+B="bench.py --no-cpu-baseline --no-iou --no-extras --no-peaks --extra-dtypes= --steps 2 --warmup 1"
 run() { echo "== $1"; n=$1; shift; timeout -k 10 240 "$@" > "$out/$n.log" 2>&1 || { echo "failed rc=$?"; tail -5 "$out/$n.log"; exit 1; }; }
 run trace rocprofv3 --kernel-trace --stats -f csv -d "$out/trace" -o run -- python3 $B "$@"
 run pmc1 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES SQ_WAIT_ANY SQ_WAVE_CYCLES -f csv -d "$out/pmc1" -o run -- python3 $B "$@"
