@@ -166,6 +166,11 @@ struct fast_rows<LinearRows> : std::true_type {};
 template <int TH>
 struct fast_rows<HaloRows<32, TH>> : std::true_type {};
 
+// Row permutation inside blocks of 8 (q -> 0, 4, 1, 5, 2, 6, 3, 7): staging
+// loops whose 8-lane ds_write_b128 groups cover two 4-piece rows then pair rows
+// 4 apart -- conflict-free for 80-B rows under the stores' mod-32 banking.
+__device__ __forceinline__ int stage_row8(int q) { return (q & ~7) | ((q & 1) << 2) | ((q >> 1) & 3); }
+
 // Column statistics of an epilogue (BN sums, BN-backward sums, concat column
 // sums): wave halves, then waves of a column block through LDS, then one fp64
 // atomic per column per workgroup into a spread group.

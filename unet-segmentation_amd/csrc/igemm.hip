@@ -63,7 +63,11 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   const int m0 = zb * args.batch_rows + blockIdx.x * BM, n0 = blockIdx.y * BN;
   const Gather& g = args.a;
   const int M = args.batch > 1 ? (zb + 1) * args.batch_rows : args.M, K = args.K;
-  const int col4 = tid % C4, row0 = tid / C4;
+  // staging row of this thread.  With BK = 16 a row is 4 x 16 B and the 8 lanes
+  // of a ds_write_b128 group store two rows; rows r and r + 1 (80-B stride) share
+  // 2 of the 32 bank quads (mod-32 banking of stores), r and r + 4 share none:
+  // pair rows 4 apart within each block of 8 (the fragment reads are unchanged)
+  const int col4 = tid % C4, row0 = C4 == 4 ? stage_row8(tid / C4) : tid / C4;
 
   // Per staged A row: pixel base in each source grid (before the tap offset).
   int rb0[AV], rb1[AV];

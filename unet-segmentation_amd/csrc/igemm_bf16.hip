@@ -382,10 +382,16 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
   // staging units: A = (halo pixel, 8-channel piece), B = (tap, row, 8-k piece)
   int pi0[NA], pi1[NA];
   int bsrc[NB];  // element offsets into args.bh (32-bit: one VGPR, scalar base)
+  // staging rows pair 4 apart in each block of 8 (stage_row8: conflict-free
+  // ds_write_b128 groups at 80-B rows); the halo's last partial block as is
+  auto arow = [&](int u) {
+    const int q = u >> 2;
+    return (q | 7) < PH ? stage_row8(q) : q;
+  };
 #pragma unroll
   for (int k = 0; k < NA; ++k) {
     const int u = min(tid + k * NT, UA - 1);
-    const int ph = u >> 2;
+    const int ph = arow(u);
     const int hy = ph / HW2, hx = ph - (ph / HW2) * HW2;
     const int yy = min(y0 + hy, Hg + 1), xx = min(x0 + hx, Wg + 1);  // overhang: any in-range pixel
     pi0[k] = (n * g.s[0].H + yy + g.s[0].oy) * g.s[0].W + xx + g.s[0].ox;
@@ -394,7 +400,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
 #pragma unroll
   for (int k = 0; k < NB; ++k) {
     const int u = min(tid + k * NT, UB - 1);
-    const int r = (u >> 2) % BN, tap = (u >> 2) / BN;
+    const int br = stage_row8(u >> 2);  // 9 x BN rows: whole blocks of 8
+    const int r = br % BN, tap = br / BN;
     bsrc[k] = (n0 + r) * K + tap * Cg + (u & 3) * 8;
   }
 
@@ -447,7 +454,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     for (int k = 0; k < NA; ++k) {
       const int u = tid + k * NT;
       if (u < UA) {
-        unsigned short* d = As + (u >> 2) * LDR + (u & 3) * 8;
+        unsigned short* d = As + arow(u) * LDR + (u & 3) * 8;
         const float4 r1 = ra1[A16 ? 0 : k];
         if constexpr (SPLIT) {
           uint4 lo;
@@ -462,7 +469,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_bf(const IgemmArgs
     for (int k = 0; k < NB; ++k) {
       const int u = tid + k * NT;
       if (u < UB) {
-        unsigned short* d = Bs + (u >> 2) * LDR + (u & 3) * 8;
+        unsigned short* d = Bs + stage_row8(u >> 2) * LDR + (u & 3) * 8;
         *reinterpret_cast<u32x4*>(d) = rb[k];
         if constexpr (SPLIT) *reinterpret_cast<u32x4*>(d + PLANE) = rbl[k];
       }
