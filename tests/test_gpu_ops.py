@@ -169,6 +169,39 @@ def test_wino4f64_pipelined_bitexact(lib, n, h, w, ci, co, tf):
           + (f", dgrad {rel_err(outs[76][1], outs[73][1]):.1e}" if dg else ""))
 
 
+@pytest.mark.parametrize("n,h,w,ci,co,tf", [(2, 14, 13, 64, 64, False), (2, 11, 17, 64, 128, True),
+                                              (1, 30, 29, 128, 64, True), (3, 7, 9, 16, 64, False)])
+def test_wino2_32col_vs_64col(lib, n, h, w, ci, co, tf):
+    """Tile 77 (fused F(2x2) over 32 output columns, two workgroups per CU)
+    against tile 75 (64 columns): same operands and per-point accumulation
+    order, so within 8 fp32 ulps of the output scale (separately compiled
+    FMA contraction), both at the oracle; forward with / without the
+    producer's BN+ReLU, input gradient."""
+    rng = np.random.default_rng(9)
+    x = rng.standard_normal((n, h, w, ci))
+    wt = rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci)
+    b = rng.standard_normal(co)
+    sc = rng.uniform(-0.5, 1.5, ci) if tf else None
+    sh = rng.standard_normal(ci) * 0.3 if tf else None
+    dy = rng.standard_normal((n, h - 2, w - 2, co))
+    ref = O.conv_valid_fwd(np.maximum(x * sc + sh, 0) if tf else x, wt, b)
+    rdx, _, _ = O.conv_valid_bwd(x, wt, dy)
+    dg = ci % 64 == 0
+    outs = {}
+    for v in (75, 77):
+        lib.unet_set_tuning(b"igemm_variant", v)
+        try:
+            outs[v] = (_conv_fwd(lib, x, wt, b, sc, sh), _conv_dgrad(lib, dy, wt, h, w, ci) if dg else None)
+        finally:
+            lib.unet_set_tuning(b"igemm_variant", -1)
+    ulp8 = 8 * 2.0 ** -23
+    assert rel_err(outs[77][0], outs[75][0]) <= ulp8
+    assert rel_err(outs[77][0], ref) < 2e-5
+    if dg:
+        assert rel_err(outs[77][1], outs[75][1]) <= ulp8
+        assert rel_err(outs[77][1], rdx) < 2e-5
+
+
 @pytest.fixture
 def wvariant(request, lib):
     """Forced weight-gradient tile (-1 = built-in; 22 / 23 = the fp32 halo-tiled

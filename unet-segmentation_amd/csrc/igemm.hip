@@ -1124,7 +1124,7 @@ int g_wino4_fwd_min_cg = env_int("UNET_WINO4_FWD_MIN_CG", 128);
 // ... and also up to this many ("wino4_fwd_small_cg" / UNET_WINO4_FWD_SMALL_CG)
 int g_wino4_fwd_small_cg = env_int("UNET_WINO4_FWD_SMALL_CG", 0);
 static int wino_tile_m(int tile) {
-  return tile == 70 || tile == 75 ? 2 : tile == 71 || tile == 72 || tile == 73 || tile == 76 ? 4 : tile == 74 ? 6 : 0;
+  return tile == 70 || tile == 75 || tile == 77 ? 2 : tile == 71 || tile == 72 || tile == 73 || tile == 76 ? 4 : tile == 74 ? 6 : 0;
 }
 
 // igemm tile table: id -> (BM, BN, waves M x N, BK), resident workgroups per CU
@@ -1194,6 +1194,7 @@ static TileInfo tile_info(int id) {
     case 72: return {32, 32, 16, 1};
     case 73: case 76: return {32, 64, 8, 1};
     case 75: return {64, 64, 8, 1};
+    case 77: return {64, 32, 8, 2};
     // fp32 halo-tiled 3x3 (k_conv3_f32): bk = one 16-channel chunk x 9 taps
     case 51: return {256, 64, 144, 2};
     case 52: return {256, 64, 144, 2};
@@ -1237,7 +1238,8 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   if (tile == 72) return wino_fused_applies(a);
   if (tile == 73) return wino_fused64_applies(a);
   if (tile == 76) return wino_fused64p_applies(a);
-  if (tile == 75) return wino_fused2_applies(a);
+  if (tile == 75) return wino_fused2_applies(a, 64);
+  if (tile == 77) return wino_fused2_applies(a, 32);
   if (is_dma_tile(tile)) {  // bf16-stored A sources, no split operands
     const int ch = tile_info(tile).bk / 9;
     const bool two = a.a.c_split < a.a.Cg;
@@ -1345,7 +1347,8 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 72: return launch_wino_fused(a, s);
     case 73: return launch_wino_fused64(a, s);
     case 76: return launch_wino_fused64p(a, s);
-    case 75: return launch_wino_fused2(a, s);
+    case 75: return launch_wino_fused2(a, s, 64);
+    case 77: return launch_wino_fused2(a, s, 32);
     case 51: return go_halo32<8, 32, 64, 8, 1, 4>(a, s);
     case 52: return go_halo32<16, 16, 64, 8, 1, 4>(a, s);
     case 53: return go_halo32<8, 32, 64, 4, 1, 2>(a, s);
@@ -1401,7 +1404,7 @@ hipError_t launch_igemm_v(const IgemmArgs& a0, hipStream_t s, GemmChoice c) {
   if (!igemm_args_ok(a0) || !igemm_tile_fits(a0, c.tile)) return hipErrorInvalidValue;
   IgemmArgs a = a0;
   const int nk = a.K / tile_info(c.tile).bk;
-  const bool wino = c.tile >= 70 && c.tile <= 76;
+  const bool wino = c.tile >= 70 && c.tile <= 77;
   if ((c.tile == 70 || c.tile == 71 || c.tile == 74) && c.split >= 100) a.wino_choice.tile = c.split - 100;  // point GEMMs
   int ks = c.split < 1 || wino ? 1 : (c.split > nk ? nk : c.split);
   if (ks > 1) {  // no empty slice: ks = ceil(nk / ceil(nk / ks))
@@ -1534,9 +1537,9 @@ hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad
 
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c) {
   int t = c.tile;
-  if (t < 0 && g_tune_igemm >= 70 && g_tune_igemm <= 76 && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;
-  if (t >= 70 && t <= 76) {
-    const int mt = t == 70 || t == 75 ? 2 : t == 74 ? 6 : 4;
+  if (t < 0 && g_tune_igemm >= 70 && g_tune_igemm <= 77 && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;
+  if (t >= 70 && t <= 77) {
+    const int mt = t == 70 || t == 75 || t == 77 ? 2 : t == 74 ? 6 : 4;
     const Gather& g = a.a;
     const double T = (double)g.nimg * ((g.Hg + mt - 1) / mt) * ((g.Wg + mt - 1) / mt);
     return 2.0 * (mt + 2) * (mt + 2) * T * g.Cg * a.N;

@@ -343,7 +343,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
                 36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 81, 82, 83, 84, 70, 71, 72, 73,
-                74, 75, 76, 88, 91, 92, 93, 94, 95, 96, 97, 98, 99}) {  // fits() filters by precision and gather
+                74, 75, 76, 77, 88, 91, 92, 93, 94, 95, 96, 97, 98, 99}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t) || tune_skipped(t)) continue;
     v.push_back({t, 1});
     if (t == 70 || t == 71 || t == 74)  // Winograd: no K split; the tile of its batched point GEMMs

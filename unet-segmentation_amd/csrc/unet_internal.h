@@ -160,8 +160,9 @@ hipError_t launch_wino_fused(const IgemmArgs& a, hipStream_t s);
 hipError_t launch_wino_fused64(const IgemmArgs& a, hipStream_t s);
 bool wino_fused64p_applies(const IgemmArgs& a);  // tile 76: tile 73 on a software-pipelined chunk loop
 hipError_t launch_wino_fused64p(const IgemmArgs& a, hipStream_t s);
-bool wino_fused2_applies(const IgemmArgs& a);  // tile 75: fused F(2x2, 3x3), 64 output channels x 64 tiles
-hipError_t launch_wino_fused2(const IgemmArgs& a, hipStream_t s);
+// tiles 75 / 77: fused F(2x2, 3x3), nc = 64 / 32 output channels x 64 tiles per workgroup
+bool wino_fused2_applies(const IgemmArgs& a, int nc);
+hipError_t launch_wino_fused2(const IgemmArgs& a, hipStream_t s, int nc);
 // MFMA flops a GEMM launch executes with variant c (Winograd: 2 * points *
 // tiles * Cg * N; otherwise the direct 2 * M * N * K)
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c);

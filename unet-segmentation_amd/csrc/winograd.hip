@@ -1824,11 +1824,19 @@ __global__ void k_wino2f_w8(const float* __restrict__ b, int N, int Cg, float* _
   }
 }
 
-__global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __restrict__ V, int N, long long T,
-                                                     int Th, int Tw, int NB, Epilogue e) {
+// NC: output columns per workgroup.  64 (tile 75): one workgroup per CU (128
+// accumulator VGPRs per lane).  32 (tile 77, round 5): half the accumulators
+// and V, two workgroups per CU, so one workgroup's loads, transforms and
+// epilogue overlap the other's MFMAs (tile 75 waits 45 % of its wave cycles,
+// profiles/r05_pmc_summary_fp32.txt); the input transform is then done per
+// 32 output columns -- cheap in F(2x2) (24 adds per patch).
+template <int NC>
+__global__ __launch_bounds__(512, NC == 32 ? 2 : 1) void k_wino2f64(Gather g, const float* __restrict__ V, int N,
+                                                                   long long T, int Th, int Tw, int NB, Epilogue e) {
   constexpr int TT = 64;      // tiles per workgroup
   constexpr int PU = TT * 8;  // U point plane
-  constexpr int PV = 64 * 8;  // V point plane
+  constexpr int PV = NC * 8;  // V point plane
+  constexpr int NJ = NC / 32;  // 16-column blocks per wave
   __shared__ __attribute__((aligned(16))) float lds[16 * PU + 16 * PV];
   float* Us = lds;
   float* Vs = lds + 16 * PU;
@@ -1838,7 +1846,7 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
   if ((G & 7) == 0) bid = (bid & 7) * (G >> 3) + (bid >> 3);  // an XCD's workgroups share tiles
   const int nb = (int)(bid % NB);
   const long long t0 = (bid / NB) * TT;
-  const int n0 = nb * 64;
+  const int n0 = nb * NC;
 
   // ---- loader role: patch (tile lt, channel lc) ----
   const int lt = tid >> 3, lc = tid & 7;
@@ -1858,8 +1866,8 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
   float raw[16];
   float sc = 1.f, sh = 0.f;  // the chunk's producer BN+ReLU (loaded with raw)
   const int nk = g.Cg >> 3;
-  // V (16 points x 2 KB per chunk) by LDS-DMA during the input transform,
-  // 4 x 1 KB per wave (as k_wino4f64)
+  // V (16 points x NC / 32 KB per chunk) by LDS-DMA during the input transform,
+  // 4 (NC 64) or 2 (NC 32) x 1 KB per wave (as k_wino4f64)
   const unsigned long long vbase = uniform_u64(V);
   const unsigned vlds = (unsigned)(size_t)(lds_u8_t*)lds + (unsigned)(16 * PU * 4);
   auto load = [&](int kc) {
@@ -1898,10 +1906,10 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
     const float* scp = second ? g.s[1].scale : g.s[0].scale;
     __builtin_amdgcn_s_waitcnt(0x0F70);  // raw(kc), sc, sh: retired visibly before the DMAs queue
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int pc = wave + 8 * j;  // 1-KB piece: point pc >> 1, half pc & 1
-      dma_sv((unsigned)((((size_t)kc * 16 + (pc >> 1)) * N + n0) * 32) + (unsigned)((pc & 1) * 1024 + lane * 16),
-             vbase, vlds + (unsigned)((pc >> 1) * PV * 4 + (pc & 1) * 1024));
+    for (int j = 0; j < 2 * NJ; ++j) {
+      const int pc = wave + 8 * j;  // 1-KB piece: point pc / NJ, part pc % NJ
+      dma_sv((unsigned)((((size_t)kc * 16 + pc / NJ) * N + n0) * 32) + (unsigned)((pc % NJ) * 1024 + lane * 16),
+             vbase, vlds + (unsigned)((pc / NJ) * PV * 4 + (pc % NJ) * 1024));
     }
     if (scp) {
 #pragma unroll
@@ -1934,12 +1942,12 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
   const int th = wave & 3, ch = wave >> 2;
   const int mi = lane & 15, mq = lane >> 4;
   const int aoff = (16 * th + mi) * 8 + wf8_slot(16 * th + mi, mq);
-  const int boff = (32 * ch + mi) * 8 + wf8_slot(mi, mq);  // rows 32 ch + 16 j + mi and mi agree on bits 2-3
-  floatx4 acc[16][2];
+  const int boff = (16 * NJ * ch + mi) * 8 + wf8_slot(mi, mq);  // rows 16 (NJ ch + j) + mi and mi agree on bits 2-3
+  floatx4 acc[16][NJ];
 #pragma unroll
   for (int p = 0; p < 16; ++p)
 #pragma unroll
-    for (int j = 0; j < 2; ++j) acc[p][j] = (floatx4){0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[p][j] = (floatx4){0.f, 0.f, 0.f, 0.f};
   load(0);
   for (int kc = 0; kc < nk; ++kc) {
     commit(kc);
@@ -1949,7 +1957,7 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
     for (int p = 0; p < 16; ++p) {
       const float2 a = *reinterpret_cast<const float2*>(Us + p * PU + aoff);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
+      for (int j = 0; j < NJ; ++j) {
         const float2 b = *reinterpret_cast<const float2*>(Vs + p * PV + boff + 16 * j * 8);
         acc[p][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.x, a.x, acc[p][j], 0, 0, 0);
         acc[p][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(b.y, a.y, acc[p][j], 0, 0, 0);
@@ -1958,14 +1966,14 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
     __syncthreads();
   }
 
-  // ---- output: tile 16 th + mi, channels n0 + 32 ch + 16 j + 4 mq + (0..3) ----
+  // ---- output: tile 16 th + mi, channels n0 + 16 (NJ ch + j) + 4 mq + (0..3) ----
   const long long tt = t0 + 16 * th + mi;
   const bool want = e.stats || e.yref || e.colsum1;
   const int nsplit = e.n_split < N ? e.n_split : N;
   const int grp = blockIdx.x % kStatGroups;
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int col0 = n0 + 32 * ch + 16 * j + 4 * mq;
+  for (int j = 0; j < NJ; ++j) {
+    const int col0 = n0 + 16 * NJ * ch + 16 * j + 4 * mq;
     const bool second = col0 >= e.n_split;  // uniform per 16-channel block (n_split % 16 == 0)
     float* dptr = second ? e.d[1].ptr : e.d[0].ptr;
     const int dC = second ? e.d[1].C : e.d[0].C;
@@ -2056,11 +2064,11 @@ __global__ __launch_bounds__(512, 1) void k_wino2f64(Gather g, const float* __re
   }
 }
 
-bool wino_fused2_applies(const IgemmArgs& a) {
+bool wino_fused2_applies(const IgemmArgs& a, int nc) {
   const Gather& g = a.a;
   if (a.b == nullptr || a.bh != nullptr || a.batch != 1) return false;
   if (g.taps_h != 3 || g.taps_w != 3 || g.stride != 1 || a.K != 9 * g.Cg || g.Cg % 8 != 0 || g.c_split % 8 != 0 ||
-      a.N % 64 != 0 || (a.e.n_split < a.N && a.e.n_split % 16 != 0))
+      a.N % nc != 0 || (a.e.n_split < a.N && a.e.n_split % 16 != 0))
     return false;
   if (g.s[0].h16 || g.s[1].h16 || a.e.shuffle_co || a.e.d[0].h16 || a.e.d[1].h16 || a.e.yref_h16) return false;
   if (a.e.d[0].oy || a.e.d[0].ox || a.e.d[0].H != g.Hg || a.e.d[0].W != g.Wg) return false;
@@ -2068,21 +2076,24 @@ bool wino_fused2_applies(const IgemmArgs& a) {
   for (int k = 0; k < 2; ++k)  // 32-bit byte offsets into the sources
     if ((long long)g.nimg * g.s[k].H * g.s[k].W * g.s[k].C * 4 >= (1ll << 32)) return false;
   const long long T = (long long)g.nimg * ((g.Hg + 1) / 2) * ((g.Wg + 1) / 2);
-  if ((T + 63) / 64 * (a.N / 64) > 0x7fffffffLL) return false;
+  if ((T + 63) / 64 * (a.N / nc) > 0x7fffffffLL) return false;
   return a.wino_ws != nullptr && (size_t)16 * a.N * g.Cg * 4 <= a.wino_ws_bytes;
 }
 
-hipError_t launch_wino_fused2(const IgemmArgs& a, hipStream_t s) {
-  if (!wino_fused2_applies(a)) return hipErrorInvalidValue;
+hipError_t launch_wino_fused2(const IgemmArgs& a, hipStream_t s, int nc) {
+  if ((nc != 64 && nc != 32) || !wino_fused2_applies(a, nc)) return hipErrorInvalidValue;
   const Gather& g = a.a;
   const int Th = (g.Hg + 1) / 2, Tw = (g.Wg + 1) / 2;
   const long long T = (long long)g.nimg * Th * Tw;
   float* V = reinterpret_cast<float*>(a.wino_ws);
   const long long nw = (long long)a.N * g.Cg;
-  const int NB = a.N / 64;
+  const int NB = a.N / nc;
   const long long G = (T + 63) / 64 * NB;
   hipLaunchKernelGGL(k_wino2f_w8, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, a.b, a.N, g.Cg, V);
-  hipLaunchKernelGGL(k_wino2f64, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  if (nc == 64)
+    hipLaunchKernelGGL(k_wino2f64<64>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
+  else
+    hipLaunchKernelGGL(k_wino2f64<32>, dim3((unsigned)G), dim3(512), 0, s, g, (const float*)V, a.N, T, Th, Tw, NB, a.e);
   return hipGetLastError();
 }
 
