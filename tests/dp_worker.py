@@ -9,7 +9,9 @@ gloo (RCCL needs one GPU per rank; the all-reduce call pattern is the same).
     env: RANK, WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT;
          UNET_DP_TUNE_DB=<path>: replay that GEMM tuning database (the bench's);
          UNET_DP_BACKEND=nccl: RCCL (one GPU per rank: world 1 on the test box),
-         UNET_DP_FORCE=1: issue the collectives at world 1 too (Trainer force_collectives)
+         UNET_DP_FORCE=1: issue the collectives at world 1 too (Trainer force_collectives),
+         UNET_DP_STEP=1: whole Trainer.step() calls (with the per-step buffer broadcast),
+         UNET_DP_SYNC_BCAST=1: that broadcast synchronous ahead of every forward (not deferred)
 """
 import os
 import sys
@@ -60,8 +62,23 @@ def main():
     tr = Trainer(m, batch, size, size, lr=1e-4, momentum=0.99, process_group=dist.group.WORLD, overlap=overlap,
                  comm_dtype=comm, precision=precision, force_collectives=force)
     tr.defer_join = os.environ.get("UNET_DP_DEFER", "1") != "0"
+    tr.defer_buffer_bcast = os.environ.get("UNET_DP_SYNC_BCAST") != "1"
     x, t, w = (torch.from_numpy(a).cuda() for a in shard(rank, batch, size))
     res = {}
+    if os.environ.get("UNET_DP_STEP") == "1":
+        starts = []
+        tr.on_buffers_synced = lambda b: starts.append(b.double().cpu().numpy().copy())
+        for s in range(steps):
+            res[f"loss{s}"] = np.array(tr.step(x, t, w).item())
+            torch.cuda.synchronize()
+            res[f"buf{s}"] = tr.flat_buffers.flat.double().cpu().numpy().copy()
+        res["params"] = tr.flat.flat.cpu().numpy().copy()
+        for s, b in enumerate(starts):
+            res[f"start{s}"] = b  # the buffers each step's forward started from
+        np.savez(out, **res)
+        dist.barrier()
+        dist.destroy_process_group()
+        return
     for s in range(steps):
         res[f"w{s}"] = tr.flat.flat.cpu().numpy().copy()         # weights this step starts from
         loss = tr.forward_loss(x, t, w)

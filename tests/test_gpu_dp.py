@@ -259,3 +259,27 @@ def test_rccl_world1_trainer_matches_no_group(tmp_path, precision, comm):
     assert np.abs(p - want).max() <= 1e-6 * np.abs(want).max()
     print(f"RCCL world-1 {precision} / {comm} wire: {exact} of {n} gradient tensors bit-equal to the no-group "
           f"Trainer, worst rel-L2 / tol {worst:.2f}, loss {float(r['loss0']):.5f}")
+
+
+@pytest.mark.parametrize("mode", ["deferred", "sync"])
+def test_two_rank_buffer_broadcast_ddp_semantics(tmp_path, mode):
+    """Trainer.step's per-step BatchNorm buffer broadcast (DDP
+    broadcast_buffers=True).  Deferred (the default): rank 0's running
+    statistics as a forward left them are broadcast beside that step's backward
+    into a staging copy and applied at the next step's start, so no collective
+    runs ahead of the forward; sync (UNET_DP_SYNC_BCAST=1): the broadcast ahead
+    of every forward.  Two ranks, whole steps: every step's forward starts, on
+    both ranks, from exactly rank 0's buffers as the previous step left them
+    (bit-equal; step 0: rank 0's initial buffers), and the ranks' buffers
+    differ after every step (each rank's own batch updates them), as under
+    DDP."""
+    steps = 4
+    env = {"UNET_DP_STEP": "1"}
+    if mode == "sync":
+        env["UNET_DP_SYNC_BCAST"] = "1"
+    ranks = run_ranks(tmp_path, True, steps=steps, extra_env=env)
+    for s in range(steps):
+        np.testing.assert_array_equal(ranks[1][f"start{s}"], ranks[0][f"start{s}"])
+        if s:
+            np.testing.assert_array_equal(ranks[0][f"start{s}"], ranks[0][f"buf{s - 1}"])
+        assert not np.array_equal(ranks[0][f"buf{s}"], ranks[1][f"buf{s}"])

@@ -19,7 +19,7 @@ SGD(lr, momentum=0.99).step() -- with the same arithmetic as the drop-in
   (UNET_BWD_DEFER_JOIN), the bucket's collective is issued from a stream that
   waits for them, and the side stream is joined once, before the optimizer;
   gradients are summed in fp32 (``comm_dtype=torch.bfloat16`` halves the xGMI
-  bytes, opt-in); every step starts by broadcasting rank 0's BatchNorm running
+  bytes, opt-in); every step starts from rank 0's BatchNorm running
   statistics (one flat buffer), as DDP does.
 """
 from __future__ import annotations
@@ -126,6 +126,15 @@ class Trainer:
         self._graph_key = None
         self._eager_steps = 0
         self.graph_error = None
+        # deferred buffer broadcast (round 5): rank 0's running statistics as a
+        # forward left them are broadcast into a staging copy beside that step's
+        # backward and applied at the next step's start -- DDP's per-step
+        # broadcast without a collective ahead of every forward
+        self.defer_buffer_bcast = True  # False: the synchronous broadcast ahead of every forward
+        self.on_buffers_synced = None   # diagnostics / tests: called with the flat buffers once a step's broadcast landed
+        self._bcast_stage = None
+        self._bcast_work = None
+        self._bcast_version = None
         self.lib = _lib.load()
         buckets = [self.flat.range_for(*self.plan.segment_grads(s)) for s in range(N_SEGMENTS)]
         # gradient all-reduce dtype: fp32 (DDP semantics) unless the caller asks
@@ -212,9 +221,21 @@ class Trainer:
         if self._graph is not None and self._graph_key[1:] != (self.lr, self.mom):
             self._graph = None  # stale hyper-parameters: capture again after this eager step
             self._eager_steps = 1
-        if self.broadcast_buffers and self.flat_buffers.flat is not None:
-            torch.distributed.broadcast(self.flat_buffers.flat, 0, group=self.pg)
+        bufs = self.flat_buffers.flat if self.broadcast_buffers else None
+        if bufs is not None:
+            self._apply_buffer_broadcast(bufs)
+            if self.on_buffers_synced is not None:
+                self.on_buffers_synced(bufs)
         loss = self.forward_loss(x, targets, weights)
+        if bufs is not None and self.defer_buffer_bcast:
+            # the backward and SGD never touch the running statistics: rank 0's
+            # post-forward values (what DDP broadcasts at the next forward) travel
+            # beside them into the staging copy
+            if self._bcast_stage is None:
+                self._bcast_stage = torch.empty_like(bufs)
+            self._bcast_stage.copy_(bufs)
+            self._bcast_work = torch.distributed.broadcast(self._bcast_stage, 0, group=self.pg, async_op=True)
+            self._bcast_version = bufs._version
         self.backward_and_reduce(x)
         self.optimizer_step()
         self._eager_steps += 1
@@ -222,6 +243,19 @@ class Trainer:
                 not self.plan.timing_on):
             self._capture(x, targets, weights)
         return loss
+
+    def _apply_buffer_broadcast(self, bufs):
+        """DDP's start-of-step buffer broadcast: the staged copy of rank 0's
+        statistics from the previous step's forward, or -- first step, or the
+        buffers were rewritten through torch since (load_state_dict, ...) -- a
+        broadcast now."""
+        work, self._bcast_work = self._bcast_work, None
+        if work is not None:
+            work.wait()  # NCCL: the current stream waits; gloo: the host does
+            if bufs._version == self._bcast_version:
+                bufs.copy_(self._bcast_stage)
+                return
+        torch.distributed.broadcast(bufs, 0, group=self.pg)
 
     def check_targets(self):
         """Wait for every step issued so far and raise IndexError if any of them
@@ -263,6 +297,9 @@ class Trainer:
         at the start of every step unless ``broadcast_buffers=False``)."""
         if self.pg is None:
             return
+        if self._bcast_work is not None:  # a staged broadcast in flight: retire it, a fresh one follows
+            self._bcast_work.wait()
+            self._bcast_work = None
         if self.flat_buffers.flat is not None:
             torch.distributed.broadcast(self.flat_buffers.flat, src, group=self.pg)
         for name, t in self.model.named_buffers():
