@@ -334,7 +334,8 @@ def run_precision(args, dtype, device, pg, world, rank):
                               "backward segment finishes" if trainer.overlap else "one all_reduce after backward",
                 "dtype": str(trainer.comm_dtype).replace("torch.", ""),
                 "bytes_per_step": trainer.reducer.bytes_per_step,
-                "buffers": "rank 0's BatchNorm running statistics broadcast at each step start (one flat buffer)"}
+                "buffers": "rank 0's BatchNorm running statistics (one flat buffer) as each forward left them, "
+                           "broadcast beside that step's backward and applied at the next step's start"}
     del trainer, model, x, t, w
     torch.cuda.empty_cache()
 
