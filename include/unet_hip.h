@@ -304,7 +304,9 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  (-1 = off, 1 = 64x64 tile, 2..9 = workgroups per CU for the
  *                  pixel split; bf16 GEMMs: 10-14, 20-21 = forced bf16 tile;
  *                  22-23 fp32 halo tiles; 71 / 74 = Winograd F(4x4,3x3) /
- *                  F(6x6,3x3) weight gradient, plan GEMMs only);
+ *                  F(6x6,3x3) weight gradient, plan GEMMs only; 1071 / 1074
+ *                  the same in slab mode; 100-104 = fp32 pixel-column tile
+ *                  0-4 in slab mode; 110-114 / 126-133 bf16 slab modes);
  *  "wino_max"      largest fp32 Winograd output tile the autotuner may pick
  *                  for forward / input-gradient GEMMs (env UNET_WINO_MAX): 6 =
  *                  F(6x6) and below, 4 (default) = F(4x4) / F(2x2), 2 = F(2x2)
@@ -342,6 +344,10 @@ int unet_set_tuning(const char* key, int value);
 size_t unet_tuning_report(char* buf, size_t len);
 /* Forget every tuned choice (the next plan run re-tunes). */
 int unet_tuning_reset(void);
+/* Slab-mode weight gradients (tuned or forced) that fell back to atomic
+ * accumulation because their split partials exceeded the plan's slab; reset
+ * != 0 also zeroes the count. */
+long long unet_slab_fallbacks(int reset);
 /* Tuning database (cf. MIOpen's perf-db): unet_tuning_save writes every tuned
  * choice as "key<TAB>tile<TAB>split" lines (returns the count or -errno);
  * unet_tuning_load merges such a file, overriding equal keys (returns the

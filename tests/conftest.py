@@ -35,6 +35,7 @@ def bench_tuning(request):
     # GEMM shapes these tests met that the database did not hold (tuned live)
     live = [ln.split(" | ")[0] for ln in _lib.tuning_report().splitlines() if ln and "tuning db" not in ln]
     print(f"\ntuning database misses (shapes tuned live): {len(live)}" + "".join(f"\n  {k}" for k in live))
+    print(f"slab-mode weight gradients that fell back to atomics: {_lib.slab_fallbacks(reset=True)}")
     _TUNE_REPORT.append((request.module.__name__, n, live))
     lib.unet_tuning_reset()
 

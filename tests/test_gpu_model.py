@@ -137,16 +137,24 @@ def gemm_mode(request):
                                        "tile12+split4", "tile14+split3", "tile3", "tile6", "tile51", "tile52",
                                        "tile53", "tile54", "tile51+split3", "heuristic+wgrad22",
                                        "heuristic+wgrad23", "tile70", "tile71", "tile72", "tile73", "tile74", "tile75", "tile76", "tile77",
-                                       "heuristic+wgrad71", "heuristic+wgrad74", "tile71+wgrad71"], indirect=True)
+                                       "heuristic+wgrad71", "heuristic+wgrad74", "tile71+wgrad71",
+                                       "heuristic+wgrad1071", "heuristic+wgrad1074", "heuristic+wgrad100",
+                                       "heuristic+wgrad103"], indirect=True)
 def test_train_step_gemm_variants_vs_oracle(gemm_mode):
     """Built-in tiles, the LDS-DMA staged tiles (11-14), the fp32 halo-tiled 3x3
     tiles (51-54; convT GEMMs fall back to the built-in tile), Winograd F(2x2,
     3x3) and F(4x4, 3x3) (70, 71, fused 72 / 73 / 76 (73 pipelined): every 3x3 forward / input-gradient GEMM with
     >= 128 channels both ways; fused F(2x2, 3x3) 75: every 3x3 forward / input
     gradient with 64-multiple outputs; 77: its 32-column form; wgrad71: the F(4x4, 3x3) weight gradient of the
-    same layers) and split-K (k_splitk_epi epilogue) on every conv / convT / dgrad GEMM
-    of a train step, against the oracle."""
+    same layers; wgrad1071 / 1074: the Winograd weight gradients in slab mode -- partials assigned, no
+    accumulator memset; wgrad100 / 103: pixel-column weight-gradient tiles 0 / 3 in slab mode, including the
+    single-split layers that store straight into the gradient) and split-K (k_splitk_epi epilogue) on every
+    conv / convT / dgrad GEMM of a train step, against the oracle."""
+    from unet_amd import _lib
+    _lib.slab_fallbacks(reset=True)
     test_train_step_vs_oracle(2, 188, 21, "fp32")
+    # a forced slab mode really ran as slab mode (none fell back to atomics)
+    assert _lib.slab_fallbacks() == 0
 
 
 @pytest.mark.parametrize("gemm_mode", ["heuristic", "tile21", "tile22", "tile23", "tile24", "tile25", "tile26",

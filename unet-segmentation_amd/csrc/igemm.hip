@@ -1101,6 +1101,7 @@ static int env_int(const char* name, int dflt) {
 // unet_set_tuning("igemm_variant", v) or UNET_IGEMM_VARIANT; -1 = heuristic
 int g_tune_igemm = env_int("UNET_IGEMM_VARIANT", -1);
 int g_tune_wgrad = env_int("UNET_WGRAD_VARIANT", -1);
+std::atomic<long long> g_slab_fallbacks{0};
 // unet_set_tuning("wino_max", m) or UNET_WINO_MAX: largest Winograd output tile
 // the fp32 forward / input-gradient candidates may use (6 = F(6x6) and below,
 // 4 = up to F(4x4), 2, 0 = none); "wino_wgrad_max" / UNET_WINO_WGRAD_MAX the
@@ -1218,11 +1219,11 @@ static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
 // tile's precision (fp32 `b` for tiles 1-14, bf16 `bh` for 21-26).
 bool igemm_tile_fits(const IgemmArgs& a, int tile) {
   // every 3x3 forward conv feeds a BatchNorm (stats); the input gradients do
-  // not.  An eval forward (BN folded into the weights: ReLU epilogue, no
-  // statistics -- no other GEMM of the plan has a ReLU epilogue) is held to the
-  // forward caps too, so eval logits see the same arithmetic as the training
-  // forward's parity checks
-  const bool fwd = a.e.stats != nullptr || a.e.relu;
+  // not.  An eval forward is held to the forward caps too, so eval logits see
+  // the same arithmetic as the training forward's parity checks;
+  // run_forward marks every 3x3 forward conv explicitly (IgemmArgs::fwd,
+  // ADVICE r04) rather than the caps being inferred from the epilogue
+  const bool fwd = a.fwd != 0;
   if (wino_tile_m(tile) > (fwd ? g_wino_max : g_wino_dgrad_max)) return false;
   if (fwd && wino_tile_m(tile) >= 4 && a.a.Cg < g_wino4_fwd_min_cg && a.a.Cg > g_wino4_fwd_small_cg)
     return false;
@@ -1464,7 +1465,13 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     if ((g_tune_wgrad == 22 || g_tune_wgrad == 23 || g_tune_wgrad == 71 || g_tune_wgrad == 74) &&
         wgrad_tile_fits(a, g_tune_wgrad))
       tile = g_tune_wgrad;  // forced fp32 halo tile (tests)
-    else if (g_tune_wgrad == 1) tile = 4;  // force the small tile (A/B tests)
+    else if ((g_tune_wgrad == 1071 || g_tune_wgrad == 1074) && wgrad_tile_fits(a, g_tune_wgrad - 1000)) {
+      tile = g_tune_wgrad - 1000;  // forced Winograd weight gradient in slab mode (tests; no Mw memset)
+      c.split = 1000;
+    } else if (g_tune_wgrad >= 100 && g_tune_wgrad <= 104 && wgrad_tile_fits(a, g_tune_wgrad - 100)) {
+      c.tile = tile = g_tune_wgrad - 100;  // forced fp32 pixel-column tile in slab mode, 2 per CU (tests)
+      c.split = 102;
+    } else if (g_tune_wgrad == 1) tile = 4;  // force the small tile (A/B tests)
     else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 0;
     else if (a.Mo % 128 == 0 && a.No % 192 == 0) tile = 1;
     else if (a.No % 192 == 0) tile = 2;
@@ -1492,7 +1499,10 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   // slab mode: one split writes its planes straight into out (plain stores),
   // more go through the slab and an assigning reduction; either way every
   // output element is written, so out needs no zeroing
-  if (!(slab_mode && wgrad_slab_fits(a, splits))) a.slab = nullptr;
+  if (!(slab_mode && wgrad_slab_fits(a, splits))) {
+    if (slab_mode) ++g_slab_fallbacks;  // split partials exceed the plan's wslab: atomics instead
+    a.slab = nullptr;
+  }
   else if (splits == 1) a.slab = a.out;
   dim3 grid(a.Mo / bm, a.No / bn, splits * a.batch);
   hipError_t e = hipSuccess;
@@ -1551,6 +1561,8 @@ double wgrad_exec_flops(const WgradArgs& a, GemmChoice c) {
   int t = c.tile;
   if (t < 0 && !a.bf16 && (g_tune_wgrad == 71 || g_tune_wgrad == 74) && wgrad_tile_fits(a, g_tune_wgrad))
     t = g_tune_wgrad;
+  if (t < 0 && !a.bf16 && (g_tune_wgrad == 1071 || g_tune_wgrad == 1074) && wgrad_tile_fits(a, g_tune_wgrad - 1000))
+    t = g_tune_wgrad - 1000;
   if (t == 71 || t == 74) {
     const int mt = t == 71 ? 4 : 6;
     const double T = (double)a.gb.nimg * ((a.gb.Hg + mt - 1) / mt) * ((a.gb.Wg + mt - 1) / mt);

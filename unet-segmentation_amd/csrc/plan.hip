@@ -299,7 +299,10 @@ std::string igemm_key(const IgemmArgs& a) {
   if (unet::g_wino4_fwd_small_cg) snprintf(small, sizeof small, "/s%d", unet::g_wino4_fwd_small_cg);
   const Epilogue& e = a.e;
   const int epi = (e.shuffle_co ? 1 : 0) | (e.stats ? 2 : 0) | (e.yref ? 4 : 0) | (e.colsum1 ? 8 : 0) |
-                  (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0) | (e.relu ? 64 : 0);
+                  (a.a.s[0].scale ? 16 : 0) | (a.a.c_split != a.a.Cg ? 32 : 0) | (e.relu ? 64 : 0) |
+                  // a forward without statistics or ReLU (unfolded eval): the
+                  // only forward the other bits do not already tell apart
+                  (a.fwd && !e.stats && !e.relu ? 128 : 0);
   // the Winograd caps decide which candidates exist: a choice tuned under other
   // caps is a different key
   snprintf(b, sizeof b, "igemm%s M=%d N=%d K=%d Cg=%d taps=%dx%d s=%d grid=%dx%d epi=%d wino=%d/%d/%d%s tt=%d",
@@ -745,6 +748,7 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
     a.K = 9 * L.ci;
     a.e.bias = p->fold ? c.f(L.coef) : P<float>(prm, L.pw + 1);
     a.e.relu = p->fold;
+    a.fwd = 1;
     a.e.d[0] = Dst{c.f(L.y), L.ho, L.wo, L.co, 0, 0, p->prec == UNET_PREC_BF16};
     a.e.stats = train ? c.d(L.stats) : nullptr;
     {
@@ -1388,6 +1392,10 @@ size_t unet_tuning_report(char* buf, size_t len) {
     buf[k] = 0;
   }
   return r.size() + 1;
+}
+
+long long unet_slab_fallbacks(int reset) {
+  return reset ? g_slab_fallbacks.exchange(0) : g_slab_fallbacks.load();
 }
 
 int unet_tuning_reset(void) {

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <cstddef>
 #include <cstdint>
+#include <atomic>
 
 namespace unet {
 
@@ -101,7 +102,15 @@ struct IgemmArgs {
   int batch_rows = 0;
   long long batch_b = 0;
   struct { int tile = -1, split = 1; } wino_choice;
+  // a 3x3 forward conv of the plan (training or eval): held to the forward
+  // Winograd caps (g_wino_max, the F(4x4) channel window); every other GEMM
+  // (input gradients, convT, op-level calls) to the input-gradient caps
+  int fwd = 0;
 };
+
+// slab-mode weight gradients that ran with atomics instead (the plan's wslab
+// too small for their split partials); unet_slab_fallbacks() reads it
+extern std::atomic<long long> g_slab_fallbacks;
 
 struct WgradArgs {
   // C[i][j] = sum_p A_p[i] * B_p[j] over the pixels p of the grid of `ga`.

@@ -2374,6 +2374,7 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
     q.slab_bytes = a.slab_bytes;
     int pps = 0;
     const bool use_slab = slab && wgrad_slab_fits(q, wgrad_splits(q, tile, per_cu, pps));
+    if (slab && !use_slab) ++g_slab_fallbacks;
     if (!use_slab && (e = hipMemsetAsync(Mw, 0, (size_t)P * Co * Ci * 4, s)) != hipSuccess) return e;
     if ((e = launch_wgrad_v(q, s, GemmChoice{tile, use_slab ? per_cu + 100 : per_cu})) != hipSuccess) return e;
   }

@@ -91,6 +91,7 @@ SIGNATURES = {
     "unet_set_tuning": (_i, [ctypes.c_char_p, _i]),
     "unet_tuning_report": (_sz, [ctypes.c_char_p, _sz]),
     "unet_tuning_reset": (_i, []),
+    "unet_slab_fallbacks": (ctypes.c_longlong, [_i]),
     "unet_tuning_save": (_i, [ctypes.c_char_p]),
     "unet_tuning_load": (_i, [ctypes.c_char_p]),
 }
@@ -174,6 +175,11 @@ def build_identity() -> dict:
     tree = source_hash()
     return {"version": v, "lib_src": built, "tree_src": tree, "src_match": built == tree,
             "ablation_build": v.endswith(" ablations")}
+
+
+def slab_fallbacks(reset: bool = False) -> int:
+    """Slab-mode weight gradients that fell back to atomics (wslab too small)."""
+    return int(load().unet_slab_fallbacks(1 if reset else 0))
 
 
 def tuning_report() -> str:
