@@ -835,3 +835,48 @@ def test_trainer_hipgraph_replay_label_flag(precision, concurrent):
         print(f"{precision} concurrent={concurrent}: label-flag slots read before landing: {tr.labels.premature}")
     finally:
         lib.unet_set_tuning(b"concurrent", 1)
+
+
+@pytest.mark.parametrize("gemm_mode", ["heuristic"], indirect=True)
+@pytest.mark.parametrize("n,h,seed", [(2, 188, 31), (1, 195, 32)])
+def test_bf16_maxpool_vec8_bitexact(gemm_mode, n, h, seed):
+    """The bf16 plans' 8-channel max-pool forward (k_maxpool_fwd_bf8) against
+    the 4-channel kernel it replaced, odd pooling sizes included (195: floor
+    mode drops a row).  Train logits, loss and eval logits are bit-identical
+    (the pooled maps and the normalised skip copies both feed them).  The
+    gradients (routed by the argmax bytes) differ only by the run-to-run noise
+    of the atomic weight-gradient and statistics sums: they are held to that
+    noise, measured from a repeat run of the 4-channel kernel."""
+    from unet_amd import WeightedCrossEntropyLoss, _lib
+    lib = _lib.load()
+    params = O.hash_init(1, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
+    outs = []
+    try:
+        for vec8 in (0, 0, 1):
+            lib.unet_set_tuning(b"maxpool_vec8", vec8)
+            m = make_model(params, precision="bf16")
+            m.train()
+            xd = torch.from_numpy(x).cuda()
+            logits = m(xd)
+            loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+            loss.backward()
+            m.eval()
+            with torch.no_grad():
+                ge = m(xd)
+            torch.cuda.synchronize()
+            outs.append(([logits.detach().cpu(), loss.detach().cpu(), ge.cpu()],
+                         [p.grad.detach().double().cpu() for p in m.parameters()]))
+            del m
+    finally:
+        lib.unet_set_tuning(b"maxpool_vec8", 1)
+    (f0, g0), (_, g0b), (f1, g1) = outs
+    for i, (a, b) in enumerate(zip(f0, f1)):
+        assert torch.equal(a, b), f"forward output {i} differs"
+    worst = 0.0
+    for i, (a, b, c) in enumerate(zip(g0, g0b, g1)):
+        nrm = a.norm().item() + 1e-30
+        noise, diff = (b - a).norm().item() / nrm, (c - a).norm().item() / nrm
+        assert diff <= 2 * noise + 1e-6, f"gradient {i}: rel-L2 {diff:.2e} vs run-to-run {noise:.2e}"
+        worst = max(worst, diff)
+    print(f"forward bit-identical; worst gradient rel-L2 {worst:.2e}")

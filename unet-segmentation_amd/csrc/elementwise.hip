@@ -785,9 +785,102 @@ __global__ void k_maxpool_fwd(Src s, int n, int h, int w, float* __restrict__ y,
   }
 }
 
+// bf16 in / bf16 out twin of k_maxpool_fwd<1, 1>: 8 channels (16 B) per lane
+// instead of 4 (8 B), the same fmaf / fmaxf / strict '>' / RNE per element, so
+// the pooled map, argmax bytes and normalised copy are bit-identical to it
+__global__ __launch_bounds__(256) void k_maxpool_fwd_bf8(Src s, int n, int h, int w, uint16_t* __restrict__ y,
+                                                         uint8_t* __restrict__ arg, uint16_t* __restrict__ anorm) {
+  const int C = s.C, C8 = C / 8, ho = h / 2, wo = w / 2;
+  const long long total = (long long)n * ho * wo * C8;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const uint16_t* src = reinterpret_cast<const uint16_t*>(s.ptr);
+  constexpr int U = 2;  // items per trip, every window load issued before any use
+  for (long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x; i0 < total; i0 += U * stride) {
+    uint4 raw[U][4];
+    size_t sb0[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = min(i0 + u * stride, total - 1);  // tail items recompute the last one (not stored)
+      const int c8 = (int)(i % C8);
+      long long p = i / C8;
+      const int xo = (int)(p % wo);
+      p /= wo;
+      const int yo = (int)(p % ho);
+      const int nn = (int)(p / ho);
+      sb0[u] = ((size_t)(nn * s.H + 2 * yo + s.oy) * s.W + 2 * xo + s.ox) * C + c8 * 8;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        raw[u][k] = *reinterpret_cast<const uint4*>(src + sb0[u] + ((size_t)(k >> 1) * s.W + (k & 1)) * C);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = i0 + u * stride;
+      if (i >= total) continue;
+      const int c = (int)(i % C8) * 8;
+      float4 v[4][2];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[k][0] = bf16x4_to_f4(make_uint2(raw[u][k].x, raw[u][k].y));
+        v[k][1] = bf16x4_to_f4(make_uint2(raw[u][k].z, raw[u][k].w));
+      }
+      if (s.scale) {
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const float4 a = ld4(s.scale + c + 4 * hh), b = ld4(s.shift + c + 4 * hh);
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float4& t = v[k][hh];
+            t.x = fmaxf(fmaf(t.x, a.x, b.x), 0.f);
+            t.y = fmaxf(fmaf(t.y, a.y, b.y), 0.f);
+            t.z = fmaxf(fmaf(t.z, a.z, b.z), 0.f);
+            t.w = fmaxf(fmaf(t.w, a.w, b.w), 0.f);
+          }
+        }
+      }
+      if (anorm) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          *reinterpret_cast<uint4*>(anorm + sb0[u] + ((size_t)(k >> 1) * s.W + (k & 1)) * C) =
+              bf16pack8(v[k][0], v[k][1]);
+      }
+      float4 best[2];
+      uchar4 am[2];
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        best[hh] = v[0][hh];
+        am[hh] = make_uchar4(0, 0, 0, 0);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+          if (v[k][hh].x > best[hh].x) { best[hh].x = v[k][hh].x; am[hh].x = k; }
+          if (v[k][hh].y > best[hh].y) { best[hh].y = v[k][hh].y; am[hh].y = k; }
+          if (v[k][hh].z > best[hh].z) { best[hh].z = v[k][hh].z; am[hh].z = k; }
+          if (v[k][hh].w > best[hh].w) { best[hh].w = v[k][hh].w; am[hh].w = k; }
+        }
+      }
+      reinterpret_cast<uint4*>(y)[i] = bf16pack8(best[0], best[1]);
+      uint2 ab;
+      ab.x = (unsigned)am[0].x | ((unsigned)am[0].y << 8) | ((unsigned)am[0].z << 16) | ((unsigned)am[0].w << 24);
+      ab.y = (unsigned)am[1].x | ((unsigned)am[1].y << 8) | ((unsigned)am[1].z << 16) | ((unsigned)am[1].w << 24);
+      reinterpret_cast<uint2*>(arg)[i] = ab;
+    }
+  }
+}
+
+// unet_set_tuning("maxpool_vec8", 0): the 4-channel forward (A/B tests).  An
+// 8-channel twin of k_maxpool_bwd_fused<1, 1> was measured too: with its
+// statistics partials kept bit-identical (128-lane blocks on the same grid) it
+// ran no faster (118 vs 115 us per launch), so the backward keeps 4 channels.
+int g_maxpool_vec8 = 1;
+
 hipError_t launch_maxpool_fwd(const Src& s, int n, int h, int w, float* y, uint8_t* arg, hipStream_t st,
                               int out_h16, uint16_t* anorm) {
   if (s.C % 4 || (anorm && (s.oy || s.ox))) return hipErrorInvalidValue;
+  if (g_maxpool_vec8 && out_h16 && s.h16 && s.C % 8 == 0) {
+    const long long work8 = (long long)n * (h / 2) * (w / 2) * (s.C / 8);
+    hipLaunchKernelGGL(k_maxpool_fwd_bf8, dim3(grid_cap(work8, 256, 8192)), dim3(256), 0, st, s, n, h, w,
+                       reinterpret_cast<uint16_t*>(y), arg, anorm);
+    return hipGetLastError();
+  }
   const long long work = (long long)n * (h / 2) * (w / 2) * (s.C / 4);
   const dim3 grid(grid_cap(work, 256, 8192));
   switch (out_h16 * 2 + (s.h16 ? 1 : 0)) {
