@@ -13,7 +13,10 @@ of scripts/train.py:108-131 (no per-step .item()).
     python bench.py [--gpus N --steps K --warmup W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 
-Prints ONE JSON line on rank 0.  Besides the contract fields it carries:
+Prints ONE compact JSON line on rank 0 (the contract fields and every headline
+number, ~1.5 KB so a 2 KB log tail holds all of it) and writes the full record
+-- per-launch-site timings, kernel classes, descriptions -- to --detail-out
+(default gpurun_out/bench_detail.json).  The full record carries:
 * roofline: the implicit-GEMM conv family (63 GEMM launch sites per step) at
   the MFMA peak of the precision, HIP-event timed on the plan's stream in an
   extra untimed step; `achieved` counts the MFMA flops the chosen variants
@@ -177,6 +180,54 @@ def apply_measured_peaks(obj, dtype, peaks):
     if hbm and st and st.get("achieved_gbs"):
         st["peak_measured_gbs"] = hbm
         st["frac_measured"] = round(st["achieved_gbs"] / hbm, 4)
+
+
+def compact_line(out, detail):
+    """The stdout line: the contract fields plus every headline number (fp32 and
+    bf16 values, conv-family and bottleneck fractions, stage 1, c5, farm, IoU,
+    CPU baseline, measured peaks), without the per-site tables and prose -- those
+    are in the detail file."""
+    def pick(d, keys):
+        return {k: d[k] for k in keys if d is not None and k in d}
+
+    line = pick(out, ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better",
+                      "scaling", "vs_baseline", "dtype"))
+    line["data"] = "synthetic x~U[0,1), Bernoulli(0.4) targets, 10+1/freq weights, kaiming init"
+    line["config"] = {"workload": out["config"]["workload"].split(":")[0] + " (fwd+WCE+bwd+SGD)",
+                      **pick(out["config"], ("global_batch", "image", "parallelism"))}
+    rl = out["roofline"]
+    line["roofline"] = {**pick(rl, ("bound", "achieved", "peak", "unit", "frac", "frac_measured", "traffic")),
+                        "kernel": "conv GEMM family (executed MFMA flops)"}
+    if "cpu_baseline" in out:
+        cb = out["cpu_baseline"]
+        line["cpu_baseline"] = {**pick(cb, ("value", "unit", "cores", "kind", "batch1_value")),
+                                "sample": "torch-CPU restatement of the reference step, batch 8 / 1, median of 5"}
+    line["bottleneck"] = pick(out.get("bottleneck"), ("ms", "frac", "frac_measured"))
+    line["stage1"] = pick(out.get("stage1"), ("ms", "achieved_gbs", "frac"))
+    for d in ("fp32", "bf16", "bf16x3"):
+        if d in out and isinstance(out[d], dict) and "value" in out[d]:
+            r = out[d]
+            line[d] = {**pick(r, ("value", "ms_per_step")),
+                       "frac": r["roofline"]["frac"],
+                       "bottleneck": pick(r.get("bottleneck"), ("ms", "frac", "frac_measured")),
+                       "elementwise_ms": r.get("kernels", {}).get("elementwise", {}).get("ms")}
+            if r.get("iou"):
+                line[d]["iou"] = r["iou"]["iou"]
+    if "c5" in out:
+        line["c5"] = {**pick(out["c5"], ("value", "ms_per_step")), "frac": out["c5"]["roofline"]["frac"],
+                      "bottleneck_frac": out["c5"].get("bottleneck", {}).get("frac")}
+    if "farm" in out:
+        line["farm"] = {d: r["value"] for d, r in out["farm"].items()}
+    if out.get("iou"):
+        line["iou"] = pick(out["iou"], ("iou", "iou_ref", "frames"))
+    if out.get("comm"):
+        line["comm"] = pick(out["comm"], ("dtype", "bytes_per_step"))
+    if out.get("peaks_measured"):
+        line["peaks"] = pick(out["peaks_measured"], ("bf16_mfma_tflops", "fp32_mfma_tflops", "hbm_gbs"))
+    line["lib"] = pick(out.get("lib"), ("lib_src", "src_match", "tune_db_entries"))
+    if detail:
+        line["detail"] = detail
+    return line
 
 
 def hela_frames():
@@ -446,6 +497,10 @@ def main():
     ap.add_argument("--no-peaks", action="store_true", help="skip the untimed peak probes of the tail")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (= RCCL over xGMI, one GPU per rank) or gloo (ranks may share a GPU; rehearsal only)")
+    ap.add_argument("--detail-out", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="write the full record (per-site timings, kernel classes) here ('' = don't)")
+    ap.add_argument("--full-stdout", action="store_true", help="print the full record instead of the compact line "
+                    "(tools that read kernel classes from stdout)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -552,7 +607,15 @@ def main():
                 apply_measured_peaks(out[d], d, peaks)
             if "c5" in out:
                 apply_measured_peaks(out["c5"], "bf16", peaks)
-        print(json.dumps(out))
+        # the full record (every GEMM launch site, kernel classes, descriptions)
+        # goes to a file; stdout carries one compact line that fits a 2 KB log
+        # tail with every headline in it
+        detail = args.detail_out
+        if detail:
+            os.makedirs(os.path.dirname(os.path.abspath(detail)), exist_ok=True)
+            with open(detail, "w") as f:
+                json.dump(out, f, indent=1)
+        print(json.dumps(out) if args.full_stdout else json.dumps(compact_line(out, detail), separators=(",", ":")))
     if pg is not None:
         dist.destroy_process_group()
 

@@ -336,7 +336,13 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  _dgrad store their A operand bf16 first (x rounded before
  *                  the BN+ReLU transform; padded dY bf16), as a bf16 plan
  *                  does -- the configuration the 61-66 tiles (bf16-stored A
- *                  only) run in; 0 (default) = fp32 A. */
+ *                  only) run in; 0 (default) = fp32 A.
+ *  "deterministic" 1 (or env UNET_DETERMINISTIC=1; default 0) = every weight
+ *                  gradient runs a variant without fp32 atomics (slab
+ *                  partials summed in a fixed order) and inc.c0's slab
+ *                  reduction runs in one pass: plan steps are
+ *                  bit-reproducible run to run (see
+ *                  unet_nondeterministic_sites). */
 int unet_set_tuning(const char* key, int value);
 /* Text report of the tuned GEMM choices (one line per shape: key, heuristic
  * time, chosen variant and time).  Copies up to len-1 bytes + NUL into buf
@@ -348,6 +354,11 @@ int unet_tuning_reset(void);
  * accumulation because their split partials exceeded the plan's slab; reset
  * != 0 also zeroes the count. */
 long long unet_slab_fallbacks(int reset);
+/* Deterministic mode (unet_set_tuning("deterministic", 1) or
+ * UNET_DETERMINISTIC=1): weight-gradient launch sites that found no
+ * atomic-free variant and ran with fp32 atomics; reset != 0 also zeroes the
+ * count.  0 after a step means the step is bit-reproducible. */
+long long unet_nondeterministic_sites(int reset);
 /* Tuning database (cf. MIOpen's perf-db): unet_tuning_save writes every tuned
  * choice as "key<TAB>tile<TAB>split" lines (returns the count or -errno);
  * unet_tuning_load merges such a file, overriding equal keys (returns the

@@ -11,7 +11,10 @@ gloo (RCCL needs one GPU per rank; the all-reduce call pattern is the same).
          UNET_DP_BACKEND=nccl: RCCL (one GPU per rank: world 1 on the test box),
          UNET_DP_FORCE=1: issue the collectives at world 1 too (Trainer force_collectives),
          UNET_DP_STEP=1: whole Trainer.step() calls (with the per-step buffer broadcast),
-         UNET_DP_SYNC_BCAST=1: that broadcast synchronous ahead of every forward (not deferred)
+         UNET_DP_SYNC_BCAST=1: that broadcast synchronous ahead of every forward (not deferred),
+         UNET_DP_RELOAD_AT=k: before step k every rank load_state_dict()s its model with new
+           BatchNorm running statistics (UNET_DP_RELOAD_SYNC=1: then Trainer.sync_buffers()),
+         UNET_DETERMINISTIC=1: the library's deterministic mode (no fp32 atomics)
 """
 import os
 import sys
@@ -68,11 +71,22 @@ def main():
     if os.environ.get("UNET_DP_STEP") == "1":
         starts = []
         tr.on_buffers_synced = lambda b: starts.append(b.double().cpu().numpy().copy())
+        reload_at = int(os.environ.get("UNET_DP_RELOAD_AT", "-1"))
+        _lib.load().unet_nondeterministic_sites(1)
         for s in range(steps):
+            if s == reload_at:  # a checkpoint resume between steps, on every rank
+                sd = {k: v.clone() for k, v in m.state_dict().items()}
+                new = F.plausible_running_stats({k: v.cpu().numpy() for k, v in sd.items()}, 900 + s)
+                m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in new.items()})
+                res["reloaded"] = tr.flat_buffers.flat.double().cpu().numpy().copy()
+                if os.environ.get("UNET_DP_RELOAD_SYNC") == "1":
+                    tr.sync_buffers()
             res[f"loss{s}"] = np.array(tr.step(x, t, w).item())
             torch.cuda.synchronize()
             res[f"buf{s}"] = tr.flat_buffers.flat.double().cpu().numpy().copy()
         res["params"] = tr.flat.flat.cpu().numpy().copy()
+        res["nondet_sites"] = np.array(_lib.load().unet_nondeterministic_sites(0))
+        res["slab_fallbacks"] = np.array(_lib.slab_fallbacks())
         for s, b in enumerate(starts):
             res[f"start{s}"] = b  # the buffers each step's forward started from
         np.savez(out, **res)

@@ -55,14 +55,18 @@ def digest(name, g, out):
     out[f"gval/{name}"] = g[idx]
 
 
-def whole_model_case(tag, n, h, n_channels=1, seed=1, steps=0):
+def whole_model_case(tag, n, h, n_channels=1, seed=1, steps=0, w=None):
+    """Train-mode forward + loss + backward (+ `steps` SGD steps) of the
+    reference on an n x c x h x w batch (w = h unless given: the reference crops
+    height and width separately, models/unet_model.py:93-100)."""
+    w = h if w is None else w
     params = O.hash_init(n_channels, 2, seed=seed, bn_random=True)
-    x, tgt, wmap = F.make_inputs(seed, n, n_channels, h)
+    x, tgt, wmap = F.make_inputs(seed, n, n_channels, h, w)
     m = ref_model(params, n_channels)
     m.train()
     crit = WeightedCrossEntropyLoss()
     xt = _t(x)
-    out = {"x_seed": np.array(seed), "n": np.array(n), "h": np.array(h), "c": np.array(n_channels)}
+    out = {"x_seed": np.array(seed), "n": np.array(n), "h": np.array(h), "w": np.array(w), "c": np.array(n_channels)}
     logits = m(xt)
     loss = crit(logits, torch.from_numpy(tgt), _t(wmap))
     loss.backward()
@@ -476,6 +480,9 @@ if __name__ == "__main__":
         whole_model_case("n2_188", 2, 188, seed=1, steps=3)
     if "m204" in which:
         whole_model_case("n2_204", 2, 204, seed=2)
+    if "mhw" in which:  # H != W (VERDICT r05 missing item 2): the crops differ per axis
+        whole_model_case("n2_188x220", 2, 188, seed=41, w=220)
+        whole_model_case("n1_204x252", 1, 204, seed=42, w=252)
     if "f512" in which:
         forward_only_case("n1_512", 1, 512, seed=3)
     if "f572" in which:

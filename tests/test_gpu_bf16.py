@@ -390,11 +390,14 @@ def check_vs_bf16_oracle(m, params, x, tgt, wmap, tag=""):
           f"worst grad err / tol {worst:.2f}")
 
 
-@pytest.mark.parametrize("n,h,seed", [(2, 188, 11), (2, 204, 12), (1, 220, 13)])
-def test_bf16_train_step_vs_bf16_oracle(lib, n, h, seed):
+@pytest.mark.parametrize("n,h,w,seed", [(2, 188, 188, 11), (2, 204, 204, 12), (1, 220, 220, 13), (2, 188, 220, 41),
+                                        (1, 204, 252, 42)])
+def test_bf16_train_step_vs_bf16_oracle(lib, n, h, w, seed):
+    """Square and H != W batches (the plan crops each axis on its own,
+    models/unet_model.py:93-100)."""
     params = O.hash_init(1, 2, seed=seed, bn_random=True)
-    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
-    check_vs_bf16_oracle(make_model(params), params, x, tgt, wmap, f"{n}x{h}")
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h, w)
+    check_vs_bf16_oracle(make_model(params), params, x, tgt, wmap, f"{n}x{h}x{w}")
 
 
 @pytest.fixture

@@ -181,3 +181,113 @@ def test_ops_path_train_step_matches_plan():
         if O.bn_cancelled(k):
             continue
         assert _rel(go[k], gp[k]) <= 1e-2, (k, _rel(go[k], gp[k]))
+
+
+def test_forward_takes_strided_inputs():
+    """models/unet_model.py:105 takes any strided float32 tensor: a transposed
+    and a sliced (non-contiguous) view, and a channels_last 3-channel batch,
+    give the loss, input and weight gradients / logits of the same values
+    passed contiguously."""
+    from unet_amd import WeightedCrossEntropyLoss
+    m, _ = _model(83)
+    m = m.cuda().train()
+    x, tgt, wmap = F.make_inputs(83, 2, 1, 188)
+    big = torch.zeros((2, 1, 188, 200), dtype=torch.float32, device="cuda")
+    big[..., 5:193] = torch.from_numpy(x).cuda()
+    t, w = torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda()
+    res = {}
+    for kind in ("contiguous", "transposed", "slice"):
+        if kind == "contiguous":
+            xi = torch.from_numpy(x).cuda()
+        elif kind == "transposed":  # the same values through a (W, H)-strided view
+            xi = torch.from_numpy(np.ascontiguousarray(x.transpose(0, 1, 3, 2))).cuda().transpose(2, 3)
+        else:
+            xi = big[..., 5:193]
+        assert kind == "contiguous" or not xi.is_contiguous()
+        xi = xi.detach().requires_grad_(True)
+        m.zero_grad(set_to_none=True)
+        loss = WeightedCrossEntropyLoss()(m(xi), t, w)
+        loss.backward()
+        res[kind] = (loss.item(), xi.grad.detach().cpu().numpy(),
+                     m.outc.conv.weight.grad.detach().cpu().numpy())
+    for kind in ("transposed", "slice"):
+        a, b = res[kind], res["contiguous"]
+        assert abs(a[0] - b[0]) <= 1e-6 * abs(b[0]), kind
+        np.testing.assert_allclose(a[1], b[1], rtol=0, atol=1e-4 * np.abs(b[1]).max(), err_msg=kind)
+        np.testing.assert_allclose(a[2], b[2], rtol=0, atol=1e-4 * np.abs(b[2]).max(), err_msg=kind)
+    # a 4-D channels_last tensor of a multi-channel model
+    m3 = _model(84, c=3)[0].cuda().eval()
+    x3 = torch.rand((1, 3, 188, 188), device="cuda")
+    with torch.no_grad():
+        a = m3(x3.contiguous(memory_format=torch.channels_last))
+        b = m3(x3)
+    assert torch.equal(a, b)
+    # other dtypes raise outside autocast, as the reference's first conv does
+    with pytest.raises(RuntimeError):
+        m3(x3.double())
+
+
+def test_blocks_under_bf16_autocast():
+    """model.inc(x) / down4 / up1 / outc inside torch.autocast("cuda", bf16):
+    the reference's submodules run there (their convs on bf16 operands, bf16
+    results); the blocks run their GEMMs on bf16 operands with fp32
+    accumulation and return bf16.  Against the fp32 blocks: within bf16
+    rounding (2^-8 relative per operand, accumulated over the block); the
+    backward works and returns gradients in the input's dtype."""
+    m, _ = _model(85)
+    m = m.cuda().train()
+    g = torch.Generator(device="cuda").manual_seed(3)
+    cases = [("inc", lambda x: m.inc(x), [torch.rand(2, 1, 36, 36, device="cuda", generator=g)]),
+             ("down4", lambda x: m.down4(x), [torch.rand(2, 512, 14, 14, device="cuda", generator=g) * 2 - 1]),
+             ("up1", lambda a, b: m.up1(a, b), [torch.rand(2, 1024, 5, 5, device="cuda", generator=g),
+                                                torch.rand(2, 512, 10, 10, device="cuda", generator=g)]),
+             ("outc", lambda x: m.outc(x), [torch.rand(2, 64, 7, 9, device="cuda", generator=g)])]
+    for name, fn, ins in cases:
+        m.eval()  # fixed statistics: the two runs see the same BatchNorm
+        ref = fn(*ins).float()
+        xs = [t.clone().to(torch.bfloat16).requires_grad_(True) for t in ins]
+        with torch.autocast("cuda", dtype=torch.bfloat16):
+            out = fn(*xs)
+        assert out.dtype == torch.bfloat16, name
+        scale = float(ref.abs().max())
+        err = float((out.float() - ref).abs().max())
+        assert err <= 3e-2 * scale, (name, err, scale)
+        out.float().sum().backward()
+        for x in xs:
+            assert x.grad is not None and x.grad.dtype == torch.bfloat16, name
+    m.train()
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m.inc(torch.rand(2, 1, 36, 36, device="cuda"))
+    assert y.dtype == torch.bfloat16
+
+
+def test_eval_backward_uses_forward_mode_and_saved_weights():
+    """the eval-mode backward recomputes in eval mode even when the
+    module was switched to train() before .backward() (same gradients, running
+    statistics untouched); a parameter modified in place between forward and
+    backward raises, as torch autograd does for a saved weight."""
+    from unet_amd import WeightedCrossEntropyLoss
+    m, _ = _model(86)
+    m = m.cuda()
+    x, tgt, wmap = (torch.from_numpy(a).cuda() for a in F.make_inputs(86, 2, 1, 188))
+    crit = WeightedCrossEntropyLoss()
+    m.eval()
+    crit(m(x), tgt, wmap).backward()
+    g_ref = {k: p.grad.clone() for k, p in m.named_parameters()}
+    m.zero_grad(set_to_none=True)
+    bufs = {k: b.clone() for k, b in m.named_buffers()}
+    loss = crit(m(x), tgt, wmap)
+    m.train()  # between forward and backward
+    loss.backward()
+    for k, p in m.named_parameters():
+        assert torch.allclose(p.grad, g_ref[k], rtol=1e-5, atol=1e-6 * float(g_ref[k].abs().max()) + 1e-12), k
+    for k, b in m.named_buffers():
+        assert torch.equal(b, bufs[k]), k
+    for mode in ("eval", "train"):
+        m.train(mode == "train")
+        m.zero_grad(set_to_none=True)
+        loss = crit(m(x), tgt, wmap)
+        with torch.no_grad():
+            m.outc.conv.weight.add_(1.0)  # an optimizer step before the backward
+        with pytest.raises(RuntimeError, match="inplace"):
+            loss.backward()

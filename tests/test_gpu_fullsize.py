@@ -274,6 +274,7 @@ def test_fp32_512_every_logit_and_gradient_vs_reference_fp64(fixture, path):
     sure = np.abs(rl[:, 1] - rl[:, 0]) > 1e-3
     np.testing.assert_array_equal((lg[:, 1] > lg[:, 0])[sure], (rl[:, 1] > rl[:, 0])[sure])
     worst, worst_name = 0.0, ""
+    above, over_1pct = [], 0
     for name, g in grads.items():
         r = rg[name]
         g = g.reshape(r.shape)
@@ -286,6 +287,15 @@ def test_fp32_512_every_logit_and_gradient_vs_reference_fp64(fixture, path):
         tol = max(1e-2, 2 * floor)
         if e / tol > worst:
             worst, worst_name = e / tol, name
+        if tol > 1e-2:  # the bar rose above SURVEY §8c's 1 % with the reference's own fp32 floor
+            above.append((name, e, floor, tol))
+        over_1pct += e > 1e-2
         assert e <= tol, (name, e, floor)
+    # every tensor whose bar exceeds 1 %: its error, the
+    # reference's own fp32-vs-fp64 floor and the bar
+    for name, e, floor, tol in sorted(above, key=lambda a: -a[3]):
+        print(f"  bar > 1 %: {name}: rel-L2 {e:.4f}, reference fp32 floor {floor:.4f}, bar {tol:.4f} "
+              f"({e / tol:.2f} of it)")
     print(f"512^2 batch {n} ({path}), every element: logits max |err| {lerr:.2e}, {int((~sure).sum())} low-margin "
-          f"pixels, worst gradient rel-L2 / tol {worst:.2f} ({worst_name})")
+          f"pixels, worst gradient rel-L2 / tol {worst:.2f} ({worst_name}); {len(above)} of {len(grads)} tensors "
+          f"have a bar above 1 %, {over_1pct} have an error above 1 %")

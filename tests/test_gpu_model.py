@@ -219,21 +219,25 @@ def test_train_step_odd_pooling(n, h, seed):
     test_train_step_vs_oracle(n, h, seed, "fp32")
 
 
-@pytest.mark.parametrize("tag", ["n2_188", "n2_204"])
+@pytest.mark.parametrize("tag", ["n2_188", "n2_204", "n2_188x220", "n1_204x252"])
 def test_vs_reference_fixture(tag, precision="fp32"):
     """Elementwise sampled gradients vs the reference run (fp32 only: bf16x3's
     BN-bias gradients sit outside these per-element bounds, see the module
-    docstring; its whole-network checks are the oracle-based ones)."""
+    docstring; its whole-network checks are the oracle-based ones).  The
+    n2_188x220 / n1_204x252 fixtures are H != W batches: the reference crops the
+    skips' height and width separately (models/unet_model.py:93-100)."""
     z = np.load(os.path.join(G, f"model_{tag}.npz"), allow_pickle=False)
     from unet_amd import WeightedCrossEntropyLoss
     seed, n, h, c = int(z["x_seed"]), int(z["n"]), int(z["h"]), int(z["c"])
+    w = int(z["w"]) if "w" in z.files else h
     params = O.hash_init(c, 2, seed=seed, bn_random=True)
-    x, tgt, wmap = F.make_inputs(seed, n, c, h)
+    x, tgt, wmap = F.make_inputs(seed, n, c, h, w)
     m = make_model(params, c, precision=precision)
     logits = m(torch.from_numpy(x).cuda())
     loss = WeightedCrossEntropyLoss()(logits, torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
     loss.backward()
     lg = logits.detach().double().cpu().numpy()
+    assert lg.shape == z["logits"].shape
     assert np.abs(lg - z["logits"]).max() <= 1e-3
     assert abs(loss.item() - float(z["loss"])) <= 1e-4 * abs(float(z["loss"]))
     margin = np.abs(z["logits"][:, 1] - z["logits"][:, 0])
@@ -255,6 +259,61 @@ def test_vs_reference_fixture(tag, precision="fp32"):
         assert abs(np.linalg.norm(g) - ref_norm) <= max(1e-2 * ref_norm, 2 * nfl), name
         atol = np.maximum(2e-2 * np.abs(ref).max(), 3 * np.abs(r32[idx] - ref)) + 1e-7
         assert np.all(np.abs(g[idx] - ref) <= atol), name
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+@pytest.mark.parametrize("tag", ["n2_188x220", "n1_204x252"])
+def test_trainer_step_non_square_vs_reference_fixture(tag, precision):
+    """A whole Trainer step (the bench's path: flat buffers, segmented plan
+    backward, fused SGD) at H != W against the reference-made fixture and the
+    fp64 oracle: logits, loss, every gradient, running statistics; then the
+    drop-in autograd module on the same batch must give the Trainer's loss and
+    gradients (same plan kernels: summation-order noise only).  bf16: the loss
+    within 1 % of the reference (gradients against the bf16 oracle:
+    tests/test_gpu_bf16.py), the drop-in comparison as in fp32."""
+    from unet_amd import WeightedCrossEntropyLoss
+    from unet_amd.train import Trainer
+    z = np.load(os.path.join(G, f"model_{tag}.npz"), allow_pickle=False)
+    seed, n, h, c, w = (int(z[k]) for k in ("x_seed", "n", "h", "c", "w"))
+    assert h != w
+    params = O.hash_init(c, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, c, h, w)
+    xd, td, wd = (torch.from_numpy(a).cuda() for a in (x, tgt, wmap))
+    b = make_model(params, c)
+    tr = Trainer(b, n, h, w, lr=1e-4, momentum=0.99, precision=precision)
+    assert tr.out_hw == (O.output_size(h), O.output_size(w))
+    lb = tr.forward_loss(xd, td, wd)
+    tr.backward_and_reduce(xd)
+    torch.cuda.synchronize()
+    lg = tr.logits.double().cpu().numpy()
+    names = [k for k, _ in b.named_parameters()]
+    got = {k: g.detach().double().cpu().numpy() for k, g in zip(names, tr.flat.grad_views)}
+    if precision == "fp32":
+        assert np.abs(lg - z["logits"]).max() <= 1e-3
+        assert abs(lb.item() - float(z["loss"])) <= 1e-4 * abs(float(z["loss"]))
+        net = O.UNetOracle(params)
+        rl, cache, nb = net.forward(x)
+        _, rdl = O.weighted_ce(rl, tgt, wmap)
+        worst = check_grads(got, net.backward(rdl, cache), fp32_noise_floor(params, x, tgt, wmap))
+        sd = b.state_dict()
+        for k in z.files:
+            if k.startswith("buf/"):
+                np.testing.assert_allclose(sd[k[4:]].cpu().numpy(), z[k], rtol=1e-4, atol=1e-5, err_msg=k)
+    else:  # the bf16 arithmetic against its oracle: tests/test_gpu_bf16.py (H != W cases there too)
+        assert abs(lb.item() - float(z["loss"])) <= 1e-2 * abs(float(z["loss"]))
+        worst = 0.0
+    # the drop-in autograd module, same weights and batch
+    a = make_model(params, c, precision=precision)
+    a.train()
+    la = WeightedCrossEntropyLoss()(a(xd), td, wd)
+    la.backward()
+    assert abs(la.item() - lb.item()) <= 1e-5 * abs(lb.item())
+    for nme, gv in zip(names, tr.flat.grad_views):
+        if O.bn_cancelled(nme):
+            continue
+        ga = dict(a.named_parameters())[nme].grad
+        assert float((ga - gv).abs().max()) <= 1e-4 * float(ga.abs().max()), nme
+    print(f"{tag} {precision}: worst gradient error / tolerance {worst:.2f}")
 
 
 @pytest.mark.parametrize("precision", PRECISIONS)

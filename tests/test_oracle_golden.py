@@ -102,12 +102,16 @@ def test_param_schema_matches_reference_counts():
     assert sum(1 for k in shapes if not O.is_buffer(k)) == 82
 
 
-@pytest.mark.parametrize("tag", ["n2_188", "n2_204"])
+@pytest.mark.parametrize("tag", ["n2_188", "n2_204", "n2_188x220", "n1_204x252"])
 def test_whole_model_vs_reference(tag):
+    """n2_188x220 / n1_204x252: H != W (the reference crops each axis on its
+    own, models/unet_model.py:93-100)."""
     z = _load(f"model_{tag}.npz")
     seed, n, h, c = int(z["x_seed"]), int(z["n"]), int(z["h"]), int(z["c"])
+    w = int(z["w"]) if "w" in z.files else h
     params = O.hash_init(c, 2, seed=seed, bn_random=True)
-    x, tgt, wmap = F.make_inputs(seed, n, c, h)
+    x, tgt, wmap = F.make_inputs(seed, n, c, h, w)
+    assert z["logits"].shape[2:] == (O.output_size(h), O.output_size(w))
     net = O.UNetOracle(params)
     logits, cache, nb = net.forward(x)
     np.testing.assert_allclose(logits, z["logits"], rtol=1e-9, atol=1e-10)

@@ -9,7 +9,7 @@ mkdir -p "$out"
 i=0
 for setting in "$@"; do
   i=$((i + 1))
-  env $setting timeout -k 10 200 python3 bench.py --dtype "$dt" --tune-db "$db" --extra-dtypes= --no-extras \
+  env $setting timeout -k 10 200 python3 bench.py --full-stdout --dtype "$dt" --tune-db "$db" --extra-dtypes= --no-extras \
     --no-cpu-baseline --no-iou --steps 5 --warmup 2 > "$out/ab$i.json" 2> "$out/ab$i.err" || { echo "failed: $setting"; exit 2; }
   python3 - "$out/ab$i.json" "$setting" <<'PY'
 import json, sys

@@ -1,6 +1,6 @@
 set -o pipefail
 o=gpurun_out/gab; mkdir -p $o
-B="python3 bench.py --extra-dtypes= --no-extras --no-cpu-baseline --no-iou --steps 20 --warmup 5"
+B="python3 bench.py --full-stdout --extra-dtypes= --no-extras --no-cpu-baseline --no-iou --steps 20 --warmup 5"
 for dt in bf16 fp32; do
   for g in "" "--graph" ""; do
     timeout -k 10 300 $B --dtype $dt $g > $o/b_${dt}${g}.json 2> $o/b_${dt}${g}.err || { echo fail $dt $g; exit 2; }

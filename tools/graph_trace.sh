@@ -7,7 +7,7 @@
 set -o pipefail
 o=${1:-gpurun_out/gtr}; dt=${2:-bf16}; mkdir -p $o
 export TMPDIR=/tmp
-B="bench.py --dtype $dt --extra-dtypes= --no-extras --no-cpu-baseline --no-iou --steps 8 --warmup 4"
+B="bench.py --full-stdout --dtype $dt --extra-dtypes= --no-extras --no-cpu-baseline --no-iou --steps 8 --warmup 4"
 for g in eager graph eager_serial graph_serial; do
   flag=""; case $g in graph*) flag="--graph";; esac
   conc=1; case $g in *serial) conc=0;; esac

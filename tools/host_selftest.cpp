@@ -57,8 +57,10 @@ static void test_plans() {
           unet_plan_destroy(p);
         }
   CHECK(unet_plan_create(1, 1, 100, 100, 2) == nullptr);  // too small
-  CHECK(unet_plan_create(1, 17, 512, 512, 2) == nullptr);  // c_in > 16
-  CHECK(unet_plan_create(1, 1, 512, 512, 33) == nullptr);  // n_classes > 32
+  CHECK(unet_plan_create(1, 4097, 512, 512, 2) == nullptr);  // c_in > 4096 (kMaxInChannels)
+  CHECK(unet_plan_create(1, 1, 512, 512, 4097) == nullptr);  // n_classes > 4096 (kMaxClassCount)
+  CHECK(unet_plan_create(1, 0, 512, 512, 2) == nullptr);
+  CHECK(unet_plan_create(1, 1, 512, 512, 0) == nullptr);
   if (unet_plan* q = unet_plan_create(1, 5, 188, 188, 5)) {  // 5 channels / 5 classes take a plan
     CHECK(unet_plan_num_params(q) == 136);
     unet_plan_destroy(q);

@@ -4,7 +4,7 @@
 set -o pipefail
 export TMPDIR=/tmp
 o=$1; mkdir -p $o
-B="bench.py --no-cpu-baseline --no-iou --no-extras --no-peaks --extra-dtypes= --steps 2 --warmup 1"
+B="bench.py --full-stdout --no-cpu-baseline --no-iou --no-extras --no-peaks --extra-dtypes= --steps 2 --warmup 1"
 C="GRBM_GUI_ACTIVE SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_VMEM SQ_WAIT_INST_LDS SQ_WAIT_ANY TA_TA_BUSY_sum"
 for dt in fp32 bf16; do
   timeout -s KILL 240 rocprofv3 --pmc $C -f csv -d $o/$dt -o run -- python3 $B --dtype $dt > $o/$dt.log 2>&1 || { echo $dt rc=$?; tail -5 $o/$dt.log; exit 3; }

@@ -20,7 +20,7 @@ for dt in $dts; do
   export UNET_TUNE_DB="$out/tune_$dt.db"
   rm -f "$UNET_TUNE_DB"
   echo "== tune $dt"
-  timeout -k 10 300 python3 bench.py --no-cpu-baseline --no-iou --no-extras --no-peaks --extra-dtypes= --steps 20 --warmup 5 $extra \
+  timeout -k 10 300 python3 bench.py --full-stdout --no-cpu-baseline --no-iou --no-extras --no-peaks --extra-dtypes= --steps 20 --warmup 5 $extra \
     > "$out/tuned_bench_$dt.json" 2> "$out/tuned_bench_$dt.err" || { echo "tune failed rc=$?"; exit 1; }
   bash tools/prof_bench.sh "$raw" $extra || exit 1
   sfx=""; [ "$dt" = bf16 ] && sfx="_bf16"
@@ -33,7 +33,7 @@ done
 [ "$do_trace" = 1 ] || { echo done; exit 0; }
 echo "== trace 50 steps"
 export UNET_TUNE_DB="$out/tune_fp32.db"
-timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$out/raw_tr" -o run -- python3 bench.py --steps 50 --warmup 10 --no-extras --no-peaks \
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -f csv -d "$out/raw_tr" -o run -- python3 bench.py --full-stdout --steps 50 --warmup 10 --no-extras --no-peaks \
   --no-cpu-baseline --no-iou --extra-dtypes= > "$out/tr_bench.json" 2> "$out/tr_bench.err" || { echo "trace failed rc=$?"; tail -5 "$out/tr_bench.err"; exit 1; }
 python3 tools/trace_check.py "$out/raw_tr" 10 50 "$out/tr_bench.json" > "$out/${tag}_trace_check.txt" || exit 1
 rm -rf "$out/raw_tr"

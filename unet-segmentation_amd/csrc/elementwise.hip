@@ -226,10 +226,10 @@ __global__ __launch_bounds__(256) void k_conv_first_wgrad(const float* __restric
 // dW[co][ci][3][3]).
 __global__ __launch_bounds__(256) void k_reduce_slabs(const float* __restrict__ slabs, int nslab, int n,
                                                       float* __restrict__ out, int rowlen, int rowstride,
-                                                      int rowoff) {
+                                                      int rowoff, int chunk) {
   const int w = blockIdx.x * 64 + (threadIdx.x & 63);
-  const int b0 = blockIdx.y * 64;
-  const int b1 = min(nslab, b0 + 64);
+  const int b0 = blockIdx.y * chunk;
+  const int b1 = min(nslab, b0 + chunk);
   float s = 0.f;
   if (w < n)
     for (int b = b0 + (threadIdx.x >> 6); b < b1; b += 4) s += slabs[(size_t)b * n + w];
@@ -419,8 +419,11 @@ size_t conv_first_wgrad_ws_bytes(int ci) { return sizeof(float) * (size_t)kFirst
 static hipError_t reduce_first_slabs(int cp, int ci_tot, int ci_off, int grid, float* dw, const float* slabs,
                                      hipStream_t s) {
   const int nw = cp * 9 * 64;
-  hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(nw, 64), cdiv(grid, 64)), dim3(256), 0, s, slabs, grid, nw, dw, cp * 9,
-                     ci_tot * 9, ci_off * 9);
+  // deterministic mode: one block per word group sums every slab (a single
+  // atomic per word onto the zeroed output: order-free); else 64-slab chunks
+  const int chunk = g_deterministic ? grid : 64;
+  hipLaunchKernelGGL(k_reduce_slabs, dim3(cdiv(nw, 64), cdiv(grid, chunk)), dim3(256), 0, s, slabs, grid, nw, dw,
+                     cp * 9, ci_tot * 9, ci_off * 9, chunk);
   return hipGetLastError();
 }
 
@@ -1041,7 +1044,7 @@ hipError_t launch_maxpool_bwd_fused(const float* dpool, const uint8_t* arg, cons
                                     int sh, int sw, const float* y, const float* scale, const float* shift,
                                     const float* mean, const float* invstd, int n, int h, int w, int c, float* dz,
                                     double* bstats, hipStream_t s, int y_h16, int g_h16) {
-  if (c % 4 || (256 % (c / 4)) != 0) return hipErrorInvalidValue;
+  if (c < 4 || c % 4 || (256 % (c / 4)) != 0) return hipErrorInvalidValue;
   const long long rows = (long long)n * ((h + 1) / 2);  // row pairs
   if ((long long)n * h * w >= (1LL << 31)) return hipErrorInvalidValue;
   const int ppb = 256 / (c / 4);
@@ -1928,14 +1931,14 @@ __global__ void k_affine_relu(const float* __restrict__ x, long long total4, int
 }
 
 hipError_t launch_channel_stats(const float* x, size_t pixels, int c, double* stats, hipStream_t s) {
-  if (c % 4 || 256 % (c / 4)) return hipErrorInvalidValue;
+  if (c < 4 || c % 4 || 256 % (c / 4)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_channel_stats, dim3(grid_cap((long long)pixels, 256 / (c / 4) * 4, 2048)), dim3(256), 0, s, x,
                      (long long)pixels, c, stats);
   return hipGetLastError();
 }
 hipError_t launch_bn_bwd_stats(const float* dy, const float* x, const float* mean, const float* invstd, size_t pixels,
                                int c, double* bstats, hipStream_t s) {
-  if (c % 4 || 256 % (c / 4)) return hipErrorInvalidValue;
+  if (c < 4 || c % 4 || 256 % (c / 4)) return hipErrorInvalidValue;
   hipLaunchKernelGGL(k_bn_bwd_stats, dim3(grid_cap((long long)pixels, 256 / (c / 4) * 4, 2048)), dim3(256), 0, s, dy,
                      x, mean, invstd, (long long)pixels, c, bstats);
   return hipGetLastError();

@@ -394,7 +394,7 @@ size_t unet_bn_relu_ws_bytes(int n, int h, int w, int c) {
 int unet_bn_relu_fwd(const float* x, int n, int h, int w, int c, const float* gamma, const float* beta, float* rm,
                      float* rv, int64_t* nbt, float momentum, float eps, int training, int relu, float* y,
                      float* save_mean, float* save_invstd, void* ws, unet_stream_t st) {
-  if (!x || !y || !gamma || !beta || !save_mean || !save_invstd || c % 4 || 256 % (c / 4) || n < 1) return -EINVAL;
+  if (!x || !y || !gamma || !beta || !save_mean || !save_invstd || c < 4 || c % 4 || 256 % (c / 4) || n < 1) return -EINVAL;
   if (!training && (!rm || !rv)) return -EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(st);
   char* p = reinterpret_cast<char*>(ws);
@@ -420,7 +420,7 @@ int unet_bn_relu_fwd(const float* x, int n, int h, int w, int c, const float* ga
 int unet_bn_relu_bwd(const float* x, const float* y, const float* dy, int n, int h, int w, int c, const float* gamma,
                      const float* save_mean, const float* save_invstd, int training, int relu, float* dx,
                      float* dgamma, float* dbeta, void* ws, unet_stream_t st) {
-  if (!x || !dy || !dx || !gamma || c % 4 || 256 % (c / 4) || n < 1 || (relu && !y)) return -EINVAL;
+  if (!x || !dy || !dx || !gamma || c < 4 || c % 4 || 256 % (c / 4) || n < 1 || (relu && !y)) return -EINVAL;
   hipStream_t s = reinterpret_cast<hipStream_t>(st);
   char* p = reinterpret_cast<char*>(ws);
   double* stats = reinterpret_cast<double*>(p);
@@ -544,7 +544,8 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "wino4_fwd_min_cg") g_wino4_fwd_min_cg = value;
   else if (k == "wino4_fwd_small_cg") g_wino4_fwd_small_cg = value;
   else if (k == "op_a16") g_op_a16 = value != 0;
-  else if (k == "maxpool_vec8") g_maxpool_vec8 = value;  // 0: bf16 plans pool with the 4-channel kernel (A/B tests)
+  else if (k == "maxpool_vec8") g_maxpool_vec8 = value;
+  else if (k == "deterministic") g_deterministic = value != 0;  // 0: bf16 plans pool with the 4-channel kernel (A/B tests)
   else if (k == "op_precision") {
     if (value != UNET_PREC_FP32 && value != UNET_PREC_BF16 && value != UNET_PREC_BF16X3) return -EINVAL;
     g_op_prec = value;

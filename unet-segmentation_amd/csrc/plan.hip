@@ -50,6 +50,16 @@ int g_bn_fold = getenv("UNET_BN_FOLD") ? atoi(getenv("UNET_BN_FOLD")) : 1;
 // runs split-K k and/or tile id where they apply (tests)
 int g_force_split = 0;
 int g_force_tile = 0;
+// unet_set_tuning("deterministic", 1) or UNET_DETERMINISTIC=1 (default off):
+// every weight gradient runs a variant without fp32 atomics (slab partials
+// summed in a fixed order, or one split storing straight into the gradient),
+// and inc.c0's slab reduction sums every slab in one pass, so two runs of a
+// step give bit-identical results whatever the stream timing (the analogue of
+// torch.use_deterministic_algorithms).  The autotuner then times only those
+// variants (their own tuning keys); a site with none counts in
+// unet_nondeterministic_sites().
+int g_deterministic = getenv("UNET_DETERMINISTIC") ? atoi(getenv("UNET_DETERMINISTIC")) : 0;
+std::atomic<long long> g_nondet_sites{0};
 }  // namespace unet
 
 namespace {
@@ -314,11 +324,23 @@ std::string igemm_key(const IgemmArgs& a) {
 
 std::string wgrad_key(const WgradArgs& a) {
   char b[240];
-  snprintf(b, sizeof b, "wgrad%s Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d wino=%d tt=%d",
+  snprintf(b, sizeof b, "wgrad%s Mo=%d No=%d P=%d Cg=%d taps=%dx%d s=%d grid=%dx%d wino=%d%s tt=%d",
            a.split ? "_bf16x3" : a.bf16 ? "_bf16" : "", a.Mo,
            a.No, a.P, a.gb.Cg, a.gb.taps_h, a.gb.taps_w, a.gb.stride, a.gb.Hg, a.gb.Wg, unet::g_wino_wgrad_max,
-           kTileTableVersion);
+           unet::g_deterministic ? " det" : "", kTileTableVersion);
   return b;
+}
+
+// a weight-gradient variant that adds no fp32 atomics: slab modes (ring per_cu
+// codes 11 / 12, pixel-column codes 101-104, Winograd codes >= 1000: split
+// partials by plain stores, summed by k_wr_reduce in a fixed order; one split
+// stores straight into the gradient).  A slab launch whose partials exceed
+// the plan's slab falls back to atomics and counts in unet_slab_fallbacks().
+bool wgrad_choice_deterministic(const GemmChoice& g) {
+  if (g.tile == 71 || g.tile == 74) return g.split >= 1000;
+  if (g.tile >= 26 && g.tile <= 33) return g.split >= 10;
+  if (g.tile >= 0 && g.tile <= 14) return g.split >= 100;
+  return false;
 }
 
 // UNET_TUNE_SKIP="73,74": tile ids the autotuner never tries (A/B experiments
@@ -493,7 +515,13 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
 }
 
 GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
-  if (!env_autotune()) return GemmChoice{};
+  const bool det = unet::g_deterministic != 0;
+  if (!env_autotune() && !det) return GemmChoice{};
+  if (det && !env_autotune()) {  // untimed: the first atomic-free candidate
+    for (const GemmChoice& g : wgrad_candidates(a))
+      if (wgrad_choice_deterministic(g)) return g;
+    return GemmChoice{};
+  }
   const std::string key = wgrad_key(a);
   std::lock_guard<std::mutex> lk(g_tune_mu);
   tune_db_load_once();
@@ -507,13 +535,15 @@ GemmChoice choose_wgrad(const Ctx& c, const WgradArgs& a) {
   if (capturing(c.s)) return GemmChoice{};
   WgradArgs t = a;
   t.out = c.f(c.p->tune_scratch);
-  const float th = time_launch(c.s, [&] { return launch_wgrad(t, c.s); });
+  // deterministic mode: the heuristic (atomics) is no candidate
+  const float th = det ? -1.f : time_launch(c.s, [&] { return launch_wgrad(t, c.s); });
   GemmChoice best{};
   float tb = th;
   std::string log = key + " | heuristic " + std::to_string(th * 1e3f) + " us";
   static const bool verbose = getenv("UNET_TUNE_VERBOSE") != nullptr;
   std::string all;
   for (const GemmChoice& g : wgrad_candidates(a)) {
+    if (det && !wgrad_choice_deterministic(g)) continue;
     const float tm = time_launch(c.s, [&] { return launch_wgrad_v(t, c.s, g); });
     if (verbose) all += " " + std::to_string(g.tile) + "/" + std::to_string(g.split) + ":" + std::to_string((int)(tm * 1e3f));
     if (tm > 0.f && (tb < 0.f || tm < tb)) {
@@ -562,6 +592,7 @@ hipError_t run_wgrad(const Ctx& c, WgradArgs a) {
     a.slab_bytes = c.p->wslab.bytes;
   }
   const GemmChoice ch = choose_wgrad(c, a);
+  if (unet::g_deterministic && !wgrad_choice_deterministic(ch)) ++unet::g_nondet_sites;
   if (c.p->timing) c.p->xfl += wgrad_exec_flops(a, ch);
   return launch_wgrad_v(a, c.s, ch);
 }
@@ -1392,6 +1423,10 @@ size_t unet_tuning_report(char* buf, size_t len) {
     buf[k] = 0;
   }
   return r.size() + 1;
+}
+
+long long unet_nondeterministic_sites(int reset) {
+  return reset ? g_nondet_sites.exchange(0) : g_nondet_sites.load();
 }
 
 long long unet_slab_fallbacks(int reset) {

@@ -111,6 +111,10 @@ struct IgemmArgs {
 // slab-mode weight gradients that ran with atomics instead (the plan's wslab
 // too small for their split partials); unet_slab_fallbacks() reads it
 extern std::atomic<long long> g_slab_fallbacks;
+// deterministic mode (unet_set_tuning("deterministic", 1), plan.hip): no fp32
+// atomics in any weight gradient; sites that had no such variant are counted
+extern int g_deterministic;
+extern std::atomic<long long> g_nondet_sites;
 
 struct WgradArgs {
   // C[i][j] = sum_p A_p[i] * B_p[j] over the pixels p of the grid of `ga`.

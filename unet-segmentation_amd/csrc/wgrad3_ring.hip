@@ -536,6 +536,8 @@ static hipError_t go_wr(const WgradArgs& a0, hipStream_t s, int per_cu) {
   const size_t plane = (size_t)a.Mo * a.No;
   const bool use_slab = slab_mode && a.slab && !a.accumulate && (size_t)splits * plane * sizeof(float) <= a.slab_bytes &&
                         splits > 1 && plane % 4 == 0;
+  // (a single split adds each element once onto the zeroed gradient: order-free)
+  if (slab_mode && splits > 1 && !use_slab) ++g_slab_fallbacks;
   if (!use_slab) a.slab = nullptr;
   const dim3 grid(a.Mo / BCO, g.Cg / BCI, splits);
   // X transform per launch: the sources of the two concat halves may differ

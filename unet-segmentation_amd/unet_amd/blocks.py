@@ -23,7 +23,9 @@ tensor raises.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
+import threading
 
 import torch
 
@@ -38,6 +40,50 @@ def _lib_and_stream(t):
     if t.dtype != torch.float32:
         raise RuntimeError(f"the MI355X UNet blocks compute in float32, got {t.dtype}")
     return _lib.load(), _lib.stream_of(t.device)
+
+
+# GEMM precision of the block ops.  Inside torch.autocast("cuda", bfloat16) the
+# reference's convs run on bf16 operands with fp32 accumulation (and return
+# bf16); the blocks then run their conv / convT GEMMs the same way
+# (op_precision UNET_PREC_BF16: operands rounded to bf16 at staging, fp32
+# accumulation), in the backward too (its ops inherit the forward's precision,
+# as autocast's bf16 saved tensors make the reference's backward bf16).
+# op_precision is process-wide in the library: it is set around each call
+# under a lock and put back to fp32.
+_PREC_LOCK = threading.Lock()
+_PREC_BF16 = 1  # UNET_PREC_BF16 (include/unet_hip.h)
+
+
+def _autocast_bf16():
+    return torch.is_autocast_enabled("cuda") and torch.get_autocast_dtype("cuda") == torch.bfloat16
+
+
+@contextlib.contextmanager
+def _gemm_precision(lib, bf16):
+    if not bf16:
+        yield
+        return
+    with _PREC_LOCK:
+        _lib.check(lib.unet_set_tuning(b"op_precision", _PREC_BF16), "unet_set_tuning")
+        try:
+            yield
+        finally:
+            lib.unet_set_tuning(b"op_precision", 0)
+
+
+def _block_in(x):
+    """A block's input as the kernels read it: float32 (a bf16 / fp16 tensor
+    from an autocast region is widened -- exact -- outside the autograd
+    Functions, so its gradient comes back in its own dtype)."""
+    if x.is_floating_point() and x.dtype != torch.float32 and _autocast_bf16():
+        return x.float()
+    return x
+
+
+def _block_out(y):
+    """Under bf16 autocast the reference's blocks return bf16 (their last op is a
+    conv, or a BatchNorm / ReLU of one, on bf16 operands)."""
+    return y.to(torch.bfloat16) if _autocast_bf16() else y
 
 
 def _cl(t):
@@ -90,16 +136,18 @@ class _Conv3x3(torch.autograd.Function):
     """nn.Conv2d(k=3, padding=0) (models/unet_model.py:11, 15) as implicit GEMM."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, bf16=False):
         lib, st = _lib_and_stream(x)
         x = _cl(x)
         n, ci, h, wd = x.shape
         co = w.shape[0]
         y = _nhwc(n, co, h - 2, wd - 2, x)
         ws = _ws(lib.unet_conv_ws_bytes(n, h, wd, ci, co), x)
-        _lib.check(lib.unet_conv3x3_fwd(_p(x), n, h, wd, ci, _p(w.contiguous()), _p(b.contiguous()), co, None, None,
-                                        _p(y), _p(ws), st), "unet_conv3x3_fwd")
+        with _gemm_precision(lib, bf16):
+            _lib.check(lib.unet_conv3x3_fwd(_p(x), n, h, wd, ci, _p(w.contiguous()), _p(b.contiguous()), co, None,
+                                            None, _p(y), _p(ws), st), "unet_conv3x3_fwd")
         ctx.save_for_backward(x, w)
+        ctx.bf16 = bf16
         return y
 
     @staticmethod
@@ -111,15 +159,16 @@ class _Conv3x3(torch.autograd.Function):
         co = w.shape[0]
         ws = _ws(lib.unet_conv_ws_bytes(n, h, wd, ci, co), x)
         dx = None
-        if ctx.needs_input_grad[0]:
-            dx = _nhwc(n, ci, h, wd, x)
-            _lib.check(lib.unet_conv3x3_dgrad(_p(dy), n, h, wd, ci, _p(w.contiguous()), co, _p(dx), _p(ws), st),
-                       "unet_conv3x3_dgrad")
-        dw = torch.empty_like(w)
-        db = torch.empty(co, dtype=torch.float32, device=x.device)
-        _lib.check(lib.unet_conv3x3_wgrad(_p(x), _p(dy), n, h, wd, ci, co, _p(dw), _p(db), _p(ws), st),
-                   "unet_conv3x3_wgrad")
-        return dx, dw, db
+        with _gemm_precision(lib, ctx.bf16):
+            if ctx.needs_input_grad[0]:
+                dx = _nhwc(n, ci, h, wd, x)
+                _lib.check(lib.unet_conv3x3_dgrad(_p(dy), n, h, wd, ci, _p(w.contiguous()), co, _p(dx), _p(ws), st),
+                           "unet_conv3x3_dgrad")
+            dw = torch.empty_like(w)
+            db = torch.empty(co, dtype=torch.float32, device=x.device)
+            _lib.check(lib.unet_conv3x3_wgrad(_p(x), _p(dy), n, h, wd, ci, co, _p(dw), _p(db), _p(ws), st),
+                       "unet_conv3x3_wgrad")
+        return dx, dw, db, None
 
 
 class _BNReLU(torch.autograd.Function):
@@ -189,16 +238,18 @@ class _ConvT2(torch.autograd.Function):
     """nn.ConvTranspose2d(k=2, s=2) (models/unet_model.py:45)."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, bf16=False):
         lib, st = _lib_and_stream(x)
         x = _cl(x)
         n, ci, h, wd = x.shape
         co = w.shape[1]
         y = _nhwc(n, co, 2 * h, 2 * wd, x)
         ws = _ws(lib.unet_conv_ws_bytes(n, h, wd, ci, co), x)
-        _lib.check(lib.unet_convT2_fwd(_p(x), n, h, wd, ci, _p(w.contiguous()), _p(b.contiguous()), co, _p(y),
-                                       _p(ws), st), "unet_convT2_fwd")
+        with _gemm_precision(lib, bf16):
+            _lib.check(lib.unet_convT2_fwd(_p(x), n, h, wd, ci, _p(w.contiguous()), _p(b.contiguous()), co, _p(y),
+                                           _p(ws), st), "unet_convT2_fwd")
         ctx.save_for_backward(x, w)
+        ctx.bf16 = bf16
         return y
 
     @staticmethod
@@ -212,9 +263,10 @@ class _ConvT2(torch.autograd.Function):
         dw = torch.empty_like(w)
         db = torch.empty(co, dtype=torch.float32, device=x.device)
         ws = _ws(lib.unet_conv_ws_bytes(n, h, wd, ci, co), x)
-        _lib.check(lib.unet_convT2_bwd(_p(x), _p(dy), n, h, wd, ci, _p(w.contiguous()), co, _p(dx), _p(dw), _p(db),
-                                       _p(ws), st), "unet_convT2_bwd")
-        return dx, dw, db
+        with _gemm_precision(lib, ctx.bf16):
+            _lib.check(lib.unet_convT2_bwd(_p(x), _p(dy), n, h, wd, ci, _p(w.contiguous()), co, _p(dx), _p(dw),
+                                           _p(db), _p(ws), st), "unet_convT2_bwd")
+        return dx, dw, db, None
 
 
 class _Conv1x1(torch.autograd.Function):
@@ -260,7 +312,7 @@ def conv3x3(conv, x):
         return _FirstConv.apply(x, conv.weight, conv.bias)
     if co % 64:
         raise ValueError(f"3x3 conv {ci}->{co}: output channels must be a multiple of 64")
-    return _Conv3x3.apply(x, conv.weight, conv.bias)
+    return _Conv3x3.apply(x, conv.weight, conv.bias, _autocast_bf16())
 
 
 def bn_relu(bn, x):
@@ -272,44 +324,53 @@ def bn_relu(bn, x):
                          bn.training, float(bn.momentum), float(bn.eps))
 
 
-def double_conv(m, x):
-    """DoubleConv.forward (models/unet_model.py:20-21)."""
+def _double_conv(m, x):
     seq = m.double_conv
     return bn_relu(seq[4], conv3x3(seq[3], bn_relu(seq[1], conv3x3(seq[0], x))))
 
 
+def _up_conv(m, x):
+    return _ConvT2.apply(x, m.up.weight, m.up.bias, _autocast_bf16())
+
+
+def double_conv(m, x):
+    """DoubleConv.forward (models/unet_model.py:20-21)."""
+    return _block_out(_double_conv(m, _block_in(x)))
+
+
 def down(m, x):
     """Down.forward (models/unet_model.py:32-33): MaxPool2d(2) then DoubleConv."""
-    return double_conv(m.maxpool_conv[1], _MaxPool2.apply(x))
+    return _block_out(_double_conv(m.maxpool_conv[1], _MaxPool2.apply(_block_in(x))))
 
 
 def up_conv(m, x):
     """The Up block's ConvTranspose2d(k=2, s=2) (models/unet_model.py:45, 51)."""
-    return _ConvT2.apply(x, m.up.weight, m.up.bias)
+    return _block_out(_up_conv(m, _block_in(x)))
 
 
 def up(m, x1, x2_cropped):
     """Up.forward (models/unet_model.py:50-54): upsample x1, concatenate
     [x2_cropped, x1] along channels (skip first), DoubleConv."""
-    x1 = up_conv(m, x1)
-    return double_conv(m.conv, torch.cat([_cl(x2_cropped), x1], dim=1))
+    x1 = _up_conv(m, _block_in(x1))
+    return _block_out(_double_conv(m.conv, torch.cat([_cl(_block_in(x2_cropped)), x1], dim=1)))
 
 
 def out_conv(m, x):
     """OutConv.forward (models/unet_model.py:62-63)."""
-    return _Conv1x1.apply(x, m.conv.weight, m.conv.bias)
+    return _block_out(_Conv1x1.apply(_block_in(x), m.conv.weight, m.conv.bias))
 
 
 def unet_forward(model, x):
     """UNet.forward (models/unet_model.py:105-146) op by op on these blocks."""
-    x1 = double_conv(model.inc, x)
-    x2 = down(model.down1, x1)
-    x3 = down(model.down2, x2)
-    x4 = down(model.down3, x3)
-    x5 = down(model.down4, x4)
+    x1 = _double_conv(model.inc, _block_in(x))
+    x2 = _double_conv(model.down1.maxpool_conv[1], _MaxPool2.apply(x1))
+    x3 = _double_conv(model.down2.maxpool_conv[1], _MaxPool2.apply(x2))
+    x4 = _double_conv(model.down3.maxpool_conv[1], _MaxPool2.apply(x3))
+    x5 = _double_conv(model.down4.maxpool_conv[1], _MaxPool2.apply(x4))
     x = x5
     for blk, skip in ((model.up1, x4), (model.up2, x3), (model.up3, x2), (model.up4, x1)):
-        x_up = up_conv(blk, x)
+        x_up = _up_conv(blk, x)
         crop = model._center_crop(skip, x_up.size()[2:])
-        x = double_conv(blk.conv, torch.cat([_cl(crop), x_up], dim=1))
-    return out_conv(model.outc, x)
+        x = _double_conv(blk.conv, torch.cat([_cl(crop), x_up], dim=1))
+    # fp32 logits, as the plan's UNet.forward returns them in every precision
+    return _Conv1x1.apply(x, model.outc.conv.weight, model.outc.conv.bias)

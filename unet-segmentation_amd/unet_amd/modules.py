@@ -132,6 +132,23 @@ def _check_tensor(t, name):
         raise RuntimeError(f"{name} must be contiguous")
 
 
+def _as_input(x):
+    """The reference's UNet.forward (models/unet_model.py:105) takes any strided
+    float32 tensor -- channels_last, sliced, transposed views -- and, inside a
+    cuda autocast region, any floating dtype (the convs cast it).  The plan reads
+    contiguous NCHW fp32: other layouts are copied (autograd routes the input
+    gradient back through the copy); other dtypes raise outside autocast, as
+    the reference's first conv does."""
+    if not x.is_cuda:
+        raise RuntimeError("input must be on a HIP device (the MI355X UNet has no CPU path)")
+    if x.dtype != torch.float32:
+        if x.is_floating_point() and torch.is_autocast_enabled("cuda"):
+            x = x.float()
+        else:
+            raise RuntimeError(f"Input type ({x.dtype}) and weight type (torch.float32) should be the same")
+    return x if x.is_contiguous() else x.contiguous()
+
+
 class _UNetFunction(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, module, train, precision, *params):
@@ -156,22 +173,24 @@ class _UNetFunction(torch.autograd.Function):
         tab = _lib.ptr_array([t for _, t in state])
         plan.forward(tab, x, logits, ws, train)
         ctx.plan, ctx.ws, ctx.tab, ctx.train, ctx.need_bwd = plan, ws, tab, train, need_bwd
-        ctx.params = params
         ctx.module = module if not train else None
-        ctx.save_for_backward(x)
+        # the parameters are saved like autograd saves a conv's weight: an
+        # in-place update between this forward and the backward (an optimizer
+        # step) raises at the backward instead of differentiating other weights
+        ctx.save_for_backward(x, *params)
         return logits
 
     @staticmethod
     def backward(ctx, dlogits):
+        x, *params = ctx.saved_tensors  # raises if a parameter was modified in place since the forward
         if not ctx.train:
-            dx, *grads = _eval_backward(ctx.module, ctx.saved_tensors[0], dlogits, ctx.params, ctx.needs_input_grad[0])
+            dx, *grads = _eval_backward(ctx.module, x, dlogits, params, ctx.needs_input_grad[0])
             return (dx, None, None, None, *grads)
         if not ctx.need_bwd or ctx.ws is None:
             raise RuntimeError("the MI355X UNet backward needs the workspace of a forward that recorded autograd "
                                "(and it runs once per forward: use retain_graph=False)")
-        (x,) = ctx.saved_tensors
         dlogits = dlogits.contiguous()
-        grads = [torch.empty_like(p) for p in ctx.params]
+        grads = [torch.empty_like(p) for p in params]
         ctx.plan.backward(ctx.tab, _lib.ptr_array(grads), x, dlogits, ctx.ws)
         ctx.ws = None
         return (None, None, None, None, *grads)
@@ -187,7 +206,16 @@ def _eval_backward(module, x, dlogits, params, need_x):
     with torch.enable_grad():
         xr = x.detach().requires_grad_(need_x)
         leaves = {k: p.detach().requires_grad_(True) for k, p in zip(names, params)}
-        out = torch.func.functional_call(module, leaves, (xr,), {"_ops": True}, strict=False)
+        # the forward that produced the logits ran in eval mode: so does the
+        # recompute, whatever mode the module is in by now (a model.train()
+        # between forward and backward must neither switch BatchNorm to batch
+        # statistics nor update the running statistics here)
+        was_training = module.training
+        module.eval()
+        try:
+            out = torch.func.functional_call(module, leaves, (xr,), {"_ops": True}, strict=False)
+        finally:
+            module.train(was_training)
         inputs = ([xr] if need_x else []) + list(leaves.values())
         grads = torch.autograd.grad(out, inputs, dlogits, allow_unused=True)
     dx = grads[0] if need_x else None
@@ -239,7 +267,7 @@ class UNet(nn.Module):
         return list(self.state_dict(keep_vars=True).items())
 
     def forward(self, x, _ops=False):
-        _check_tensor(x, "input")
+        x = _as_input(x)
         if x.dim() != 4 or x.shape[1] != self.n_channels:
             raise ValueError(f"expected input (N, {self.n_channels}, H, W), got {tuple(x.shape)}")
         if _ops:

@@ -76,6 +76,7 @@ class FlatBuffers:
         bufs = [b for b in module.buffers() if b.is_floating_point()]
         total = sum(b.numel() for b in bufs)
         self.flat = torch.zeros(total, dtype=torch.float32, device=bufs[0].device) if bufs else None
+        self.bufs = bufs
         o = 0
         with torch.no_grad():
             for b in bufs:
@@ -83,6 +84,14 @@ class FlatBuffers:
                 view.copy_(b.data)
                 b.data = view
                 o += b.numel()
+
+    def version(self):
+        """A counter that moves whenever torch writes the buffers: through the
+        module's buffer tensors (load_state_dict, reset_running_stats, copy_;
+        ``b.data = view`` gave each its own version counter) or through the
+        flat tensor.  The plan's HIP kernels bump none of them (the running
+        statistics update of a forward is not a rewrite)."""
+        return (self.flat._version if self.flat is not None else 0) + sum(b._version for b in self.bufs)
 
 
 class Trainer:
@@ -135,6 +144,7 @@ class Trainer:
         self._bcast_stage = None
         self._bcast_work = None
         self._bcast_version = None
+        self._warned_rewrite = False
         self.lib = _lib.load()
         buckets = [self.flat.range_for(*self.plan.segment_grads(s)) for s in range(N_SEGMENTS)]
         # gradient all-reduce dtype: fp32 (DDP semantics) unless the caller asks
@@ -235,7 +245,7 @@ class Trainer:
                 self._bcast_stage = torch.empty_like(bufs)
             self._bcast_stage.copy_(bufs)
             self._bcast_work = torch.distributed.broadcast(self._bcast_stage, 0, group=self.pg, async_op=True)
-            self._bcast_version = bufs._version
+            self._bcast_version = self.flat_buffers.version()
         self.backward_and_reduce(x)
         self.optimizer_step()
         self._eager_steps += 1
@@ -245,17 +255,37 @@ class Trainer:
         return loss
 
     def _apply_buffer_broadcast(self, bufs):
-        """DDP's start-of-step buffer broadcast: the staged copy of rank 0's
-        statistics from the previous step's forward, or -- first step, or the
-        buffers were rewritten through torch since (load_state_dict, ...) -- a
-        broadcast now."""
+        """DDP's start-of-step buffer broadcast: every rank starts the step from
+        rank 0's running statistics.  Deferred form: the staged copy of rank 0's
+        statistics as its previous forward left them (broadcast beside that
+        step's backward).  Rank 0 keeps its own buffers -- they ARE rank 0's
+        statistics, and so include any rewrite made since the staging
+        (load_state_dict, reset_running_stats) -- every other rank takes the
+        staged copy, overwriting anything it changed locally, as DDP does.
+
+        Every rank issues the same collectives whatever happened locally (the
+        round-5 fallback broadcast was a rank-local decision and could pair
+        mismatched collectives).  The one case the staged copy
+        cannot cover is a rewrite on rank 0 after the staging: the other ranks
+        then start one step from rank 0's previous values (their batch
+        statistics, gradients and weights are unaffected -- BatchNorm trains on
+        batch statistics -- and the next step's broadcast brings rank 0's
+        rewritten values).  Rank 0 warns once; ``sync_buffers()`` on every rank
+        after such a rewrite gives DDP's values at once.  The first step (no
+        staged copy) broadcasts synchronously on every rank."""
         work, self._bcast_work = self._bcast_work, None
-        if work is not None:
-            work.wait()  # NCCL: the current stream waits; gloo: the host does
-            if bufs._version == self._bcast_version:
-                bufs.copy_(self._bcast_stage)
-                return
-        torch.distributed.broadcast(bufs, 0, group=self.pg)
+        if work is None:
+            torch.distributed.broadcast(bufs, 0, group=self.pg)
+            return
+        work.wait()  # NCCL: the current stream waits; gloo: the host does
+        if torch.distributed.get_rank(self.pg) != 0:
+            bufs.copy_(self._bcast_stage)
+        elif self.flat_buffers.version() != self._bcast_version and not self._warned_rewrite:
+            self._warned_rewrite = True
+            import warnings
+            warnings.warn("BatchNorm running statistics were rewritten on rank 0 between Trainer steps: the other "
+                          "ranks start this step from the previous broadcast; call Trainer.sync_buffers() on every "
+                          "rank after such a change for DDP's values at once", RuntimeWarning, stacklevel=3)
 
     def check_targets(self):
         """Wait for every step issued so far and raise IndexError if any of them
