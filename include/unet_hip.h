@@ -117,6 +117,15 @@ int unet_plan_segment_grads(const unet_plan* p, int seg, int* first_grad, int* n
 int unet_plan_backward(unet_plan* p, void* const* host_params, void* const* host_grads,
                        const float* x_nchw, const float* dlogits_nchw, void* workspace,
                        int seg_begin, int seg_end, unet_stream_t stream);
+/* Gradient of the network input (the reference's x.grad when the input
+ * requires grad; models/unet_model.py:105): after the backward segment that
+ * holds inc.c0 (segment 8, i.e. a whole backward), materialises inc.c0's
+ * BatchNorm-backward output into `scratch` (fp32,
+ * unet_plan_input_grad_scratch_bytes) and writes dx (N, C, H, W) fp32.  Same
+ * stream as the backward. */
+size_t unet_plan_input_grad_scratch_bytes(const unet_plan* p);
+int unet_plan_input_grad(unet_plan* p, void* const* params, float* dx, void* workspace, void* scratch,
+                         unet_stream_t stream);
 /* The same with flags.  UNET_BWD_DEFER_JOIN: the weight gradients of these
  * segments (which run on the plan's side stream beside the input-gradient
  * chain once the plan is tuned) are NOT joined into `stream` on return, so the

@@ -439,17 +439,44 @@ def gemm_mode(request, lib):
                                        "heuristic+wtile31", "heuristic+wtile32", "heuristic+wtile33",
                                        "norm+heuristic+wtile26", "tile91", "tile92", "tile93", "tile94",
                                        "tile95", "tile96", "tile97", "tile98", "tile99", "tile92+split2",
-                                       "tile95+split3", "tile96+split2"],
+                                       "tile95+split3", "tile96+split2",
+                                       "heuristic+wtile140", "heuristic+wtile141", "heuristic+wtile142",
+                                       "heuristic+wtile143", "heuristic+wtile144", "heuristic+wtile40",
+                                       "heuristic+wtile43"],
                          indirect=True)
 def test_bf16_gemm_variants_vs_bf16_oracle(gemm_mode):
     """Every bf16 tile (21-26 row gather, 31-36 halo-tiled 3x3, 63-67 LDS-DMA
     halo, 81-84 LDS-DMA halo / weight rings -- the convT GEMMs fall back to the
     built-in tile there; 91-95 the convT forward / input-gradient K rings --
     the 3x3 GEMMs fall back there) and split-K on every conv / convT / dgrad
-    GEMM of a train step; the weight gradients run the bf16 wgrad tiles."""
+    GEMM of a train step; the weight gradients run the bf16 wgrad tiles
+    (wtile140-144: the convT weight-gradient ring tiles 40-44 in slab mode on
+    every convT layer they fit; wtile40 / 43: the same with fp32 atomics)."""
     params = O.hash_init(1, 2, seed=21, bn_random=True)
     x, tgt, wmap = F.make_inputs(21, 2, 1, 188)
     check_vs_bf16_oracle(make_model(params), params, x, tgt, wmap, gemm_mode)
+
+
+@pytest.mark.parametrize("wtile", [140, 141, 142, 143, 144])
+@pytest.mark.parametrize("n,h,w,seed", [(2, 204, 204, 22), (1, 220, 252, 23), (3, 196, 196, 24)])
+def test_bf16_convT_wgrad_ring_vs_bf16_oracle(wtile, n, h, w, seed):
+    """The convT weight-gradient ring (wgradT_ring.hip, tiles 40-44 in slab
+    mode) on every convT layer of a whole train step where it fits, at sizes
+    whose pixel counts leave ragged last stages and splits (the zeroed tail
+    rows), an H != W batch and an odd batch."""
+    from unet_amd import _lib
+    lib = _lib.load()
+    lib.unet_tuning_reset()
+    lib.unet_set_tuning(b"autotune", 0)
+    lib.unet_set_tuning(b"wgrad_variant", wtile)
+    try:
+        params = O.hash_init(1, 2, seed=seed, bn_random=True)
+        x, tgt, wmap = F.make_inputs(seed, n, 1, h, w)
+        check_vs_bf16_oracle(make_model(params), params, x, tgt, wmap, f"wtile{wtile} {n}x{h}x{w}")
+    finally:
+        lib.unet_set_tuning(b"wgrad_variant", -1)
+        lib.unet_set_tuning(b"autotune", 1)
+        lib.unet_tuning_reset()
 
 
 def test_bf16_3ch_572_forward_vs_fp32_fixture(lib):

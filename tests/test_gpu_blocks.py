@@ -204,17 +204,21 @@ def test_forward_takes_strided_inputs():
         else:
             xi = big[..., 5:193]
         assert kind == "contiguous" or not xi.is_contiguous()
-        xi = xi.detach().requires_grad_(True)
-        m.zero_grad(set_to_none=True)
-        loss = WeightedCrossEntropyLoss()(m(xi), t, w)
-        loss.backward()
-        res[kind] = (loss.item(), xi.grad.detach().cpu().numpy(),
-                     m.outc.conv.weight.grad.detach().cpu().numpy())
+        out = []
+        for mode in ("train", "eval"):
+            m.train(mode == "train")
+            xr = xi.detach().requires_grad_(True)
+            m.zero_grad(set_to_none=True)
+            loss = WeightedCrossEntropyLoss()(m(xr), t, w)
+            loss.backward()
+            out += [loss.item(), xr.grad.detach().cpu().numpy(), m.inc.double_conv[0].weight.grad.detach().cpu().numpy()]
+        res[kind] = out
     for kind in ("transposed", "slice"):
         a, b = res[kind], res["contiguous"]
-        assert abs(a[0] - b[0]) <= 1e-6 * abs(b[0]), kind
-        np.testing.assert_allclose(a[1], b[1], rtol=0, atol=1e-4 * np.abs(b[1]).max(), err_msg=kind)
-        np.testing.assert_allclose(a[2], b[2], rtol=0, atol=1e-4 * np.abs(b[2]).max(), err_msg=kind)
+        for i in range(0, len(a), 3):
+            assert abs(a[i] - b[i]) <= 1e-6 * abs(b[i]), kind
+            for k in (i + 1, i + 2):
+                np.testing.assert_allclose(a[k], b[k], rtol=0, atol=1e-4 * np.abs(b[k]).max(), err_msg=kind)
     # a 4-D channels_last tensor of a multi-channel model
     m3 = _model(84, c=3)[0].cuda().eval()
     x3 = torch.rand((1, 3, 188, 188), device="cuda")
@@ -291,3 +295,34 @@ def test_eval_backward_uses_forward_mode_and_saved_weights():
             m.outc.conv.weight.add_(1.0)  # an optimizer step before the backward
         with pytest.raises(RuntimeError, match="inplace"):
             loss.backward()
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16"])
+def test_train_mode_input_gradient_vs_reference(precision):
+    """x.grad through a train-mode forward (the reference's autograd gives it
+    whenever the input requires grad): unet_plan_input_grad materialises
+    inc.c0's BatchNorm backward and correlates it with inc.c0's weights.
+    Against the reference arithmetic in fp64 (BatchNorm on batch statistics);
+    bf16 GEMMs within 3 % rel-L2 (a bf16 dgrad chain), fp32 within
+    max(1e-3, 2 x the reference's own fp32 error)."""
+    from oracle import torch_cpu_ref as R
+    from unet_amd import WeightedCrossEntropyLoss
+    m, params = _model(87)
+    m = m.cuda().train()
+    m.precision = precision
+    x, tgt, wmap = F.make_inputs(87, 2, 1, 188)
+    xd = torch.from_numpy(x).cuda().requires_grad_(True)
+    loss = WeightedCrossEntropyLoss()(m(xd), torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
+    loss.backward()
+    refs = {}
+    for dt in (torch.float64, torch.float32):
+        net = R.TorchCpuUNet(params, dtype=dt, training=True)
+        xr = torch.from_numpy(x).to(dt).requires_grad_(True)
+        lo = R.weighted_ce(net.forward(xr), torch.from_numpy(tgt), torch.from_numpy(wmap).to(dt))
+        lo.backward()
+        refs[dt] = xr.grad.double().numpy()
+    g = xd.grad.double().cpu().numpy()
+    e = _rel(g, refs[torch.float64])
+    tol = 3e-2 if precision == "bf16" else max(1e-3, 2 * _rel(refs[torch.float32], refs[torch.float64]))
+    assert e <= tol, (precision, e, tol)
+    print(f"train-mode input gradient ({precision}): rel-L2 {e:.2e} (tol {tol:.2e})")

@@ -88,6 +88,8 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
   const int wm = wave / WN, wn = wave % WN;
   const Gather& g = args.a;
   const int Cg = g.Cg, K = args.K, Hg = g.Hg, Wg = g.Wg;
+  int bx, by, bz;  // grid position in XCD-aware order (the column blocks' weights stay in one L2)
+  xcd_block(bx, by, bz);
   const int tiles_x = (Wg + 31) / 32, tiles_y = (Hg + TH - 1) / TH;
   const long long ntiles = (long long)g.nimg * tiles_y * tiles_x;
   auto coords = [&](long long t, int& n_, int& y0_, int& x0_) {
@@ -100,10 +102,10 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
   // + gridDim.x, ...; the next tile's first halo and tap-0/1 weights are DMA'd
   // during this tile's last chunk exactly like a next chunk's, so its
   // prologue latency hides under this tile's MFMAs and epilogue
-  long long tile = blockIdx.x;
+  long long tile = bx;
   int n, y0, x0;
   coords(tile, n, y0, x0);
-  const int n0 = blockIdx.y * BN;
+  const int n0 = by * BN;
 
   // XTF: BN scale / shift of source 0 (the only source that can carry a
   // transform: a skip or a previous conv output; the convT output never does)
@@ -186,7 +188,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
   int kc0 = 0, kc1 = nk_all;
   if (args.ksplit > 1) {
     const int per = (nk_all + args.ksplit - 1) / args.ksplit;
-    kc0 = blockIdx.z * per;
+    kc0 = bz * per;
     kc1 = min(nk_all, kc0 + per);
   }
 
@@ -391,7 +393,7 @@ __global__ __launch_bounds__(WM * WN * 64, MINW) void k_conv3_ring(const IgemmAr
       }
     }
     igemm_finish<TH * 32, BN, WM, WN, NT, HaloRows<32, TH>, 1>(args, acc, 0, n0, wm, wn, tid, red,
-                                                                HaloRows<32, TH>{n, y0, x0, Hg, Wg}, stage);
+                                                                HaloRows<32, TH>{n, y0, x0, Hg, Wg}, stage, bz);
     if (!PT || !wrap) return;
 #pragma unroll
     for (int i = 0; i < TM; ++i)

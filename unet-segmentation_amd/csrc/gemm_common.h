@@ -465,10 +465,13 @@ __device__ __forceinline__ void epi_shuffle(const Epilogue& e, const floatx16 (&
 // reads or writes any more -- enables epi_lds for bf16 destinations at TN = 2.
 // KSTAGE2: also stage the input gradient's masked form (KIND 2; callers with the
 // register budget for it -- k_conv3_bf's 128 VGPRs spilled).
+// kz: this workgroup's K slice (split-K partial plane), when its grid position
+// is remapped (xcd_block); < 0: blockIdx.z.
 template <int BM, int BN, int WM, int WN, int NT, class RowMap = LinearRows, int KSTAGE2 = 0>
 __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&acc)[BM / (WM * 32)][BN / (WN * 32)],
                                              int m0, int n0, int wm, int wn, int tid, float* red,
-                                             RowMap rows = RowMap{0, 0}, unsigned short* stage = nullptr) {
+                                             RowMap rows = RowMap{0, 0}, unsigned short* stage = nullptr,
+                                             int kz = -1) {
   if constexpr (std::is_same<RowMap, LinearRows>::value) {
     if (rows.M == 0) rows = LinearRows{m0, args.M};  // callers may pass a batched bound
   }
@@ -479,7 +482,7 @@ __device__ __forceinline__ void igemm_finish(const IgemmArgs& args, floatx16 (&a
   const int HWg = g.Hg * g.Wg;
   const int N = args.N;
   if (args.ksplit > 1) {  // raw partial tile; k_splitk_epi finishes
-    float* sl = args.slab + (size_t)blockIdx.z * M * N;
+    float* sl = args.slab + (size_t)(kz >= 0 ? kz : (int)blockIdx.z) * M * N;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = n0 + wn * TN * 32 + j * 32 + li;

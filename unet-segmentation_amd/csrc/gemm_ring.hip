@@ -38,6 +38,80 @@ namespace {
 typedef __bf16 bf16x8g_t __attribute__((ext_vector_type(8)));
 }  // namespace
 
+// LDS-staged pixel-shuffle epilogue of the convT forward (bf16 destination,
+// 64 columns per wave inside one sub-pixel ab): a 32-row fragment x 64 columns
+// passes through the wave's 4 KB of LDS ([row][64] bf16, 128-B rows) and leaves
+// by four 16-B stores per lane -- each row's 64 channels are 128 contiguous
+// bytes at output pixel (2y + a, 2x + b) -- instead of 32 2-B stores per lane
+// and fragment (epi_shuffle; round 5's phase probe put that per-element form at
+// a quarter of a small-K workgroup's time, profiles/r05_conv3_bf_phases.txt).
+// Same values (bias, optional ReLU, RNE to bf16) as epi_shuffle.  Returns false
+// (nothing stored) when the launch's epilogue is not of that form.
+template <int TM, int TN, int WM, int WN>
+__device__ __forceinline__ bool epi_shuffle_staged(const IgemmArgs& args, const floatx16 (&acc)[TM][TN], int m0, int n0,
+                                                   int wm, int wn, int tid, unsigned short* stage) {
+  static_assert(TN == 2, "64 columns per wave");
+  const Epilogue& e = args.e;
+  const Gather& g = args.a;
+  const Dst& d = e.d[0];
+  const int Co = e.shuffle_co, N = args.N;
+  if (!(Co > 0 && Co % 64 == 0 && e.n_split >= N && !e.stats && !e.yref && !e.colsum1 && d.h16 && d.C == Co &&
+        d.oy == 0 && d.ox == 0 && d.H == 2 * g.Hg && d.W == 2 * g.Wg &&
+        (reinterpret_cast<size_t>(d.ptr) & 15) == 0 && (size_t)args.M * 4 * (size_t)Co * 2 < (1ull << 32)))
+    return false;
+  const int lane = tid & 63, h = lane >> 5, li = lane & 31;
+  unsigned short* wl = stage + (tid >> 6) * (32 * 64);
+  const int col0 = n0 + wn * 64;
+  const int ab = col0 / Co, co0 = col0 - ab * Co;  // one sub-pixel per 64-column block (Co % 64 == 0)
+  const unsigned W2 = (unsigned)d.W, H2 = (unsigned)d.H;
+  const int Hg = g.Hg, Wg = g.Wg, M = args.M;
+  float bias[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bias[j] = e.bias ? e.bias[co0 + j * 32 + li] : 0.f;
+  uint16_t* const dst = reinterpret_cast<uint16_t*>(d.ptr);
+  const int rq = lane >> 3, cq = (lane & 7) * 8;  // this lane's rows rq + 8q and 8 channels of the readback
+#pragma unroll
+  for (int i = 0; i < TM; ++i) {
+    const int mb = m0 + (wm * TM + i) * 32;
+    const int lim = M - mb;
+    if (lim <= 0) continue;  // wave-uniform
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k = (r & 3) + 8 * (r >> 2) + 4 * h;
+        float v = acc[i][j][r] + bias[j];
+        if (e.relu) v = fmaxf(v, 0.f);
+        wl[k * 64 + j * 32 + li] = (unsigned short)bf16_of(v);
+      }
+    __builtin_amdgcn_sched_barrier(0);
+    // the output pixel of row mb + rq, then + 8 per q
+    int m = mb + rq;
+    int n = m / (Hg * Wg);
+    int rr = m - n * Hg * Wg;
+    int y = rr / Wg, x = rr - y * Wg;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int k = rq + 8 * q;
+      const uint4 val = *reinterpret_cast<const uint4*>(wl + k * 64 + cq);
+      if (k < lim) {
+        const unsigned pix = ((unsigned)n * H2 + 2u * y + (ab >> 1)) * W2 + 2u * x + (ab & 1);
+        *reinterpret_cast<uint4*>(dst + (size_t)pix * Co + co0 + cq) = val;
+      }
+      x += 8;  // next row of this lane
+      while (x >= Wg) {
+        x -= Wg;
+        if (++y == Hg) {
+          y = 0;
+          ++n;
+        }
+      }
+    }
+    lgkm_wait0();  // this fragment's LDS reads retired before the next one overwrites the tile
+  }
+  return true;
+}
+
 template <int BM, int BN, int BK, int NSTG>
 struct GemmRingGeo {
   static constexpr int RB = BK * 2, CPR = RB / 16, RPB = 256 / RB;  // row bytes, 16-B pieces per row, rows per bank row
@@ -70,7 +144,9 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm_ring(const IgemmArgs a
   const Gather& g = args.a;
   const Src& s0 = g.s[0];
   const int K = args.K, Cg = g.Cg, M = args.M;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int bx, by, bz;  // grid position in XCD-aware order
+  xcd_block(bx, by, bz);
+  const int m0 = bx * BM, n0 = by * BN;
   const int HWg = g.Hg * g.Wg;
 
   // XTF: BN scale / shift of the source channels, after the ring
@@ -113,7 +189,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm_ring(const IgemmArgs a
   int kc0 = 0, kc1 = nk_all;
   if (args.ksplit > 1) {
     const int per = (nk_all + args.ksplit - 1) / args.ksplit;
-    kc0 = blockIdx.z * per;
+    kc0 = bz * per;
     kc1 = min(nk_all, kc0 + per);
   }
   const int nk = kc1 - kc0;
@@ -213,7 +289,15 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_gemm_ring(const IgemmArgs a
   }
   vm_wait<0>();
   __syncthreads();
-  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, reinterpret_cast<float*>(lds));
+  // the whole LDS image is free: the waves' 4-KB staging tiles first, the
+  // statistics buffer after them
+  constexpr bool kStage = TN == 2 && (size_t)NW * 4096 + (size_t)WM * 3 * BN * 4 <= G::smem;
+  unsigned short* stage = kStage ? reinterpret_cast<unsigned short*>(lds) : nullptr;
+  float* red = reinterpret_cast<float*>(lds + (kStage ? NW * 4096 : 0));
+  if constexpr (kStage) {
+    if (epi_shuffle_staged<TM, TN, WM, WN>(args, acc, m0, n0, wm, wn, tid, stage)) return;
+  }
+  igemm_finish<BM, BN, WM, WN, NT, LinearRows, 1>(args, acc, m0, n0, wm, wn, tid, red, LinearRows{0, 0}, stage, bz);
 }
 
 // ---------------------------------------------------------------------------

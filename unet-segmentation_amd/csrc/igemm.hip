@@ -21,6 +21,10 @@
 #include "gemm_common.h"
 
 namespace unet {
+// convT weight gradient on an LDS-DMA ring of pixel stages (wgradT_ring.hip,
+// wgrad tiles 40-43)
+bool wgradT_ring_fits(const WgradArgs& a, int tile);
+hipError_t go_wgradT_ring(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
 
 // Occupancy the register allocator must preserve: as many workgroups as the
 // LDS footprint admits per CU (without it hipcc moves the accumulators to
@@ -1438,6 +1442,7 @@ bool wgrad_tile_fits(const WgradArgs& a, int tile) {
   if (tile == 22 || tile == 23) return wgrad3_f32_fits(a);  // fp32 twin
   if (tile == 24 || tile == 25) return wgrad3w_fits(a, tile);  // wide halo-tiled 3x3, two-stage ring
   if (tile >= 26 && tile <= 33) return wgrad3_ring_fits(a, tile);  // LDS-DMA ring of pixel tiles
+  if (tile >= 40 && tile <= 44) return wgradT_ring_fits(a, tile);  // convT: LDS-DMA ring of pixel stages
   int bm, bn;
   wgrad_tile(tile, bm, bn);
   return bm > 0 && (tile >= 10) == (a.bf16 != 0) && a.Mo % bm == 0 && a.No % bn == 0;
@@ -1456,6 +1461,9 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
     } else if (g_tune_wgrad >= 110 && g_tune_wgrad <= 114 && wgrad_tile_fits(a, g_tune_wgrad - 100)) {
       c.tile = tile = g_tune_wgrad - 100;  // forced pixel-column tile in slab mode, 2 per CU (tests)
       c.split = 102;
+    } else if (g_tune_wgrad >= 140 && g_tune_wgrad <= 144 && wgrad_tile_fits(a, g_tune_wgrad - 100)) {
+      tile = g_tune_wgrad - 100;  // forced convT ring tile in slab mode, 1 per CU (tests)
+      c.split = 11;
     }
     else if (wgrad3_fits(a)) tile = 20;
     else if (a.Mo % 128 == 0 && a.No % 128 == 0) tile = 10;
@@ -1484,6 +1492,7 @@ hipError_t launch_wgrad_v(const WgradArgs& a0, hipStream_t s, GemmChoice c) {
   if (tile == 22) return go_wgrad3_f32<8, 16>(a, s, c.split > 0 ? c.split : 4);
   if (tile == 24 || tile == 25) return go_wgrad3w_bf16(a, s, tile, c.split > 0 ? c.split : 1);
   if (tile >= 26 && tile <= 33) return go_wgrad3_ring(a, s, tile, c.split > 0 ? c.split : 1);
+  if (tile >= 40 && tile <= 44) return go_wgradT_ring(a, s, tile, c.split > 0 ? c.split : 1);
   if (tile == 23) return go_wgrad3_f32<4, 32>(a, s, c.split > 0 ? c.split : 4);
   int bm, bn;
   wgrad_tile(tile, bm, bn);

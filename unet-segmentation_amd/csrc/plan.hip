@@ -302,7 +302,7 @@ constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 // Version of the GEMM variant tables (tile ids and their kernels): part of every
 // tuning key, so a database written by a build with another tile set is never
 // replayed (its lines simply miss).  Bump whenever a tile id changes meaning.
-constexpr int kTileTableVersion = 10;
+constexpr int kTileTableVersion = 13;
 
 std::string igemm_key(const IgemmArgs& a) {
   char b[240], small[16] = "";
@@ -339,6 +339,7 @@ std::string wgrad_key(const WgradArgs& a) {
 bool wgrad_choice_deterministic(const GemmChoice& g) {
   if (g.tile == 71 || g.tile == 74) return g.split >= 1000;
   if (g.tile >= 26 && g.tile <= 33) return g.split >= 10;
+  if (g.tile >= 40 && g.tile <= 44) return g.split >= 10;
   if (g.tile >= 0 && g.tile <= 14) return g.split >= 100;
   return false;
 }
@@ -373,7 +374,10 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
     v.push_back({t, 1});
     if (t == 70 || t == 71 || t == 74)  // Winograd: no K split; the tile of its batched point GEMMs
       for (int inner : {1, 2, 3, 4, 6, 7, 8, 9}) v.push_back({t, 100 + inner});
-    if (t >= 70) continue;
+    // Winograd (70-77) and the persistent ring 88 take no K split; the LDS-DMA
+    // rings 81-84 (3x3) and 91-99 (convT) do (the 24-48^2
+    // bottleneck grids give them 144-192 workgroups for 256 CUs)
+    if ((t >= 70 && t <= 77) || t == 88) continue;
     const long long cnt = igemm_tile_count(a, t);
     const long long slots = (long long)igemm_tile_slots(t) * cus;
     if (cnt >= 4 * slots || a.N % 64 != 0) continue;  // enough workgroup rounds already
@@ -387,8 +391,13 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
 
 std::vector<GemmChoice> wgrad_candidates(const WgradArgs& a) {
   std::vector<GemmChoice> v;
-  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 71, 74}) {  // fits() filters by precision
+  for (int t : {0, 1, 2, 3, 4, 10, 11, 12, 13, 14, 20, 21, 22, 23, 24, 25, 26, 27, 28, 29, 30, 31, 32, 33, 40, 41, 42, 43, 44,
+                71, 74}) {  // fits() filters by precision
     if (!wgrad_tile_fits(a, t) || tune_skipped(t)) continue;
+    if (t >= 40 && t <= 44) {  // convT LDS-DMA ring (one resident workgroup per CU): slab mode only
+      for (int per_cu : {11, 12}) v.push_back({t, per_cu});
+      continue;
+    }
     if (t == 71 || t == 74) {  // Winograd: point-GEMM tile (k_wgrad 0-4) x workgroups per CU
       // (each pixel split adds a full points x Co x Ci slab by fp32 atomics:
       // 1-2 per CU cut that traffic on the deep, few-tile layers); + 1000:
@@ -1385,6 +1394,32 @@ int unet_plan_backward_ex(unet_plan* p, void* const* prm, void* const* grd, cons
   }
   return run_backward(p, prm, grd, x, dlogits, reinterpret_cast<char*>(ws), sb, se,
                       reinterpret_cast<hipStream_t>(stream), flags);
+}
+
+size_t unet_plan_input_grad_scratch_bytes(const unet_plan* p) {
+  return p ? (size_t)p->n * p->L[0].ho * p->L[0].wo * p->L[0].co * sizeof(float) : 0;
+}
+
+// The gradient of the network input (the reference's x.grad when x requires
+// grad, models/unet_model.py:105 under autograd).  The training backward never
+// forms it -- inc.c0's BatchNorm backward is fused into its weight gradient and
+// dY(0) is not materialised -- so after the backward segment holding inc.c0
+// this call materialises dY(0) = k0 dz0 + k1 (y0 - mean) + k2 into `scratch`
+// (fp32, unet_plan_input_grad_scratch_bytes) and correlates it with inc.c0's
+// weights into dx (NCHW fp32, overwritten).
+int unet_plan_input_grad(unet_plan* p, void* const* prm, float* dx, void* ws, void* scratch, unet_stream_t stream) {
+  if (!p || !prm || !dx || !ws || !scratch) {
+    set_err("unet_plan_input_grad: bad argument");
+    return -EINVAL;
+  }
+  const hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  Ctx c{p, reinterpret_cast<char*>(ws), s};
+  const Conv& L = p->L[0];
+  const int g16 = p->prec == UNET_PREC_BF16;
+  float* dy0 = reinterpret_cast<float*>(scratch);
+  CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), p->n, L.ho, L.wo, L.co, dy0, 0, s, 0, g16, g16));
+  CK(launch_conv_first_dgrad(dy0, p->n, p->cin, p->h, p->w, P<float>(prm, L.pw), dx, s));
+  return 0;
 }
 
 int unet_plan_wait_segment(unet_plan* p, int seg, unet_stream_t stream) {

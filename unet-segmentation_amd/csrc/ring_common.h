@@ -43,6 +43,23 @@ __device__ __forceinline__ void dma4_sv(unsigned voff, unsigned long long sbase,
       : "memory");
 }
 
+// XCD-aware workgroup order (cdna_hip_programming.md T1): workgroups are dealt
+// round robin over the 8 XCDs (linear id = x + gx (y + gy z)); remapped, each
+// XCD runs one contiguous run of that order, so the column blocks it computes
+// -- the weight slabs every pixel tile of a block re-reads -- and the split's
+// operand slices stay in its own 4 MB L2 instead of being fetched from the
+// Infinity Cache by all eight.  Identity when the grid does not split evenly.
+// Speed only: every (bx, by, bz) is still visited exactly once.
+__device__ __forceinline__ void xcd_block(int& bx, int& by, int& bz) {
+  const unsigned gx = gridDim.x, gy = gridDim.y, total = gx * gy * gridDim.z;
+  unsigned bid = blockIdx.x + gx * (blockIdx.y + gy * blockIdx.z);
+  if ((total & 7u) == 0) bid = (bid & 7u) * (total >> 3) + (bid >> 3);
+  bx = (int)(bid % gx);
+  bid /= gx;
+  by = (int)(bid % gy);
+  bz = (int)(bid / gy);
+}
+
 __device__ __forceinline__ unsigned long long uniform_u64(const void* p) {
   const unsigned long long v = reinterpret_cast<unsigned long long>(p);
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);

@@ -102,7 +102,9 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int tg = SLIDE ? 0 : wave >> 2, wr = SLIDE ? wave : wave & 3, ct = wr % NCI, cg = wr / NCI;
-  const int i0 = blockIdx.x * BCO, cb = (blockIdx.y + cblk0) * BCI;
+  int bx, by, bz;  // grid position in XCD-aware order (a pixel split's operand slices stay in one L2)
+  xcd_block(bx, by, bz);
+  const int i0 = bx * BCO, cb = (by + cblk0) * BCI;
   const Gather& gb = args.gb;
   const Src& ds = args.ga.s[0];
   const int Hg = gb.Hg, Wg = gb.Wg, Ci = gb.Cg;
@@ -124,7 +126,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
   }
   const int tiles_x = (Wg + TW - 1) / TW, tiles_y = (Hg + TH - 1) / TH;
   const int tiles = gb.nimg * tiles_x * tiles_y;
-  const int z = blockIdx.z, gz = gridDim.z;
+  const int z = bz, gz = gridDim.z;
   const int cnt = z < tiles ? (tiles - z + gz - 1) / gz : 0;
   if (cnt == 0) return;
 
@@ -410,7 +412,7 @@ __global__ __launch_bounds__(512, 1) void k_wgrad3_ring(const WgradArgs args, in
   // plain stores, summed into out by k_wr_reduce
   const int h = lane >> 5, li = lane & 31;
   const int t0 = tg * 5, nt = SLIDE ? 9 : tg ? 4 : 5;
-  float* const plane = args.slab ? args.slab + (size_t)blockIdx.z * args.Mo * args.No : nullptr;
+  float* const plane = args.slab ? args.slab + (size_t)bz * args.Mo * args.No : nullptr;
 #pragma unroll
   for (int i = 0; i < TMC1; ++i)
 #pragma unroll

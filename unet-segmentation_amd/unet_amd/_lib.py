@@ -36,6 +36,8 @@ SIGNATURES = {
     "unet_plan_backward": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _vp]),
     "unet_plan_backward_ex": (_i, [_vp, _vp, _vp, _vp, _vp, _vp, _i, _i, _i, _vp]),
     "unet_plan_wait_segment": (_i, [_vp, _i, _vp]),
+    "unet_plan_input_grad_scratch_bytes": (_sz, [_vp]),
+    "unet_plan_input_grad": (_i, [_vp, _vp, _vp, _vp, _vp, _vp]),
     "unet_plan_join": (_i, [_vp, _vp]),
     "unet_plan_set_timing": (_i, [_vp, _i]),
     "unet_plan_timing": (_i, [_vp, _vp, _vp, _vp, _vp]),
@@ -152,7 +154,7 @@ def stream_of(device=None):
 # csrc/Makefile SRC_HASH: sha256 over these files, in this order
 _HASHED = ["igemm.hip", "igemm_bf16.hip", "conv3_dma.hip", "conv3_ring.hip", "winograd.hip", "elementwise.hip", "elastic.hip",
            "tiling.hip", "weightmap.hip", "postproc.hip", "track.hip", "ops.hip", "plan.hip", "wgrad3_ring.hip",
-           "conv3_ring_pt.hip", "peak.hip", "gemm_ring.hip", "unet_internal.h", "gemm_common.h", "ring_common.h", "conv3_ring_kernel.h",
+           "conv3_ring_pt.hip", "peak.hip", "gemm_ring.hip", "wgradT_ring.hip", "unet_internal.h", "gemm_common.h", "ring_common.h", "conv3_ring_kernel.h",
            os.path.join("..", "..", "include", "unet_hip.h")]
 
 

@@ -192,8 +192,11 @@ class _UNetFunction(torch.autograd.Function):
         dlogits = dlogits.contiguous()
         grads = [torch.empty_like(p) for p in params]
         ctx.plan.backward(ctx.tab, _lib.ptr_array(grads), x, dlogits, ctx.ws)
+        # x.grad only when asked for (the training loop never does): the fused
+        # inc.c0 backward does not form it
+        dx = ctx.plan.input_grad(ctx.tab, x, ctx.ws) if ctx.needs_input_grad[0] else None
         ctx.ws = None
-        return (None, None, None, None, *grads)
+        return (dx, None, None, None, *grads)
 
 
 def _eval_backward(module, x, dlogits, params, need_x):

@@ -61,6 +61,18 @@ class Plan:
                                                   _lib.stream_of(x.device)),
                    "unet_plan_backward_ex")
 
+    def input_grad(self, param_tab, x, ws):
+        """x.grad of the last backward (unet_plan_input_grad): inc.c0's
+        BatchNorm-backward output materialised in a scratch tensor, then its
+        full correlation with inc.c0's weights.  Same stream as the backward."""
+        import torch
+        scratch = torch.empty(int(self.lib.unet_plan_input_grad_scratch_bytes(self.handle)), dtype=torch.uint8,
+                              device=x.device)
+        dx = torch.empty_like(x)
+        _lib.check(self.lib.unet_plan_input_grad(self.handle, param_tab, dx.data_ptr(), ws.data_ptr(),
+                                                 scratch.data_ptr(), _lib.stream_of(x.device)), "unet_plan_input_grad")
+        return dx
+
     def wait_segment(self, seg, stream):
         """Make `stream` (a torch stream) wait for segment seg's weight gradients."""
         _lib.check(self.lib.unet_plan_wait_segment(self.handle, seg, ctypes.c_void_p(stream.cuda_stream)),
