@@ -46,7 +46,8 @@ typedef __bf16 bf16x8g_t __attribute__((ext_vector_type(8)));
 // and fragment (epi_shuffle; round 5's phase probe put that per-element form at
 // a quarter of a small-K workgroup's time, profiles/r05_conv3_bf_phases.txt).
 // Same values (bias, optional ReLU, RNE to bf16) as epi_shuffle.  Returns false
-// (nothing stored) when the launch's epilogue is not of that form.
+// (nothing stored) when the launch's epilogue is not of that form (a split-K
+// slice stores its raw partial through igemm_finish instead).
 template <int TM, int TN, int WM, int WN>
 __device__ __forceinline__ bool epi_shuffle_staged(const IgemmArgs& args, const floatx16 (&acc)[TM][TN], int m0, int n0,
                                                    int wm, int wn, int tid, unsigned short* stage) {
@@ -55,7 +56,8 @@ __device__ __forceinline__ bool epi_shuffle_staged(const IgemmArgs& args, const 
   const Gather& g = args.a;
   const Dst& d = e.d[0];
   const int Co = e.shuffle_co, N = args.N;
-  if (!(Co > 0 && Co % 64 == 0 && e.n_split >= N && !e.stats && !e.yref && !e.colsum1 && d.h16 && d.C == Co &&
+  if (!(args.ksplit <= 1 && Co > 0 && Co % 64 == 0 && e.n_split >= N && !e.stats && !e.yref && !e.colsum1 && d.h16 &&
+        d.C == Co &&
         d.oy == 0 && d.ox == 0 && d.H == 2 * g.Hg && d.W == 2 * g.Wg &&
         (reinterpret_cast<size_t>(d.ptr) & 15) == 0 && (size_t)args.M * 4 * (size_t)Co * 2 < (1ull << 32)))
     return false;

@@ -21,9 +21,10 @@
 //    k_wgrad3_ring), 16-B chunks XOR-swizzled by row & 3 on 64-B segments
 //    (rswz) on the DMA source address, so each 32-lane read group covers the 64
 //    banks once;
-//  * per lane the DMA source is a pixel iterator (n, y, x) per piece advanced
-//    by BK per stage: X at (n, y, x), dY at (n, 2y + a, 2x + b) with the lane's
-//    (ab, co) fixed -- no division in the loop;
+//  * per lane the DMA source offsets are affine in the pixel (whole-grid
+//    sources): a stage adds a constant for X and, for dY at (n, 2y + a, 2x + b),
+//    tracks x = p mod w by one conditional subtraction -- a few VALU per piece,
+//    no division or loop;
 //  * X's BatchNorm + ReLU is applied in place one stage ahead of its MFMAs
 //    (XTF); pixels past the split's end read a clamped valid pixel and their X
 //    rows are zeroed in the same pass, so they add nothing;
@@ -59,19 +60,6 @@ __host__ __device__ constexpr int tswz(int row, int c) {
   else return (((c >> 2) ^ (row & 3)) << 2) | (c & 3);
 }
 
-struct PixPos {
-  int n, y, x;
-};
-__device__ __forceinline__ void pix_advance(PixPos& q, int d, int H, int W) {
-  q.x += d;
-  while (q.x >= W) {
-    q.x -= W;
-    if (++q.y == H) {
-      q.y = 0;
-      ++q.n;
-    }
-  }
-}
 }  // namespace
 
 template <int BMO, int BNO, int BK, int NS>
@@ -124,7 +112,7 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_wgradT_ring(const WgradArgs
   const Gather& gb = args.gb;  // dY: 2 x 2 stride-2 taps, channels Co
   const Src& xs = ga.s[0];
   const Src& ds = gb.s[0];
-  const int Hg = ga.Hg, Wg = ga.Wg, Co = gb.Cg;
+  const int Wg = ga.Wg, Co = gb.Cg;
   const bool xtf = XTF && xs.scale != nullptr;
   if constexpr (XTF) {
     if (xtf)
@@ -134,71 +122,54 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_wgradT_ring(const WgradArgs
       }
   }
 
-  // ---- per-lane DMA pieces: pixel row, channel / column, source position ----
+  // ---- per-lane DMA pieces ----
+  // Both sources are whole grids without an origin (fits(): X on the h x w
+  // convT input grid, dY on its 2h x 2w output), so a piece's byte offset is
+  // affine in its pixel p = (n*h + y)*w + x, up to dY's column term:
+  //   X:  (p*C + ci) * 2
+  //   dY: ((4p - 2x)*Co + ab_off + co) * 2      (ab_off = (a*2w + b)*Co)
+  // and a stage advances p by BK: X adds a constant, dY tracks x = p mod w by
+  // one conditional subtraction (BK mod w precomputed).  Pieces past the last
+  // pixel are clamped to a valid address (their X rows are zeroed in LDS).
   const unsigned long long xbase = uniform_u64(xs.ptr), dbase = uniform_u64(ds.ptr);
-  int arow[DA], brow[DB];
-  unsigned acol[DA], boff0[DB];  // element offsets of the piece's channels
-  int ba[DB], bb[DB];            // sub-pixel of the piece
-  PixPos ap[DA], bp[DB];
+  const int Cx = xs.C;
+  const int rbk = BK % Wg;
+  const unsigned xlast = (unsigned)((size_t)(args.P - 1) * Cx * 2);                   // + the piece's channel bytes
+  const unsigned dlast = (unsigned)(((size_t)ga.nimg * ds.H * ds.W * Co - 8) * 2);  // last 16-B piece of dY
+  unsigned axo[DA], acb[DA];  // X: byte offset of the piece's pixel row, its channel bytes
+  int bpix[DB], bx[DB];       // dY: the piece's pixel and its x
+  unsigned bcb[DB];           // dY: (ab_off + co) * 2
 #pragma unroll
   for (int u = 0; u < DA; ++u) {
     const int b = (wave + NW * u) * 1024 + lane * 16;
-    arow[u] = b / RA;
-    acol[u] = (unsigned)(i0 + tswz<RA>(arow[u], (b % RA) / 16) * 8);
+    const int row = b / RA;
+    acb[u] = (unsigned)((i0 + tswz<RA>(row, (b % RA) / 16) * 8) * 2);
+    axo[u] = (unsigned)((size_t)(pbeg + row) * Cx * 2);
   }
 #pragma unroll
   for (int u = 0; u < DB; ++u) {
     const int b = (wave + NW * u) * 1024 + lane * 16;
-    brow[u] = b / RB;
-    const int col = j0 + tswz<RB>(brow[u], (b % RB) / 16) * 8;
+    const int row = b / RB;
+    const int col = j0 + tswz<RB>(row, (b % RB) / 16) * 8;
     const int ab = col / Co;
-    ba[u] = ab >> 1;
-    bb[u] = ab & 1;
-    boff0[u] = (unsigned)(col - ab * Co);
-  }
-  // pixel iterators of the first stage (clamped into the grid: rows past the
-  // split's end read a valid pixel, zeroed in LDS for X)
-  auto pos_of = [&](int p) {
-    p = min(p, args.P - 1);
-    PixPos q;
-    const int hw = Hg * Wg;
-    q.n = p / hw;
-    const int r = p - q.n * hw;
-    q.y = r / Wg;
-    q.x = r - q.y * Wg;
-    return q;
-  };
-  // unclamped pixel of each piece: its iterator stops at the last pixel
-  int pa[DA], pbv[DB];
-#pragma unroll
-  for (int u = 0; u < DA; ++u) {
-    pa[u] = pbeg + arow[u];
-    ap[u] = pos_of(pa[u]);
-  }
-#pragma unroll
-  for (int u = 0; u < DB; ++u) {
-    pbv[u] = pbeg + brow[u];
-    bp[u] = pos_of(pbv[u]);
+    bcb[u] = (unsigned)((((ab >> 1) * ds.W + (ab & 1)) * Co + (col - ab * Co)) * 2);
+    bpix[u] = pbeg + row;
+    bx[u] = bpix[u] % Wg;
   }
 
   // DMA u (0 .. D-1: X pieces, then dY pieces) of the next stage to issue, into
-  // ring slot `slot`; advances that piece's iterator by BK
+  // ring slot `slot`; then advances that piece by BK pixels
   auto issue1 = [&](int slot, int u) {
     if (u < DA) {
-      const PixPos& q = ap[u];
-      const unsigned off =
-          (unsigned)((((q.n * xs.H + q.y + xs.oy) * xs.W + q.x + xs.ox) * xs.C) + acol[u]) * 2u;
-      dma_sv(off, xbase, lds0 + slot * SSZ + (wave + NW * u) * 1024);
-      if (pa[u] + BK < args.P) pix_advance(ap[u], BK, Hg, Wg);
-      pa[u] += BK;
+      dma_sv(min(axo[u], xlast) + acb[u], xbase, lds0 + slot * SSZ + (wave + NW * u) * 1024);
+      axo[u] += (unsigned)(BK * Cx * 2);
     } else {
       const int k = u - DA;
-      const PixPos& q = bp[k];
-      const unsigned off = (unsigned)((((q.n * ds.H + 2 * q.y + ba[k] + ds.oy) * ds.W + 2 * q.x + bb[k] + ds.ox) *
-                                       ds.C) + boff0[k]) * 2u;
-      dma_sv(off, dbase, lds0 + slot * SSZ + ASZ + (wave + NW * k) * 1024);
-      if (pbv[k] + BK < args.P) pix_advance(bp[k], BK, Hg, Wg);
-      pbv[k] += BK;
+      const unsigned off = (unsigned)(4 * bpix[k] - 2 * bx[k]) * (unsigned)(Co * 2) + bcb[k];
+      dma_sv(min(off, dlast), dbase, lds0 + slot * SSZ + ASZ + (wave + NW * k) * 1024);
+      bpix[k] += BK;
+      bx[k] += rbk;
+      bx[k] -= bx[k] >= Wg ? Wg : 0;
     }
   };
 
@@ -262,28 +233,34 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_wgradT_ring(const WgradArgs
     fix_stage(0, pbeg);
     lgkm_wait0();     // its rewritten pieces land before the first barrier releases them
   }
-  for (int i = 0; i < nk; ++i) {
-    // stage i + 1 landed for this wave (stage i was fixed before the barrier);
-    // the barrier publishes every wave's pieces and the fix of stage i, and
-    // frees slot i - 1 for the refill below
+  // ring step for stage i in slot S (compile-time: the LDS read addresses are a
+  // per-lane base plus immediates):
+  // stage i + 1 landed for this wave (stage i was fixed before the barrier);
+  // the barrier publishes every wave's pieces and the fix of stage i, and
+  // frees slot i - 1 for the refill below
+  auto step = [&](auto Sc, int i) {
+    constexpr int S = decltype(Sc)::value, S1 = (S + 1) % NS, SN = (S + P) % NS;
     vm_wait<D * (P - 2)>();
     raw_barrier();
-    const int slot = i % NS, nslot = (i + P) % NS;
     if (i + 1 < nk) {
-      fix_stage((i + 1) % NS, pbeg + (i + 1) * BK);
+      fix_stage(S1, pbeg + (i + 1) * BK);
       lgkm_wait0();  // (the fixed stage i + 1 is read only after the next barrier)
     }
-    const unsigned sb = lds0 + slot * SSZ;
+    unsigned ra[TM], rb[TN];
+#pragma unroll
+    for (int t = 0; t < TM; ++t) ra[t] = lds0 + S * SSZ + aoff[t];
+#pragma unroll
+    for (int t = 0; t < TN; ++t) rb[t] = lds0 + S * SSZ + boff[t];
     bf16x8t_t fa[2][TM], fb[2][TN];
     auto rd = [&](int ks, int b) {
 #pragma unroll
       for (int t = 0; t < TM; ++t)
-        fa[b][t] = __builtin_shufflevector(tr4(sb + aoff[t] + (16 * ks) * RA), tr4(sb + aoff[t] + (16 * ks + 4) * RA),
-                                           0, 1, 2, 3, 4, 5, 6, 7);
+        fa[b][t] = __builtin_shufflevector(tr4(ra[t] + (16 * ks) * RA), tr4(ra[t] + (16 * ks + 4) * RA), 0, 1, 2, 3,
+                                           4, 5, 6, 7);
 #pragma unroll
       for (int t = 0; t < TN; ++t)
-        fb[b][t] = __builtin_shufflevector(tr4(sb + boff[t] + (16 * ks) * RB), tr4(sb + boff[t] + (16 * ks + 4) * RB),
-                                           0, 1, 2, 3, 4, 5, 6, 7);
+        fb[b][t] = __builtin_shufflevector(tr4(rb[t] + (16 * ks) * RB), tr4(rb[t] + (16 * ks + 4) * RB), 0, 1, 2, 3,
+                                           4, 5, 6, 7);
     };
     rd(0, 0);
 #pragma unroll
@@ -298,7 +275,22 @@ __global__ __launch_bounds__(WM * WN * 64, 1) void k_wgradT_ring(const WgradArgs
       // the stage P ahead, its DMAs spread over the k-steps
 #pragma unroll
       for (int u = 0; u < D; ++u)
-        if (u * KS / D == ks) issue1(nslot, u);
+        if (u * KS / D == ks) issue1(SN, u);
+    }
+  };
+  static_assert(NS <= 6, "ring steps unrolled below");
+  for (int i = 0; i < nk; i += NS) {
+    step(std::integral_constant<int, 0>{}, i);
+    if (i + 1 < nk) step(std::integral_constant<int, 1>{}, i + 1);
+    if (i + 2 < nk) step(std::integral_constant<int, 2 % NS>{}, i + 2);
+    if constexpr (NS > 3) {
+      if (i + 3 < nk) step(std::integral_constant<int, 3 % NS>{}, i + 3);
+    }
+    if constexpr (NS > 4) {
+      if (i + 4 < nk) step(std::integral_constant<int, 4 % NS>{}, i + 4);
+    }
+    if constexpr (NS > 5) {
+      if (i + 5 < nk) step(std::integral_constant<int, 5 % NS>{}, i + 5);
     }
   }
   vm_wait<0>();  // the tail's re-issued DMAs land before the workgroup exits
@@ -353,7 +345,10 @@ bool wgradT_ring_fits(const WgradArgs& a, int tile) {
          gb.taps_h == 2 && gb.taps_w == 2 && gb.stride == 2 && gb.c_split >= gb.Cg && a.No == 4 * gb.Cg &&
          gb.Cg % 8 == 0 && a.Mo % bmo == 0 && a.No % bno == 0 && ga.Hg == gb.Hg && ga.Wg == gb.Wg &&
          ga.nimg == gb.nimg && a.P == ga.nimg * ga.Hg * ga.Wg && xs.h16 && ds.h16 && ds.scale == nullptr &&
-         (xs.scale == nullptr || xs.shift != nullptr) && xb < 4294967296.0 && db < 4294967296.0 && a.P > 0;
+         (xs.scale == nullptr || xs.shift != nullptr) && xb < 4294967296.0 && db < 4294967296.0 && a.P > 0 &&
+         // whole grids without an origin (the plan's convT input and output gradient)
+         xs.oy == 0 && xs.ox == 0 && xs.H == ga.Hg && xs.W == ga.Wg && xs.C == a.Mo && ds.oy == 0 && ds.ox == 0 &&
+         ds.H == 2 * gb.Hg && ds.W == 2 * gb.Wg && ds.C == gb.Cg;
 }
 
 template <int BMO, int BNO, int WM, int WN, int BK, int NS>
