@@ -540,8 +540,10 @@ class UNetOracle:
         logits = conv_valid_fwd(a, self._w("outc.conv.weight"), self._w("outc.conv.bias"))
         return np.transpose(logits, (0, 3, 1, 2)), cache, nb
 
-    def backward(self, dlogits_nchw, cache):
-        """Gradients for every parameter (same keys as the reference's named_parameters)."""
+    def backward(self, dlogits_nchw, cache, input_grad=False):
+        """Gradients for every parameter (same keys as the reference's named_parameters);
+        input_grad: also the gradient of the network input, NCHW (the reference's
+        x.grad under autograd, models/unet_model.py:105), returned as (grads, dx)."""
         grads = OrderedDict()
         dl = np.ascontiguousarray(np.transpose(np.asarray(dlogits_nchw, self.dtype), (0, 2, 3, 1)))
         d, dw, db = conv_valid_bwd(cache["outc.in"], self._w("outc.conv.weight"), dl)
@@ -564,7 +566,9 @@ class UNetOracle:
             dpool = self._double_conv_bwd(_dc_prefix(f"down{k}"), d, cache, grads)
             arg, in_shape = cache[f"pool{k}"]
             d = maxpool2_bwd(self._q(dpool), arg, in_shape) + dskips[k - 1]
-        self._double_conv_bwd(_dc_prefix("inc"), d, cache, grads, need_dx=False)
+        dx = self._double_conv_bwd(_dc_prefix("inc"), d, cache, grads, need_dx=input_grad)
+        if input_grad:
+            return grads, np.transpose(dx, (0, 3, 1, 2))
         return grads
 
 

@@ -224,6 +224,73 @@ def test_bf16_ring_persistent_bitexact(op_bf16, pt, base, kind):
     assert torch.equal(outs[0], outs[1])
 
 
+def _flat_tiling(n, hg, wg, bm=256, npx=400):
+    """conv3_flat.hip's flat_map: ("cross" | "image" | None, tiles, worst
+    halo run in pixels) of an (n, hg, wg) output grid."""
+    hw, hin, win = hg * wg, hg + 2, wg + 2
+
+    def qin(p):
+        img, rem = divmod(p, hw)
+        y, x = divmod(rem, wg)
+        return (img * hin + y) * win + x
+
+    def span(p0, c):
+        return qin(p0 + c - 1) + 2 * win + 2 - qin(p0) + 1
+    m = n * hw
+    nt = (m + bm - 1) // bm
+    worst = max(span(t * bm, min(bm, m - t * bm)) for t in range(nt))
+    if worst <= npx:
+        return "cross", nt, worst
+    tpi = (hw + bm - 1) // bm
+    worst = max(span(t * bm, min(bm, hw - t * bm)) for t in range(tpi))
+    return ("image" if worst <= npx else None), n * tpi, worst
+
+
+@pytest.mark.parametrize("kind", ["fwd", "fwd_tf", "dgrad"])
+@pytest.mark.parametrize("n,h,w,ci,co", [(8, 26, 26, 128, 128), (2, 48, 48, 64, 128), (3, 30, 50, 64, 256),
+                                         (1, 10, 9, 64, 128), (8, 28, 28, 64, 256)])
+def test_bf16_flat_tile_bitexact_vs_ring(op_bf16, kind, n, h, w, ci, co):
+    """The ring on flat pixel tiles (85, conv3_flat.hip: 256 consecutive
+    output pixels per tile, fragments wrapping grid rows, tiles crossing image
+    boundaries or per image) against the row-tiled ring of the same chunk / tap /
+    k-step order (81): bit-identical outputs -- on grids narrower than a
+    fragment (24, 26, 28), a 46-wide one, H != W with an odd batch, and a
+    single tile with idle rows."""
+    lib = op_bf16
+    # the shapes are ones tile 85 takes (else the forced variant falls back)
+    assert _flat_tiling(n, h - 2, w - 2)[0] and _flat_tiling(n, h, w)[0]
+    rng = np.random.default_rng(h * 1000 + w)
+    x = dev(f32(rng.standard_normal((n, h, w, ci))))
+    wt = dev(f32(rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci)))
+    b = dev(f32(rng.standard_normal(co)))
+    sc = dev(f32(rng.uniform(-0.5, 1.5, ci)))
+    sh = dev(f32(rng.standard_normal(ci) * 0.3))
+    dy = dev(f32(rng.standard_normal((n, h - 2, w - 2, co))))
+    ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
+    lib.unet_set_tuning(b"op_a16", 1)
+    outs = []
+    try:
+        for v in (81, 85):
+            lib.unet_set_tuning(b"igemm_variant", v)
+            if kind == "dgrad":
+                out = torch.full((n, h, w, ci), float("nan"), device="cuda")
+                ck(lib.unet_conv3x3_dgrad(dy.data_ptr(), n, h, w, ci, wt.data_ptr(), co, out.data_ptr(),
+                                          ws.data_ptr(), stream()))
+            else:
+                tf = kind == "fwd_tf"
+                out = torch.full((n, h - 2, w - 2, co), float("nan"), device="cuda")
+                ck(lib.unet_conv3x3_fwd(x.data_ptr(), n, h, w, ci, wt.data_ptr(), b.data_ptr(), co,
+                                        sc.data_ptr() if tf else None, sh.data_ptr() if tf else None,
+                                        out.data_ptr(), ws.data_ptr(), stream()))
+            torch.cuda.synchronize()
+            outs.append(out)
+    finally:
+        lib.unet_set_tuning(b"op_a16", 0)
+        lib.unet_set_tuning(b"igemm_variant", -1)
+    assert torch.isfinite(outs[1]).all()
+    assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
+
+
 @pytest.mark.parametrize("variant", DMA)
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 19, 40, 128, 64), (2, 8, 8, 64, 256),
                                          (1, 36, 66, 64, 128)])
@@ -431,7 +498,8 @@ def gemm_mode(request, lib):
                                        "tile67", "tile67+split3", "tile63+split2", "norm+tile81", "norm+tile82",
                                        "norm+tile83", "norm+tile84", "norm+tile81+split3", "norm+tile83+split2",
                                        "norm+tile31", "norm+heuristic", "tile81", "tile82", "tile83", "tile84",
-                                       "tile88", "norm+tile88",
+                                       "tile88", "norm+tile88", "tile85", "norm+tile85", "tile85+split3",
+                                       "norm+tile85+split2",
                                        "tile81+split3", "heuristic+wtile26", "heuristic+wtile27",
                                        "heuristic+wtile126", "heuristic+wtile130", "heuristic+wtile132",
                                        "heuristic+wtile110", "heuristic+wtile112",

@@ -304,9 +304,12 @@ def test_train_mode_input_gradient_vs_reference(precision):
     """x.grad through a train-mode forward (the reference's autograd gives it
     whenever the input requires grad): unet_plan_input_grad materialises
     inc.c0's BatchNorm backward and correlates it with inc.c0's weights.
-    Against the reference arithmetic in fp64 (BatchNorm on batch statistics);
-    bf16 GEMMs within 3 % rel-L2 (a bf16 dgrad chain), fp32 within the
-    parameter gradients' bar max(1e-2, 2 x the reference's own fp32 error)."""
+    fp32: against the reference arithmetic in fp64 (BatchNorm on batch
+    statistics) within the parameter gradients' bar max(1e-2, 2 x the
+    reference's own fp32 error).  bf16: the input gradient is ill-conditioned
+    under bf16 GEMM operands (BatchNorm's backward cancels its mean terms; the
+    bf16 oracle itself lands 0.42 rel-L2 from fp64), so against the bf16 oracle
+    (tests/test_gpu_bf16.py's bar: max(2e-2, 3 x its fp32-vs-fp64 floor))."""
     from oracle import torch_cpu_ref as R
     from unet_amd import WeightedCrossEntropyLoss
     m, params = _model(87)
@@ -316,17 +319,26 @@ def test_train_mode_input_gradient_vs_reference(precision):
     xd = torch.from_numpy(x).cuda().requires_grad_(True)
     loss = WeightedCrossEntropyLoss()(m(xd), torch.from_numpy(tgt).cuda(), torch.from_numpy(wmap).cuda())
     loss.backward()
-    refs = {}
-    for dt in (torch.float64, torch.float32):
-        net = R.TorchCpuUNet(params, dtype=dt, training=True)
-        xr = torch.from_numpy(x).to(dt).requires_grad_(True)
-        lo = R.weighted_ce(net.forward(xr), torch.from_numpy(tgt), torch.from_numpy(wmap).to(dt))
-        lo.backward()
-        refs[dt] = xr.grad.double().numpy()
     g = xd.grad.double().cpu().numpy()
-    e = _rel(g, refs[torch.float64])
-    # the parameter gradients' bar (rel-L2 <= 1e-2, or twice the
-    # reference's own fp32 error); measured fp32 1.1e-3
-    tol = 3e-2 if precision == "bf16" else max(1e-2, 2 * _rel(refs[torch.float32], refs[torch.float64]))
+    if precision == "bf16":
+        refs = {}
+        for dt in (np.float64, np.float32):
+            net = O.UNetOracle(params, dtype=dt, gemm="bf16")
+            rl, cache, _ = net.forward(x)
+            _, rdl = O.weighted_ce(rl, tgt, wmap)
+            refs[dt] = net.backward(np.asarray(rdl, dt), cache, input_grad=True)[1].astype(np.float64)
+        e = _rel(g, refs[np.float64])
+        tol = max(2e-2, 3 * _rel(refs[np.float32], refs[np.float64]))
+    else:
+        refs = {}
+        for dt in (torch.float64, torch.float32):
+            net = R.TorchCpuUNet(params, dtype=dt, training=True)
+            xr = torch.from_numpy(x).to(dt).requires_grad_(True)
+            lo = R.weighted_ce(net.forward(xr), torch.from_numpy(tgt), torch.from_numpy(wmap).to(dt))
+            lo.backward()
+            refs[dt] = xr.grad.double().numpy()
+        e = _rel(g, refs[torch.float64])
+        # the parameter gradients' bar; measured fp32 1.1e-3
+        tol = max(1e-2, 2 * _rel(refs[torch.float32], refs[torch.float64]))
     assert e <= tol, (precision, e, tol)
     print(f"train-mode input gradient ({precision}): rel-L2 {e:.2e} (tol {tol:.2e})")

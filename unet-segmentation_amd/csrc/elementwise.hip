@@ -688,8 +688,12 @@ hipError_t launch_bnb_apply(const float* dz, const float* y, const float* coef, 
   const int gx = (int)((rowlen + 255) / 256);
   // ~4 rows per block keeps the row loop short while filling the chip
   const dim3 grid(gx, (unsigned)std::max<long long>(1, std::min<long long>(rows, std::max<long long>(1, 32768 / gx))));
-  if (dz_h16) {  // bf16 plans: dz, y and dYpad all bf16
-    if (!out_h16 || !y_h16) return hipErrorInvalidValue;
+  if (dz_h16) {  // bf16 plans: dz and y bf16; dYpad bf16 (fp32 only for the input gradient's dY(0))
+    if (!y_h16) return hipErrorInvalidValue;
+    if (!out_h16) {
+      hipLaunchKernelGGL((k_bnb_apply<0, 1, 1>), grid, dim3(256), 0, s, dz, y, coef, n, h, w, c, dypad, pad);
+      return hipGetLastError();
+    }
     if (c % 8 == 0) {
       const long long rl8 = (long long)(w + 2 * pad) * (c / 8);
       const int gx8 = (int)((rl8 + 255) / 256);

@@ -19,12 +19,17 @@
 #include <cstdlib>
 
 #include "gemm_common.h"
+#include "ring_common.h"
 
 namespace unet {
 // convT weight gradient on an LDS-DMA ring of pixel stages (wgradT_ring.hip,
 // wgrad tiles 40-43)
 bool wgradT_ring_fits(const WgradArgs& a, int tile);
 hipError_t go_wgradT_ring(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
+// conv3_flat.hip (tile 85: the ring on flat pixel tiles)
+bool conv3_flat_fits(const IgemmArgs& a, int tile);
+long long conv3_flat_tiles(const IgemmArgs& a);
+hipError_t go_conv3_flat_tile(const IgemmArgs& a, hipStream_t s, int tile);
 
 // Occupancy the register allocator must preserve: as many workgroups as the
 // LDS footprint admits per CU (without it hipcc moves the accumulators to
@@ -63,8 +68,10 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   // batched dense GEMMs (Winograd points): rows of batch z are z*batch_rows ..
-  const int zb = args.batch > 1 ? (int)blockIdx.z : 0;
-  const int m0 = zb * args.batch_rows + blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int bx, by, bz;  // XCD-aware grid order: an XCD's run shares the B panels (and a batch entry) in its L2
+  xcd_block(bx, by, bz);
+  const int zb = args.batch > 1 ? bz : 0;
+  const int m0 = zb * args.batch_rows + bx * BM, n0 = by * BN;
   const Gather& g = args.a;
   const int M = args.batch > 1 ? (zb + 1) * args.batch_rows : args.M, K = args.K;
   // staging row of this thread.  With BK = 16 a row is 4 x 16 B and the 8 lanes
@@ -97,7 +104,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   int kc0 = 0, kc1 = nk_all;
   if (args.ksplit > 1 && args.batch <= 1) {
     const int per = (nk_all + args.ksplit - 1) / args.ksplit;
-    kc0 = blockIdx.z * per;
+    kc0 = bz * per;
     kc1 = min(nk_all, kc0 + per);
   }
   // K iterator (uniform): chunk -> (tap_y, tap_x, c0).  A chunk never straddles
@@ -258,7 +265,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_minw(BM, BN, WM, WN, BK)) void 
   }
 
   __shared__ float red[WM * 3 * BN];
-  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, red, LinearRows{m0, M});
+  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, red, LinearRows{m0, M}, nullptr, bz);
 }
 
 
@@ -314,7 +321,9 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_g_minw(BM, BN, WM, WN)) void k_
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  int bx, by, bz;  // XCD-aware grid order
+  xcd_block(bx, by, bz);
+  const int m0 = bx * BM, n0 = by * BN;
   const Gather& g = args.a;
   const int M = args.M, K = args.K, Cg = g.Cg;
   const int lrow = lane >> 2, lslot = lane & 3;
@@ -358,7 +367,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_g_minw(BM, BN, WM, WN)) void k_
   int kc0 = 0, kc1 = nk_all;
   if (args.ksplit > 1) {
     const int per = (nk_all + args.ksplit - 1) / args.ksplit;
-    kc0 = blockIdx.z * per;
+    kc0 = bz * per;
     kc1 = min(nk_all, kc0 + per);
   }
   // producer-side K iterator (issue runs two steps ahead of compute)
@@ -452,7 +461,7 @@ __global__ __launch_bounds__(WM * WN * 64, igemm_g_minw(BM, BN, WM, WN)) void k_
     slot = slot == 2 ? 0 : slot + 1;
   }
   __syncthreads();  // the ring is reused as the epilogue's reduction buffer
-  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, dl);
+  igemm_finish<BM, BN, WM, WN, NT>(args, acc, m0, n0, wm, wn, tid, dl, LinearRows{0, 0}, nullptr, bz);
 }
 
 template <int BM, int BN>
@@ -946,10 +955,12 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int i0 = blockIdx.x * BM, j0 = blockIdx.y * BN;
+  int bx, by, bz;  // XCD-aware grid order: an XCD's run shares a pixel split's panels in its L2
+  xcd_block(bx, by, bz);
+  const int i0 = bx * BM, j0 = by * BN;
   const int nz = gridDim.z / args.batch;  // pixel splits per batch entry
-  const int zb = blockIdx.z / nz;
-  const int pbeg = (blockIdx.z - zb * nz) * args.pix_per_split;
+  const int zb = bz / nz;
+  const int pbeg = (bz - zb * nz) * args.pix_per_split;
   const int pend = min(args.P, pbeg + args.pix_per_split);
   const Gather& ga = args.ga;
   const Gather& gb = args.gb;
@@ -1056,7 +1067,7 @@ __global__ __launch_bounds__(256, 2) void k_wgrad(const WgradArgs args) {
   // accumulate the tile into out (fp32 atomics; the output is small next to the
   // reduction), or (slab mode, batch 1) store this split's partial for
   // launch_slab_reduce
-  float* const plane = args.slab ? args.slab + (size_t)blockIdx.z * args.Mo * args.No : nullptr;
+  float* const plane = args.slab ? args.slab + (size_t)bz * args.Mo * args.No : nullptr;
 #pragma unroll
   for (int i = 0; i < TM; ++i)
 #pragma unroll
@@ -1181,6 +1192,8 @@ static TileInfo tile_info(int id) {
     case 82: return {256, 64, 288, 2};
     case 83: return {128, 128, 288, 3};
     case 84: return {256, 64, 576, 1};
+    // the ring on flat tiles of 256 consecutive pixels (k_conv3_flat, conv3_flat.hip)
+    case 85: return {256, 128, 576, 1};
     // 84 persistent (k_conv3_ring PT): whole K per workgroup
     case 88: return {256, 64, 576, 1};
     // bf16 convT forward / input gradient on LDS-DMA K rings (k_gemm_ring,
@@ -1214,7 +1227,7 @@ static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 
 static bool is_ring_tile(int tile) { return (tile >= 81 && tile <= 84) || tile == 88; }
 static bool is_gemm_ring_tile(int tile) { return tile >= 91 && tile <= 99; }
 static bool is_bf16_tile(int tile) {
-  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile) ||
+  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile) || tile == 85 ||
          is_gemm_ring_tile(tile);
 }
 static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
@@ -1238,6 +1251,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
   if (is_ring_tile(tile)) return conv3_ring_fits(a, tile);
+  if (tile == 85) return conv3_flat_fits(a, tile);
   if (is_gemm_ring_tile(tile)) return gemm_ring_fits(a, tile);
   if (tile == 70 || tile == 71 || tile == 74) return wino_applies(a, tile == 70 ? 2 : tile == 71 ? 4 : 6);
   if (tile == 72) return wino_fused_applies(a);
@@ -1262,6 +1276,7 @@ long long igemm_tile_count(const IgemmArgs& a, int tile) {
   const TileInfo t = tile_info(tile);
   if (t.bm == 0) return 0;
   int th, tw, bn, ch;
+  if (tile == 85) return conv3_flat_tiles(a);
   if (halo_tile_shape(tile, th, tw, bn))
     return (long long)a.a.nimg * ((a.a.Hg + th - 1) / th) * ((a.a.Wg + tw - 1) / tw) * (a.N / bn);
   if (conv3_dma_tile_shape(tile, th, bn, ch) || conv3_ring_tile_shape(tile, th, bn, ch))
@@ -1344,6 +1359,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
     case 63: case 65: case 66: case 67: case 68: return go_conv3_dma_tile(a, s, tile);
     case 81: case 82: case 83: case 84: case 88: return go_conv3_ring_tile(a, s, tile);
+    case 85: return go_conv3_flat_tile(a, s, tile);
     case 91: case 92: case 93: case 94: case 95: case 96: case 97: case 98: case 99:
       return go_gemm_ring_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);

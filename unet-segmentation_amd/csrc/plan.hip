@@ -302,7 +302,7 @@ constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 // Version of the GEMM variant tables (tile ids and their kernels): part of every
 // tuning key, so a database written by a build with another tile set is never
 // replayed (its lines simply miss).  Bump whenever a tile id changes meaning.
-constexpr int kTileTableVersion = 13;
+constexpr int kTileTableVersion = 14;
 
 std::string igemm_key(const IgemmArgs& a) {
   char b[240], small[16] = "";
@@ -368,7 +368,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
   std::vector<GemmChoice> v;
   const long long cus = num_cus();
   for (int t : {4, 1, 2, 8, 6, 3, 9, 7, 11, 12, 13, 14, 51, 52, 53, 54, 21, 22, 23, 24, 25, 26, 31, 32, 33, 34, 35,
-                36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 81, 82, 83, 84, 70, 71, 72, 73,
+                36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 81, 82, 83, 84, 85, 70, 71, 72, 73,
                 74, 75, 76, 77, 88, 91, 92, 93, 94, 95, 96, 97, 98, 99}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t) || tune_skipped(t)) continue;
     v.push_back({t, 1});
@@ -1417,7 +1417,8 @@ int unet_plan_input_grad(unet_plan* p, void* const* prm, float* dx, void* ws, vo
   const Conv& L = p->L[0];
   const int g16 = p->prec == UNET_PREC_BF16;
   float* dy0 = reinterpret_cast<float*>(scratch);
-  CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), p->n, L.ho, L.wo, L.co, dy0, 0, s, 0, g16, g16));
+  CK(launch_bnb_apply(c.f(L.dz), c.f(L.y), c.f(L.coef), p->n, L.ho, L.wo, L.co, dy0, 0, s, 0,
+                      p->prec == UNET_PREC_BF16, g16));
   CK(launch_conv_first_dgrad(dy0, p->n, p->cin, p->h, p->w, P<float>(prm, L.pw), dx, s));
   return 0;
 }
