@@ -498,7 +498,7 @@ def gemm_mode(request, lib):
                                        "tile67", "tile67+split3", "tile63+split2", "norm+tile81", "norm+tile82",
                                        "norm+tile83", "norm+tile84", "norm+tile81+split3", "norm+tile83+split2",
                                        "norm+tile31", "norm+heuristic", "tile81", "tile82", "tile83", "tile84",
-                                       "tile88", "norm+tile88", "tile85", "norm+tile85", "tile85+split3",
+                                       "tile88", "norm+tile88", "tile85", "norm+tile85", "tile85+split3", "tile86", "norm+tile86",
                                        "norm+tile85+split2",
                                        "tile81+split3", "heuristic+wtile26", "heuristic+wtile27",
                                        "heuristic+wtile126", "heuristic+wtile130", "heuristic+wtile132",

@@ -28,7 +28,7 @@ bool wgradT_ring_fits(const WgradArgs& a, int tile);
 hipError_t go_wgradT_ring(const WgradArgs& a, hipStream_t s, int tile, int per_cu);
 // conv3_flat.hip (tile 85: the ring on flat pixel tiles)
 bool conv3_flat_fits(const IgemmArgs& a, int tile);
-long long conv3_flat_tiles(const IgemmArgs& a);
+long long conv3_flat_tiles(const IgemmArgs& a, int tile);
 hipError_t go_conv3_flat_tile(const IgemmArgs& a, hipStream_t s, int tile);
 
 // Occupancy the register allocator must preserve: as many workgroups as the
@@ -1194,6 +1194,8 @@ static TileInfo tile_info(int id) {
     case 84: return {256, 64, 576, 1};
     // the ring on flat tiles of 256 consecutive pixels (k_conv3_flat, conv3_flat.hip)
     case 85: return {256, 128, 576, 1};
+    // 85 stream-K: one workgroup per CU, equal runs of (tile, column block, chunk) units
+    case 86: return {256, 128, 576, 1};
     // 84 persistent (k_conv3_ring PT): whole K per workgroup
     case 88: return {256, 64, 576, 1};
     // bf16 convT forward / input gradient on LDS-DMA K rings (k_gemm_ring,
@@ -1227,7 +1229,7 @@ static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 
 static bool is_ring_tile(int tile) { return (tile >= 81 && tile <= 84) || tile == 88; }
 static bool is_gemm_ring_tile(int tile) { return tile >= 91 && tile <= 99; }
 static bool is_bf16_tile(int tile) {
-  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile) || tile == 85 ||
+  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile) || tile == 85 || tile == 86 ||
          is_gemm_ring_tile(tile);
 }
 static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
@@ -1251,7 +1253,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
     return prec_ok && a.N % t.bn == 0 && a.a.taps_h == 3 && a.a.taps_w == 3 && a.a.stride == 1 &&
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
   if (is_ring_tile(tile)) return conv3_ring_fits(a, tile);
-  if (tile == 85) return conv3_flat_fits(a, tile);
+  if (tile == 85 || tile == 86) return conv3_flat_fits(a, tile);
   if (is_gemm_ring_tile(tile)) return gemm_ring_fits(a, tile);
   if (tile == 70 || tile == 71 || tile == 74) return wino_applies(a, tile == 70 ? 2 : tile == 71 ? 4 : 6);
   if (tile == 72) return wino_fused_applies(a);
@@ -1276,7 +1278,7 @@ long long igemm_tile_count(const IgemmArgs& a, int tile) {
   const TileInfo t = tile_info(tile);
   if (t.bm == 0) return 0;
   int th, tw, bn, ch;
-  if (tile == 85) return conv3_flat_tiles(a);
+  if (tile == 85 || tile == 86) return conv3_flat_tiles(a, tile);
   if (halo_tile_shape(tile, th, tw, bn))
     return (long long)a.a.nimg * ((a.a.Hg + th - 1) / th) * ((a.a.Wg + tw - 1) / tw) * (a.N / bn);
   if (conv3_dma_tile_shape(tile, th, bn, ch) || conv3_ring_tile_shape(tile, th, bn, ch))
@@ -1359,7 +1361,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 41: case 42: case 43: case 44: return go_igemm_bf16(a, s, tile);
     case 63: case 65: case 66: case 67: case 68: return go_conv3_dma_tile(a, s, tile);
     case 81: case 82: case 83: case 84: case 88: return go_conv3_ring_tile(a, s, tile);
-    case 85: return go_conv3_flat_tile(a, s, tile);
+    case 85: case 86: return go_conv3_flat_tile(a, s, tile);
     case 91: case 92: case 93: case 94: case 95: case 96: case 97: case 98: case 99:
       return go_gemm_ring_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);

@@ -28,6 +28,7 @@ using namespace unet;
 
 namespace unet {
 extern int g_wino_max, g_wino_dgrad_max, g_wino_wgrad_max, g_wino4_fwd_min_cg, g_wino4_fwd_small_cg;  // igemm.hip (Winograd tile caps)
+size_t conv3_flat_sk_slab_bytes(const IgemmArgs& a);  // conv3_flat.hip (tile 86: stream-K partial slots)
 // unet_set_tuning("autotune", v) or UNET_AUTOTUNE (default on)
 int g_autotune = getenv("UNET_AUTOTUNE") ? atoi(getenv("UNET_AUTOTUNE")) : 1;
 // unet_set_tuning("concurrent", v) or UNET_CONCURRENT (default on): weight
@@ -371,13 +372,16 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
                 36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 81, 82, 83, 84, 85, 70, 71, 72, 73,
                 74, 75, 76, 77, 88, 91, 92, 93, 94, 95, 96, 97, 98, 99}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t) || tune_skipped(t)) continue;
+    // (86, the stream-K form of 85, is forced only: measured slower on every
+    // bottleneck shape but one, where it tied -- DESIGN.md §13)
+    if (t == 86 && conv3_flat_sk_slab_bytes(a) > slab_bytes) continue;  // stream-K partial slots
     v.push_back({t, 1});
     if (t == 70 || t == 71 || t == 74)  // Winograd: no K split; the tile of its batched point GEMMs
       for (int inner : {1, 2, 3, 4, 6, 7, 8, 9}) v.push_back({t, 100 + inner});
     // Winograd (70-77) and the persistent ring 88 take no K split; the LDS-DMA
     // rings 81-84 (3x3) and 91-99 (convT) do (the 24-48^2
     // bottleneck grids give them 144-192 workgroups for 256 CUs)
-    if ((t >= 70 && t <= 77) || t == 88) continue;
+    if ((t >= 70 && t <= 77) || t == 88 || t == 86) continue;
     const long long cnt = igemm_tile_count(a, t);
     const long long slots = (long long)igemm_tile_slots(t) * cus;
     if (cnt >= 4 * slots || a.N % 64 != 0) continue;  // enough workgroup rounds already
@@ -472,7 +476,9 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
     const int ks = unet::g_force_split > 1 ? unet::g_force_split : 1;
     if (igemm_slab_bytes(a, ks) > c.p->slab.bytes) return GemmChoice{};
     if (unet::g_force_tile > 0) {
-      if (igemm_tile_fits(a, unet::g_force_tile)) return GemmChoice{unet::g_force_tile, ks};
+      if (igemm_tile_fits(a, unet::g_force_tile) &&
+          (unet::g_force_tile != 86 || (ks == 1 && conv3_flat_sk_slab_bytes(a) <= c.p->slab.bytes)))
+        return GemmChoice{unet::g_force_tile, ks};
     }
     for (int t : {4, 1, 2, 8, 21, 22, 24, 23})
       if (igemm_tile_fits(a, t)) return GemmChoice{t, ks};
@@ -488,7 +494,8 @@ GemmChoice choose_igemm(const Ctx& c, const IgemmArgs& a) {
     // database from another tile set, or a split whose partials no longer fit
     // the slab): otherwise it is dropped and the shape re-tuned
     const GemmChoice g = it->second;
-    const bool slab_ok = g.tile >= 70 || igemm_slab_bytes(a, g.split) <= c.p->slab.bytes;  // Winograd: split = inner tile
+    const bool slab_ok = g.tile == 86 ? conv3_flat_sk_slab_bytes(a) <= c.p->slab.bytes
+                                      : g.tile >= 70 || igemm_slab_bytes(a, g.split) <= c.p->slab.bytes;  // Winograd: split = inner tile
     if (g.tile < 0 || (igemm_tile_fits(a, g.tile) && slab_ok)) return g;
     g_tuned.erase(it);
     g_tune_log.erase(key);
