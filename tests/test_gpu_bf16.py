@@ -291,6 +291,48 @@ def test_bf16_flat_tile_bitexact_vs_ring(op_bf16, kind, n, h, w, ci, co):
     assert torch.equal(outs[0], outs[1]), float((outs[0] - outs[1]).abs().max())
 
 
+@pytest.mark.parametrize("kind", ["fwd", "fwd_tf", "dgrad"])
+@pytest.mark.parametrize("n,h,w", [(2, 12, 11), (1, 40, 70), (8, 130, 131), (3, 9, 200)])
+def test_bf16_conv3x3_c64_resident_weights(op_bf16, kind, n, h, w):
+    """Tile 87 (conv3_c64.hip: 64 -> 64 channels, the weight slab resident in
+    LDS, persistent workgroups walking double-buffered halo tiles) against the
+    bf16-operand oracle: forward with and without the consumer BN+ReLU applied
+    in LDS, and the input gradient; grids with fewer and with more tiles (680)
+    than workgroups, ragged in both axes."""
+    lib = op_bf16
+    ci = co = 64
+    lib.unet_set_tuning(b"op_a16", 1)
+    try:
+        lib.unet_set_tuning(b"igemm_variant", 87)
+        rng = np.random.default_rng(h * 7 + w)
+        x = f32(rng.standard_normal((n, h, w, ci)))
+        wt = f32(rng.standard_normal((co, ci, 3, 3)) / np.sqrt(9 * ci))
+        ws = torch.empty(lib.unet_conv_ws_bytes(n, h, w, ci, co), dtype=torch.uint8, device="cuda")
+        if kind == "dgrad":
+            dy = f32(rng.standard_normal((n, h - 2, w - 2, co)))
+            ref, _, _ = O.conv_valid_bwd(x, q(wt), q(dy))
+            out = torch.full((n, h, w, ci), float("nan"), device="cuda")
+            ck(lib.unet_conv3x3_dgrad(dev(dy).data_ptr(), n, h, w, ci, dev(wt).data_ptr(), co, out.data_ptr(),
+                                      ws.data_ptr(), stream()))
+        else:
+            tf = kind == "fwd_tf"
+            b = f32(rng.standard_normal(co))
+            sc = f32(rng.uniform(-0.5, 1.5, ci)) if tf else None
+            sh = f32(rng.standard_normal(ci) * 0.3) if tf else None
+            xq = f32(q(x))
+            xin = np.maximum(f32(xq * sc + sh), 0) if tf else xq
+            ref = O.conv_valid_fwd(q(xin), q(wt), b)
+            out = torch.full((n, h - 2, w - 2, co), float("nan"), device="cuda")
+            ck(lib.unet_conv3x3_fwd(dev(x).data_ptr(), n, h, w, ci, dev(wt).data_ptr(), dev(b).data_ptr(), co,
+                                    dev(sc).data_ptr() if tf else None, dev(sh).data_ptr() if tf else None,
+                                    out.data_ptr(), ws.data_ptr(), stream()))
+        torch.cuda.synchronize()
+        assert rel_err(host(out), ref) < 5e-5
+    finally:
+        lib.unet_set_tuning(b"op_a16", 0)
+        lib.unet_set_tuning(b"igemm_variant", -1)
+
+
 @pytest.mark.parametrize("variant", DMA)
 @pytest.mark.parametrize("n,h,w,ci,co", [(2, 12, 11, 64, 64), (1, 19, 40, 128, 64), (2, 8, 8, 64, 256),
                                          (1, 36, 66, 64, 128)])
@@ -498,7 +540,7 @@ def gemm_mode(request, lib):
                                        "tile67", "tile67+split3", "tile63+split2", "norm+tile81", "norm+tile82",
                                        "norm+tile83", "norm+tile84", "norm+tile81+split3", "norm+tile83+split2",
                                        "norm+tile31", "norm+heuristic", "tile81", "tile82", "tile83", "tile84",
-                                       "tile88", "norm+tile88", "tile85", "norm+tile85", "tile85+split3", "tile86", "norm+tile86",
+                                       "tile88", "norm+tile88", "tile85", "norm+tile85", "tile85+split3", "tile86", "norm+tile86", "tile87", "norm+tile87",
                                        "norm+tile85+split2",
                                        "tile81+split3", "heuristic+wtile26", "heuristic+wtile27",
                                        "heuristic+wtile126", "heuristic+wtile130", "heuristic+wtile132",

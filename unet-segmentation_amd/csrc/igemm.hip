@@ -30,6 +30,10 @@ hipError_t go_wgradT_ring(const WgradArgs& a, hipStream_t s, int tile, int per_c
 bool conv3_flat_fits(const IgemmArgs& a, int tile);
 long long conv3_flat_tiles(const IgemmArgs& a, int tile);
 hipError_t go_conv3_flat_tile(const IgemmArgs& a, hipStream_t s, int tile);
+// conv3_c64.hip (tile 87: 64 -> 64 channels, resident weights, persistent)
+bool conv3_c64_fits(const IgemmArgs& a);
+long long conv3_c64_tiles(const IgemmArgs& a);
+hipError_t go_conv3_c64(const IgemmArgs& a, hipStream_t s);
 
 // Occupancy the register allocator must preserve: as many workgroups as the
 // LDS footprint admits per CU (without it hipcc moves the accumulators to
@@ -1196,6 +1200,8 @@ static TileInfo tile_info(int id) {
     case 85: return {256, 128, 576, 1};
     // 85 stream-K: one workgroup per CU, equal runs of (tile, column block, chunk) units
     case 86: return {256, 128, 576, 1};
+    // 64 -> 64 channels with the weights resident in LDS (k_conv3_c64, conv3_c64.hip): persistent
+    case 87: return {256, 64, 576, 1};
     // 84 persistent (k_conv3_ring PT): whole K per workgroup
     case 88: return {256, 64, 576, 1};
     // bf16 convT forward / input gradient on LDS-DMA K rings (k_gemm_ring,
@@ -1229,7 +1235,7 @@ static bool is_dma_tile(int tile) { return tile == 63 || (tile >= 65 && tile <= 
 static bool is_ring_tile(int tile) { return (tile >= 81 && tile <= 84) || tile == 88; }
 static bool is_gemm_ring_tile(int tile) { return tile >= 91 && tile <= 99; }
 static bool is_bf16_tile(int tile) {
-  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile) || tile == 85 || tile == 86 ||
+  return (tile >= 21 && tile <= 26) || is_halo_tile(tile) || is_dma_tile(tile) || is_ring_tile(tile) || tile == 85 || tile == 86 || tile == 87 ||
          is_gemm_ring_tile(tile);
 }
 static bool is_halo32_tile(int tile) { return tile >= 51 && tile <= 54; }
@@ -1254,6 +1260,7 @@ bool igemm_tile_fits(const IgemmArgs& a, int tile) {
            a.K == 9 * a.a.Cg && a.a.Cg % 32 == 0 && a.a.c_split % 32 == 0 && a.a.Cg <= 1024;
   if (is_ring_tile(tile)) return conv3_ring_fits(a, tile);
   if (tile == 85 || tile == 86) return conv3_flat_fits(a, tile);
+  if (tile == 87) return conv3_c64_fits(a);
   if (is_gemm_ring_tile(tile)) return gemm_ring_fits(a, tile);
   if (tile == 70 || tile == 71 || tile == 74) return wino_applies(a, tile == 70 ? 2 : tile == 71 ? 4 : 6);
   if (tile == 72) return wino_fused_applies(a);
@@ -1279,6 +1286,7 @@ long long igemm_tile_count(const IgemmArgs& a, int tile) {
   if (t.bm == 0) return 0;
   int th, tw, bn, ch;
   if (tile == 85 || tile == 86) return conv3_flat_tiles(a, tile);
+  if (tile == 87) return conv3_c64_tiles(a);
   if (halo_tile_shape(tile, th, tw, bn))
     return (long long)a.a.nimg * ((a.a.Hg + th - 1) / th) * ((a.a.Wg + tw - 1) / tw) * (a.N / bn);
   if (conv3_dma_tile_shape(tile, th, bn, ch) || conv3_ring_tile_shape(tile, th, bn, ch))
@@ -1362,6 +1370,7 @@ static hipError_t go_tile(const IgemmArgs& a, hipStream_t s, int tile) {
     case 63: case 65: case 66: case 67: case 68: return go_conv3_dma_tile(a, s, tile);
     case 81: case 82: case 83: case 84: case 88: return go_conv3_ring_tile(a, s, tile);
     case 85: case 86: return go_conv3_flat_tile(a, s, tile);
+    case 87: return go_conv3_c64(a, s);
     case 91: case 92: case 93: case 94: case 95: case 96: case 97: case 98: case 99:
       return go_gemm_ring_tile(a, s, tile);
     case 70: return launch_wino(a, s, 2);

@@ -303,7 +303,7 @@ constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 // Version of the GEMM variant tables (tile ids and their kernels): part of every
 // tuning key, so a database written by a build with another tile set is never
 // replayed (its lines simply miss).  Bump whenever a tile id changes meaning.
-constexpr int kTileTableVersion = 14;
+constexpr int kTileTableVersion = 15;
 
 std::string igemm_key(const IgemmArgs& a) {
   char b[240], small[16] = "";
@@ -372,8 +372,9 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
                 36, 41, 42, 43, 44, 63, 65, 66, 67, 68, 81, 82, 83, 84, 85, 70, 71, 72, 73,
                 74, 75, 76, 77, 88, 91, 92, 93, 94, 95, 96, 97, 98, 99}) {  // fits() filters by precision and gather
     if (!igemm_tile_fits(a, t) || tune_skipped(t)) continue;
-    // (86, the stream-K form of 85, is forced only: measured slower on every
-    // bottleneck shape but one, where it tied -- DESIGN.md §13)
+    // (86, the stream-K form of 85, and 87, the resident-weight 64-channel
+    // kernel, are forced only: measured slower on the shapes they target --
+    // DESIGN.md §13)
     if (t == 86 && conv3_flat_sk_slab_bytes(a) > slab_bytes) continue;  // stream-K partial slots
     v.push_back({t, 1});
     if (t == 70 || t == 71 || t == 74)  // Winograd: no K split; the tile of its batched point GEMMs
@@ -381,7 +382,7 @@ std::vector<GemmChoice> igemm_candidates(const IgemmArgs& a, size_t slab_bytes) 
     // Winograd (70-77) and the persistent ring 88 take no K split; the LDS-DMA
     // rings 81-84 (3x3) and 91-99 (convT) do (the 24-48^2
     // bottleneck grids give them 144-192 workgroups for 256 CUs)
-    if ((t >= 70 && t <= 77) || t == 88 || t == 86) continue;
+    if ((t >= 70 && t <= 77) || t == 88 || t == 86 || t == 87) continue;
     const long long cnt = igemm_tile_count(a, t);
     const long long slots = (long long)igemm_tile_slots(t) * cus;
     if (cnt >= 4 * slots || a.N % 64 != 0) continue;  // enough workgroup rounds already

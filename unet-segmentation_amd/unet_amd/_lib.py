@@ -154,7 +154,7 @@ def stream_of(device=None):
 # csrc/Makefile SRC_HASH: sha256 over these files, in this order
 _HASHED = ["igemm.hip", "igemm_bf16.hip", "conv3_dma.hip", "conv3_ring.hip", "winograd.hip", "elementwise.hip", "elastic.hip",
            "tiling.hip", "weightmap.hip", "postproc.hip", "track.hip", "ops.hip", "plan.hip", "wgrad3_ring.hip",
-           "conv3_ring_pt.hip", "peak.hip", "gemm_ring.hip", "wgradT_ring.hip", "conv3_flat.hip", "unet_internal.h", "gemm_common.h", "ring_common.h", "conv3_ring_kernel.h",
+           "conv3_ring_pt.hip", "peak.hip", "gemm_ring.hip", "wgradT_ring.hip", "conv3_flat.hip", "conv3_c64.hip", "unet_internal.h", "gemm_common.h", "ring_common.h", "conv3_ring_kernel.h",
            os.path.join("..", "..", "include", "unet_hip.h")]
 
 
