@@ -303,7 +303,7 @@ constexpr size_t kSlabBudget = 256ull << 20;  // split-K partials (fp32)
 // Version of the GEMM variant tables (tile ids and their kernels): part of every
 // tuning key, so a database written by a build with another tile set is never
 // replayed (its lines simply miss).  Bump whenever a tile id changes meaning.
-constexpr int kTileTableVersion = 15;
+constexpr int kTileTableVersion = 14;
 
 std::string igemm_key(const IgemmArgs& a) {
   char b[240], small[16] = "";
