@@ -351,7 +351,13 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  partials summed in a fixed order) and inc.c0's slab
  *                  reduction runs in one pass: plan steps are
  *                  bit-reproducible run to run (see
- *                  unet_nondeterministic_sites). */
+ *                  unet_nondeterministic_sites).
+ *  "bnb_fuse"      1 (env UNET_BNB_FUSE=1) = fp32 plans form the
+ *                  BatchNorm-backward dY of a layer whose weight gradient runs
+ *                  Winograd F(6x6) in one pass with that weight gradient's dY
+ *                  transform (see unet_fused_bnb_sites); 0 (default) = the
+ *                  two-pass form (bit-identical results; faster with the
+ *                  concurrent weight-gradient stream). */
 int unet_set_tuning(const char* key, int value);
 /* Text report of the tuned GEMM choices (one line per shape: key, heuristic
  * time, chosen variant and time).  Copies up to len-1 bytes + NUL into buf
@@ -368,6 +374,12 @@ long long unet_slab_fallbacks(int reset);
  * atomic-free variant and ran with fp32 atomics; reset != 0 also zeroes the
  * count.  0 after a step means the step is bit-reproducible. */
 long long unet_nondeterministic_sites(int reset);
+/* Layer backward steps of fp32 plans whose BatchNorm-backward dY was formed by
+ * the fused apply + F(6x6) dY-transform pass (unet_set_tuning "bnb_fuse")
+ * instead of the standalone apply pass; reset != 0 also zeroes the count.
+ * Replaces nothing in the reference: it is a counter of this implementation's
+ * schedule (models/unet_model.py:12,16 is the BatchNorm2d it differentiates). */
+long long unet_fused_bnb_sites(int reset);
 /* Tuning database (cf. MIOpen's perf-db): unet_tuning_save writes every tuned
  * choice as "key<TAB>tile<TAB>split" lines (returns the count or -errno);
  * unet_tuning_load merges such a file, overriding equal keys (returns the

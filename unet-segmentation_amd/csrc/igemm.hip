@@ -1581,6 +1581,21 @@ bool wgrad_slab_fits(const WgradArgs& a, int splits) {
 
 hipError_t launch_wgrad(const WgradArgs& a, hipStream_t s) { return launch_wgrad_v(a, s, GemmChoice{}); }
 
+// The Winograd tile (mt = 4 / 6) launch_wgrad_v(a, s, c) runs for an fp32
+// launch, 0 if it runs another kernel (the same resolution of forced and
+// heuristic tiles as launch_wgrad_v)
+int wgrad_winograd_mt(const WgradArgs& a, GemmChoice c) {
+  if (a.bf16) return 0;
+  int tile = c.tile;
+  if (tile < 0) {
+    if ((g_tune_wgrad == 71 || g_tune_wgrad == 74) && wgrad_tile_fits(a, g_tune_wgrad)) tile = g_tune_wgrad;
+    else if ((g_tune_wgrad == 1071 || g_tune_wgrad == 1074) && wgrad_tile_fits(a, g_tune_wgrad - 1000))
+      tile = g_tune_wgrad - 1000;
+  }
+  if ((tile == 71 || tile == 74) && wgrad_tile_fits(a, tile)) return tile == 71 ? 4 : 6;
+  return 0;
+}
+
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c) {
   int t = c.tile;
   if (t < 0 && g_tune_igemm >= 70 && g_tune_igemm <= 77 && igemm_tile_fits(a, g_tune_igemm)) t = g_tune_igemm;

@@ -61,6 +61,17 @@ int g_force_tile = 0;
 // unet_nondeterministic_sites().
 int g_deterministic = getenv("UNET_DETERMINISTIC") ? atoi(getenv("UNET_DETERMINISTIC")) : 0;
 std::atomic<long long> g_nondet_sites{0};
+// unet_set_tuning("bnb_fuse", v) or UNET_BNB_FUSE (default off): fp32 plans form
+// dY of a layer whose weight gradient runs Winograd F(6x6) in one pass with
+// that weight gradient's dY transform (k_bnb_wino6_dy) instead of k_bnb_apply
+// + k_wino6_dy (bit-identical results).  Off by default: measured 0.2 ms per
+// step SLOWER on the fp32 bench (25.99 vs 25.78 ms, A/B/A/B on one box) -- it
+// removes 0.16 ms of serial work but moves the dY transform from the side
+// stream (beside the input gradients) onto the main stream's critical path
+// (DESIGN.md §13).  Its per-layer Vd buffers are allocated by plans created
+// while it is on.
+int g_bnb_fuse = getenv("UNET_BNB_FUSE") ? atoi(getenv("UNET_BNB_FUSE")) : 0;
+std::atomic<long long> g_fused_bnb_sites{0};
 }  // namespace unet
 
 namespace {
@@ -89,6 +100,7 @@ struct Conv {
   int ci = 0, co = 0, hi = 0, wi = 0, ho = 0, wo = 0;
   int pw = 0, gw = 0;  // param / grad table base (conv w, b, bn w, bn b, rm, rv, nbt)
   Buf y, mean, invstd, scale, shift, wf, wd, dwp, dz, dyp, coef, stats, bstats;
+  Buf vdw;  // fp32 plans: the F(6x6) weight gradient's dY transform (k_bnb_wino6_dy), one per layer
   Buf a;  // bf16 plans: relu(bn(y)) in bf16, the operand its GEMM consumers read
 };
 struct ConvT {
@@ -597,7 +609,7 @@ hipError_t run_igemm(const Ctx& c, IgemmArgs a) {
   return launch_igemm_v(a, c.s, ch);
 }
 
-hipError_t run_wgrad(const Ctx& c, WgradArgs a) {
+void prep_wgrad(const Ctx& c, WgradArgs& a) {
   a.bf16 = c.p->prec != UNET_PREC_FP32;
   a.split = c.p->prec == UNET_PREC_BF16X3;
   if (c.p->wino_w.bytes) {  // fp32 training plans: the Winograd weight-gradient scratch (side stream)
@@ -608,6 +620,10 @@ hipError_t run_wgrad(const Ctx& c, WgradArgs a) {
     a.slab = c.f(c.p->wslab);
     a.slab_bytes = c.p->wslab.bytes;
   }
+}
+
+hipError_t run_wgrad(const Ctx& c, WgradArgs a) {
+  prep_wgrad(c, a);
   const GemmChoice ch = choose_wgrad(c, a);
   if (unet::g_deterministic && !wgrad_choice_deterministic(ch)) ++unet::g_nondet_sites;
   if (c.p->timing) c.p->xfl += wgrad_exec_flops(a, ch);
@@ -898,7 +914,42 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     }
     CK(launch_bnb_finalize(c.d(L.bstats), L.co, M, P<float>(prm, L.pw + 2), c.f(L.mean), c.f(L.invstd),
                            P<float>(grd, L.gw + 2), P<float>(grd, L.gw + 3), P<float>(grd, L.gw + 1), c.f(L.coef), s));
-    {
+    Src dy;  // dY interior of the padded buffer
+    dy.ptr = c.f(L.dyp);
+    dy.H = L.ho + 4;
+    dy.W = L.wo + 4;
+    dy.C = L.co;
+    dy.oy = dy.ox = 2;
+    dy.h16 = dy16;
+    WgradArgs w;  // weight gradient dW(l) = dY(l)^T x im2col(input of l)
+    w.ga.s[0] = dy;
+    w.ga.s[1] = dy;
+    w.ga.Cg = w.ga.c_split = L.co;
+    w.ga.Hg = L.ho;
+    w.ga.Wg = L.wo;
+    w.ga.nimg = n;
+    w.gb = input_gather(c, l);
+    w.Mo = L.co;
+    w.No = 9 * L.ci;
+    w.P = n * L.ho * L.wo;
+    w.out = c.f(L.dwp);
+    // fp32: when this weight gradient runs Winograd F(6x6), dY and its transform
+    // Vd come out of one pass over dz and y (k_bnb_wino6_dy)
+    bool fused_vd = false;
+    if (p->prec == UNET_PREC_FP32 && unet::g_bnb_fuse && L.vdw.bytes) {
+      WgradArgs q = w;
+      prep_wgrad(cw, q);
+      fused_vd = wgrad_winograd_mt(q, choose_wgrad(cw, q)) == 6 &&
+                 L.vdw.bytes >= bnb_wino6_vd_bytes(n, L.ho, L.wo, L.co);
+    }
+    if (fused_vd) {
+      Timer t(p, s, UNET_KC_ELEMWISE, 0,
+              4.0 * n * ((double)(L.ho + 4) * (L.wo + 4) + 2.0 * L.ho * L.wo) * L.co +
+                  4.0 * 64.0 * n * ((L.ho + 5) / 6) * ((L.wo + 5) / 6) * L.co);
+      CK(launch_bnb_wino6_dy(c.f(L.dz), c.f(L.y), c.f(L.coef), n, L.ho, L.wo, L.co, c.f(L.dyp), c.f(L.vdw), s));
+      w.vd_pre = c.f(L.vdw);
+      ++unet::g_fused_bnb_sites;
+    } else {
       Timer t(p, s, UNET_KC_ELEMWISE, 0, (g16 ? 2.0 : 4.0) * n * ((double)(L.ho + 4) * (L.wo + 4) + 2.0 * L.ho * L.wo) * L.co);
       // bf16 plans store dY(l > 0) in bf16: it only feeds bf16 GEMMs (inc.c0's
       // fp32 direct weight-gradient kernel reads dY(0))
@@ -909,27 +960,7 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
       CK(hipEventRecord(p->ev_dy[l], s));
       CK(hipStreamWaitEvent(sw, p->ev_dy[l], 0));
     }
-    Src dy;  // dY interior of the padded buffer
-    dy.ptr = c.f(L.dyp);
-    dy.H = L.ho + 4;
-    dy.W = L.wo + 4;
-    dy.C = L.co;
-    dy.oy = dy.ox = 2;
-    dy.h16 = dy16;
-    // weight gradient
     {
-      WgradArgs w;
-      w.ga.s[0] = dy;
-      w.ga.s[1] = dy;
-      w.ga.Cg = w.ga.c_split = L.co;
-      w.ga.Hg = L.ho;
-      w.ga.Wg = L.wo;
-      w.ga.nimg = n;
-      w.gb = input_gather(c, l);
-      w.Mo = L.co;
-      w.No = 9 * L.ci;
-      w.P = n * L.ho * L.wo;
-      w.out = c.f(L.dwp);
       Timer t(p, sw, UNET_KC_CONV_WGRAD, conv_flops(L, n), 0, true, site_conv(l, 2));
       Timer tb(p, sw, UNET_KC_BOTTLENECK, conv_flops(L, n), 0, bottleneck_conv(l));
       CK(run_wgrad(cw, w));
@@ -1321,6 +1352,14 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
       wmx = std::max(wmx, wino_ws_bytes_grid(n, L.ho, L.wo, L.ci, L.co));
     }
     p->wino_w = al.take(wmx);
+    // k_bnb_wino6_dy's Vd planes (bnb_fuse on at plan creation): one buffer
+    // per layer, so that the main stream's next layers never overwrite a plane
+    // the side stream's point GEMMs still read (64/36 of the layer's dY: 4.2 GB
+    // at 8 x 512^2)
+    for (int l = 1; l < 18 && unet::g_bnb_fuse; ++l) {
+      Conv& L = p->L[l];
+      if (L.co % 64 == 0) L.vdw = al.take(bnb_wino6_vd_bytes(n, L.ho, L.wo, L.co));
+    }
   }
   // slab-mode weight gradients (ring tiles 26-33 with per_cu codes 11 / 12,
   // pixel-column tiles with codes 101-104): one [Mo][No] fp32 plane per pixel
@@ -1473,6 +1512,9 @@ long long unet_nondeterministic_sites(int reset) {
   return reset ? g_nondet_sites.exchange(0) : g_nondet_sites.load();
 }
 
+long long unet_fused_bnb_sites(int reset) {
+  return reset ? unet::g_fused_bnb_sites.exchange(0) : unet::g_fused_bnb_sites.load();
+}
 long long unet_slab_fallbacks(int reset) {
   return reset ? g_slab_fallbacks.exchange(0) : g_slab_fallbacks.load();
 }

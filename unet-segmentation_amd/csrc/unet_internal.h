@@ -114,6 +114,7 @@ extern std::atomic<long long> g_slab_fallbacks;
 // deterministic mode (unet_set_tuning("deterministic", 1), plan.hip): no fp32
 // atomics in any weight gradient; sites that had no such variant are counted
 extern int g_deterministic;
+extern int g_bnb_fuse;  // plan.hip: fp32 BN-backward apply fused with the F(6x6) dY transform
 extern std::atomic<long long> g_nondet_sites;
 
 struct WgradArgs {
@@ -145,6 +146,10 @@ struct WgradArgs {
   // Winograd F(4x4, 3x3) weight gradient (wgrad tile 71, winograd.hip): scratch
   float* wino_ws = nullptr;
   size_t wino_ws_bytes = 0;
+  // F(6x6) weight gradient (tile 74) of an fp32 plan: the dY transform Vd was
+  // already written here by k_bnb_wino6_dy (fused with the BatchNorm-backward
+  // apply); launch_wino_wgrad then skips k_wino6_dy
+  const float* vd_pre = nullptr;
   // timing ablations of k_wgrad3_bf (UNET_WG_ABL; results wrong with any bit):
   // 1 = plain stores instead of the output atomics, 2 = no MFMA, 4 = no operand
   // loads after the first tile
@@ -181,6 +186,12 @@ hipError_t launch_wino_fused2(const IgemmArgs& a, hipStream_t s, int nc);
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c);
 double wgrad_exec_flops(const WgradArgs& a, GemmChoice c);
 hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int mt);
+int wgrad_winograd_mt(const WgradArgs& a, GemmChoice c);  // 4 / 6: the launch is Winograd F(mt x mt); else 0
+// fp32 BatchNorm-backward apply fused with the F(6x6) weight gradient's dY
+// transform: dYpad (pad 2, border zeroed) and Vd[64][T][c] in one pass
+size_t bnb_wino6_vd_bytes(int n, int h, int w, int c);
+hipError_t launch_bnb_wino6_dy(const float* dz, const float* y, const float* coef, int n, int h, int w, int c,
+                               float* dypad, float* vd, hipStream_t s);
 // bf16 halo conv with LDS-DMA weights (conv3_dma.hip), tile ids 63 and 65-68
 bool conv3_dma_tile_shape(int tile, int& th, int& bn, int& ch);
 hipError_t go_conv3_dma_tile(const IgemmArgs& a, hipStream_t s, int tile);

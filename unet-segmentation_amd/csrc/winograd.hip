@@ -2259,6 +2259,116 @@ __global__ __launch_bounds__(256) void k_wino6_dy(Src dy, int Hg, int Wg, int Th
   }
 }
 
+// BatchNorm-backward apply fused with k_wino6_dy (fp32 plans whose weight
+// gradient runs F(6x6), wgrad tile 74).  The unfused pair streams dY three
+// times: k_bnb_apply reads dz and y and writes dYpad, k_wino6_dy reads dYpad
+// back.  Here a thread owns one 6x6 dY tile x V channels (the tiles partition
+// the grid, so every dY element has one owner): it forms
+// dY = k0*dz + k1*(y - mean) + k2 with k_bnb_apply's exact expression, stores
+// it into dYpad for the input gradient, writes its tile's share of dYpad's
+// zero border, and transforms the values still in registers into Vd
+// (k_wino6_dy's arithmetic and layout) -- dY is never read back.  BN backward:
+// models/unet_model.py:12,16 (nn.BatchNorm2d in DoubleConv).
+template <int V>
+__global__ __launch_bounds__(256) void k_bnb_wino6_dy(const float* __restrict__ dz, const float* __restrict__ yr,
+                                                      const float* __restrict__ coef, int Ho, int Wo, int Co, int Th,
+                                                      int Tw, long long T, float* __restrict__ dyp,
+                                                      float* __restrict__ vd) {
+  typedef float vec __attribute__((ext_vector_type(V)));
+  const int CV = Co / V;
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i >= T * CV) return;
+  const long long t = i / CV;
+  const int c = (int)(i - t * CV) * V;
+  const int tx = (int)(t % Tw);
+  const long long r = t / Tw;
+  const int ty = (int)(r % Th), n = (int)(r / Th);
+  const int vr = min(6, Ho - 6 * ty), vc = min(6, Wo - 6 * tx);
+  const vec k0 = *reinterpret_cast<const vec*>(coef + c), k1 = *reinterpret_cast<const vec*>(coef + Co + c);
+  const vec k2 = *reinterpret_cast<const vec*>(coef + 2 * Co + c), mu = *reinterpret_cast<const vec*>(coef + 3 * Co + c);
+  const int Wp = Wo + 4;
+  const size_t src0 = ((size_t)(n * Ho + 6 * ty) * Wo + 6 * tx) * Co + c;
+  const size_t dst0 = ((size_t)(n * (Ho + 4) + 6 * ty + 2) * Wp + 6 * tx + 2) * Co + c;
+  float e[V][8][6];
+#pragma unroll
+  for (int xx = 0; xx < 6; ++xx) {
+    float d[V][6];
+#pragma unroll
+    for (int yy = 0; yy < 6; ++yy) {
+      vec o;
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = 0.f;
+      if (yy < vr && xx < vc) {
+        const size_t so = src0 + ((size_t)yy * Wo + xx) * Co;
+        const vec dv = *reinterpret_cast<const vec*>(dz + so), yv = *reinterpret_cast<const vec*>(yr + so);
+#pragma unroll
+        for (int k = 0; k < V; ++k) o[k] = fmaf(k0[k], dv[k], fmaf(k1[k], yv[k] - mu[k], k2[k]));
+        *reinterpret_cast<vec*>(dyp + dst0 + ((size_t)yy * Wp + xx) * Co) = o;
+      }
+#pragma unroll
+      for (int k = 0; k < V; ++k) d[k][yy] = o[k];
+    }
+#pragma unroll
+    for (int k = 0; k < V; ++k) {
+      float rr[8];
+      a8(d[k], rr);
+#pragma unroll
+      for (int a = 0; a < 8; ++a) e[k][a][xx] = rr[a];
+    }
+  }
+  float* ob = vd + (size_t)t * Co + c;
+  const size_t plane = (size_t)T * Co;
+#pragma unroll
+  for (int a = 0; a < 8; ++a) {
+    float rr[V][8];
+#pragma unroll
+    for (int k = 0; k < V; ++k) a8(e[k][a], rr[k]);
+#pragma unroll
+    for (int bb = 0; bb < 8; ++bb) {
+      vec o;
+#pragma unroll
+      for (int k = 0; k < V; ++k) o[k] = rr[k][bb];
+      *reinterpret_cast<vec*>(ob + (size_t)(a * 8 + bb) * plane) = o;
+    }
+  }
+  // the zero border of dYpad (2 rows / columns each side): the first / last
+  // tile row owns the top / bottom rows over its tiles' column span (the outer
+  // tiles' spans run into the corners), the first / last tile column the left
+  // / right columns beside its tile's rows
+  if (ty == 0 || ty == Th - 1 || tx == 0 || tx == Tw - 1) {
+    vec z;
+#pragma unroll
+    for (int k = 0; k < V; ++k) z[k] = 0.f;
+    float* pb = dyp + (size_t)n * (Ho + 4) * Wp * Co + c;
+    const int x0 = tx == 0 ? 0 : 6 * tx + 2, x1 = tx == Tw - 1 ? Wo + 4 : 6 * tx + 8;
+    auto zero = [&](int py, int px) { *reinterpret_cast<vec*>(pb + ((size_t)py * Wp + px) * Co) = z; };
+    if (ty == 0)
+      for (int py = 0; py < 2; ++py)
+        for (int px = x0; px < x1; ++px) zero(py, px);
+    if (ty == Th - 1)
+      for (int py = Ho + 2; py < Ho + 4; ++py)
+        for (int px = x0; px < x1; ++px) zero(py, px);
+    for (int py = 6 * ty + 2; py < 6 * ty + 2 + vr; ++py) {
+      if (tx == 0) { zero(py, 0); zero(py, 1); }
+      if (tx == Tw - 1) { zero(py, Wo + 2); zero(py, Wo + 3); }
+    }
+  }
+}
+
+size_t bnb_wino6_vd_bytes(int n, int h, int w, int c) {
+  return (size_t)64 * n * ((h + 5) / 6) * ((w + 5) / 6) * c * sizeof(float);
+}
+
+hipError_t launch_bnb_wino6_dy(const float* dz, const float* y, const float* coef, int n, int h, int w, int c,
+                               float* dypad, float* vd, hipStream_t s) {
+  if (c % 64 != 0 || n < 1 || h < 1 || w < 1) return hipErrorInvalidValue;  // wino_wgrad_applies: Co % 64 == 0
+  const int Th = (h + 5) / 6, Tw = (w + 5) / 6;
+  const long long T = (long long)n * Th * Tw, nd = T * (c / 2);
+  hipLaunchKernelGGL(k_bnb_wino6_dy<2>, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, dz, y, coef, h, w, c,
+                     Th, Tw, T, dypad, vd);
+  return hipGetLastError();
+}
+
 __global__ __launch_bounds__(256) void k_wino6_wout(const float* __restrict__ mw, int Co, int Ci,
                                                     float* __restrict__ out) {
   const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
@@ -2332,8 +2442,11 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
                        Tw, T, Co, Vd);
   } else {
     launch_wino6_in(gb, Th, Tw, T, U, s);
-    hipLaunchKernelGGL(k_wino6_dy<2>, dim3((unsigned)((nd / 2 + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg,
-                       gb.Wg, Th, Tw, T, Co, Vd);  // Co % 64 == 0 (wino_wgrad_applies)
+    if (a.vd_pre)  // written by k_bnb_wino6_dy beside dYpad (same tiles, same layout)
+      Vd = const_cast<float*>(a.vd_pre);
+    else
+      hipLaunchKernelGGL(k_wino6_dy<2>, dim3((unsigned)((nd / 2 + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg,
+                         gb.Wg, Th, Tw, T, Co, Vd);  // Co % 64 == 0 (wino_wgrad_applies)
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

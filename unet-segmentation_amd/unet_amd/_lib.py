@@ -95,6 +95,7 @@ SIGNATURES = {
     "unet_tuning_reset": (_i, []),
     "unet_slab_fallbacks": (ctypes.c_longlong, [_i]),
     "unet_nondeterministic_sites": (ctypes.c_longlong, [_i]),
+    "unet_fused_bnb_sites": (ctypes.c_longlong, [_i]),
     "unet_tuning_save": (_i, [ctypes.c_char_p]),
     "unet_tuning_load": (_i, [ctypes.c_char_p]),
 }
