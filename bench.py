@@ -326,7 +326,22 @@ def run_farm(args, dtype, device, iters=20, warmup=3):
 
 
 def run_precision(args, dtype, device, pg, world, rank):
-    """Time args.steps train steps of one GEMM precision; returns its summary."""
+    """Time args.steps train steps of one GEMM precision; returns its summary.
+    UNET_MAIN_PRIORITY=<p> (experiment): the whole leg runs on a torch stream
+    of priority p (lower = higher), the plan's side stream keeps the lowest."""
+    prio = os.environ.get("UNET_MAIN_PRIORITY")
+    if not prio:
+        return _run_precision(args, dtype, device, pg, world, rank)
+    s = torch.cuda.Stream(device=device, priority=int(prio))
+    print(f"main stream priority {int(prio)} (range {torch.cuda.Stream.priority_range()})", file=sys.stderr)
+    torch.cuda.current_stream(device).synchronize()
+    with torch.cuda.stream(s):
+        r = _run_precision(args, dtype, device, pg, world, rank)
+    s.synchronize()
+    return r
+
+
+def _run_precision(args, dtype, device, pg, world, rank):
     from unet_amd import UNet
     from unet_amd.train import Trainer
     torch.manual_seed(0)
