@@ -352,12 +352,16 @@ int unet_linear_sum_assignment(long long nr, long long nc, const double* host_co
  *                  reduction runs in one pass: plan steps are
  *                  bit-reproducible run to run (see
  *                  unet_nondeterministic_sites).
- *  "bnb_fuse"      1 (env UNET_BNB_FUSE=1) = fp32 plans form the
+ *  "bnb_fuse"      1 (default; env UNET_BNB_FUSE) = fp32 plans form the
  *                  BatchNorm-backward dY of a layer whose weight gradient runs
  *                  Winograd F(6x6) in one pass with that weight gradient's dY
- *                  transform (see unet_fused_bnb_sites); 0 (default) = the
- *                  two-pass form (bit-identical results; faster with the
- *                  concurrent weight-gradient stream). */
+ *                  transform (see unet_fused_bnb_sites; read for the workspace
+ *                  layout at plan creation); 0 = the two-pass form
+ *                  (bit-identical results).
+ *  "wgrad_early_u" 1 (default; env UNET_WGRAD_EARLY_U) = the Winograd weight
+ *                  gradients' input transform is issued on the side stream
+ *                  before the wait for the layer's dY; 0 = after it
+ *                  (bit-identical results). */
 int unet_set_tuning(const char* key, int value);
 /* Text report of the tuned GEMM choices (one line per shape: key, heuristic
  * time, chosen variant and time).  Copies up to len-1 bytes + NUL into buf

@@ -11,9 +11,9 @@ are forced to Winograd F(6x6) in slab mode (wgrad1074: no fp32 atomics), which
 makes every tensor of the step run-to-run reproducible except the leaves whose
 kernels keep atomics under the heuristic (the ConvTranspose2d weight gradients
 and inc.c0's weight gradient): those are held to the run-to-run noise of a
-repeated unfused step.  The fused pass is off by default (slower beside the
-concurrent weight-gradient stream); with it on, the last case
-also checks the step against the fp64 oracle."""
+repeated unfused step.  The fused pass is on by default, together with the
+early input transforms of the Winograd weight gradients; the
+oracle case checks a step under the tuned choices against fp64.
 import numpy as np
 import pytest
 
@@ -65,7 +65,7 @@ def test_fused_bnb_wino6_dy_bit_identical(n, h, w, seed):
             runs.append(_step(params, x, tgt, wmap))
             sites.append(lib.unet_fused_bnb_sites(1))
     finally:
-        lib.unet_set_tuning(b"bnb_fuse", 0)
+        lib.unet_set_tuning(b"bnb_fuse", 1)
         lib.unet_set_tuning(b"wgrad_variant", -1)
         lib.unet_set_tuning(b"autotune", 1)
         lib.unet_tuning_reset()
@@ -90,7 +90,7 @@ def test_fused_bnb_wino6_dy_bit_identical(n, h, w, seed):
 
 
 def test_fused_bnb_wino6_dy_vs_oracle():
-    """The fused pass (opt-in) under the autotuner's own choices: a train step
+    """The fused pass under the autotuner's own choices: a train step
     against the fp64 oracle at the fp32 bars of test_gpu_model.py (rel-L2 per
     gradient <= max(1e-2, 2 x the fp32 oracle's own error))."""
     from unet_amd import _lib
@@ -102,5 +102,60 @@ def test_fused_bnb_wino6_dy_vs_oracle():
         TM.test_train_step_vs_oracle(2, 188, 44, "fp32")
         used = lib.unet_fused_bnb_sites(1)
     finally:
-        lib.unet_set_tuning(b"bnb_fuse", 0)
+        lib.unet_set_tuning(b"bnb_fuse", 1)
     print(f"fused sites under the tuned choices: {used}")
+
+
+def _two_steps(params, x, tgt, wmap):
+    """Two train steps of a fresh model: the first tunes / runs serially, the
+    second runs the concurrent schedule (weight gradients on the side stream);
+    returns the second step's outputs."""
+    from unet_amd import UNet, WeightedCrossEntropyLoss
+    m = UNet(1, 2)
+    m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in params.items()})
+    m = m.cuda().train()
+    xd, td, wd = (torch.from_numpy(a).cuda() for a in (x, tgt, wmap))
+    for _ in range(2):
+        m.zero_grad(set_to_none=True)
+        logits = m(xd)
+        loss = WeightedCrossEntropyLoss()(logits, td, wd)
+        loss.backward()
+    torch.cuda.synchronize()
+    return (logits.detach().cpu(), loss.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()})
+
+
+@pytest.mark.parametrize("n,h,seed", [(2, 188, 45), (1, 195, 46)])
+def test_wgrad_early_u_bit_identical(n, h, seed):
+    """unet_set_tuning("wgrad_early_u", 1): the Winograd weight gradients' input
+    transform U is issued on the side stream before the wait for the layer's dY
+    (scheduling only: the same kernels on the same operands).  With F(6x6)
+    forced in slab mode the concurrent step is bit-identical to the default
+    schedule on every reproducible tensor."""
+    from unet_amd import _lib
+    lib = _lib.load()
+    params = O.hash_init(1, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
+    runs = []
+    lib.unet_tuning_reset()
+    lib.unet_set_tuning(b"autotune", 0)
+    lib.unet_set_tuning(b"wgrad_variant", 1074)
+    try:
+        for early in (0, 0, 1):
+            lib.unet_set_tuning(b"wgrad_early_u", early)
+            runs.append(_two_steps(params, x, tgt, wmap))
+    finally:
+        lib.unet_set_tuning(b"wgrad_early_u", 1)
+        lib.unet_set_tuning(b"wgrad_variant", -1)
+        lib.unet_set_tuning(b"autotune", 1)
+        lib.unet_tuning_reset()
+    (l0, s0, g0), (_, _, g0b), (l1, s1, g1) = runs
+    assert torch.equal(l0, l1) and torch.equal(s0, s1)
+    for k in g0:
+        if _atomic_leaf(k):
+            a, b, c = (t.double() for t in (g0[k], g0b[k], g1[k]))
+            nrm = a.norm().item() + 1e-30
+            noise, diff = (b - a).norm().item() / nrm, (c - a).norm().item() / nrm
+            assert diff <= 2 * noise + 1e-6, (k, diff, noise)
+        else:
+            assert torch.equal(g0[k], g0b[k]), f"{k}: the default step is not reproducible"
+            assert torch.equal(g0[k], g1[k]), f"{k}: early-U and default gradients differ"

@@ -546,6 +546,7 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "op_a16") g_op_a16 = value != 0;
   else if (k == "maxpool_vec8") g_maxpool_vec8 = value;
   else if (k == "bnb_fuse") g_bnb_fuse = value;
+  else if (k == "wgrad_early_u") g_wgrad_early_u = value;
   else if (k == "deterministic") g_deterministic = value != 0;  // 0: bf16 plans pool with the 4-channel kernel (A/B tests)
   else if (k == "op_precision") {
     if (value != UNET_PREC_FP32 && value != UNET_PREC_BF16 && value != UNET_PREC_BF16X3) return -EINVAL;

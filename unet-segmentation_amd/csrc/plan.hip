@@ -61,17 +61,23 @@ int g_force_tile = 0;
 // unet_nondeterministic_sites().
 int g_deterministic = getenv("UNET_DETERMINISTIC") ? atoi(getenv("UNET_DETERMINISTIC")) : 0;
 std::atomic<long long> g_nondet_sites{0};
-// unet_set_tuning("bnb_fuse", v) or UNET_BNB_FUSE (default off): fp32 plans form
+// unet_set_tuning("bnb_fuse", v) or UNET_BNB_FUSE (default on): fp32 plans form
 // dY of a layer whose weight gradient runs Winograd F(6x6) in one pass with
 // that weight gradient's dY transform (k_bnb_wino6_dy) instead of k_bnb_apply
-// + k_wino6_dy (bit-identical results).  Off by default: measured 0.2 ms per
-// step SLOWER on the fp32 bench (25.99 vs 25.78 ms, A/B/A/B on one box) -- it
-// removes 0.16 ms of serial work but moves the dY transform from the side
-// stream (beside the input gradients) onto the main stream's critical path
-// (DESIGN.md §13).  Its per-layer Vd buffers are allocated by plans created
-// while it is on.
-int g_bnb_fuse = getenv("UNET_BNB_FUSE") ? atoi(getenv("UNET_BNB_FUSE")) : 0;
+// + k_wino6_dy (bit-identical results).  Measured with the early U transforms
+// below (both on by default): 25.60 vs 25.74 ms per fp32 step (three A/B pairs,
+// one box); alone it is 0.2 ms SLOWER, because the dY transform leaves the side
+// stream for the main stream's critical path and the side stream idles while
+// the main stream runs the fused pass.  Its per-layer Vd buffers
+// are allocated by plans created while it is on.
+int g_bnb_fuse = getenv("UNET_BNB_FUSE") ? atoi(getenv("UNET_BNB_FUSE")) : 1;
 std::atomic<long long> g_fused_bnb_sites{0};
+// unet_set_tuning("wgrad_early_u", v) or UNET_WGRAD_EARLY_U (default on): with
+// the side stream, a Winograd weight gradient's input transform U (forward
+// tensors only) is issued on the side stream before it waits for the layer's
+// dY, so it runs beside the main stream's BN-backward finalize / apply (or
+// fused pass) of that layer instead of after it
+int g_wgrad_early_u = getenv("UNET_WGRAD_EARLY_U") ? atoi(getenv("UNET_WGRAD_EARLY_U")) : 1;
 }  // namespace unet
 
 namespace {
@@ -139,6 +145,7 @@ struct unet_plan {
   // backward (joined at the end of every backward call)
   hipStream_t side = nullptr;
   hipEvent_t ev_dy[18] = {}, ev_du[4] = {}, ev_join = nullptr;
+  hipEvent_t ev_bwd0 = nullptr;  // main stream at a backward call's start (early U transforms wait on it)
   // per backward segment: recorded on the side stream after the segment's
   // weight gradients (UNET_BWD_DEFER_JOIN calls), waited on by the caller's
   // collective stream (unet_plan_wait_segment)
@@ -858,6 +865,7 @@ hipError_t ensure_side_stream(unet_plan* p) {
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
   for (auto& ev : p->ev_seg)
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
+  if ((e = hipEventCreateWithFlags(&p->ev_bwd0, hipEventDisableTiming)) != hipSuccess) return e;
   return hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming);
 }
 
@@ -878,6 +886,12 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
   Ctx cw{p, ws, conc ? p->side : s};
   const hipStream_t sw = cw.s;
   auto in_seg = [&](int sg) { return sg >= seg_b && sg < seg_e; };
+  if (conc && unet::g_wgrad_early_u) {
+    // early U transforms read this step's forward tensors: the side stream
+    // starts after everything the main stream has queued so far
+    CK(hipEventRecord(p->ev_bwd0, s));
+    CK(hipStreamWaitEvent(sw, p->ev_bwd0, 0));
+  }
   if (seg_b == 0) {
     // accumulators (bstats, colsums, packed weight grads) were zeroed by the
     // train-mode forward that filled this workspace
@@ -936,11 +950,16 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     // fp32: when this weight gradient runs Winograd F(6x6), dY and its transform
     // Vd come out of one pass over dz and y (k_bnb_wino6_dy)
     bool fused_vd = false;
-    if (p->prec == UNET_PREC_FP32 && unet::g_bnb_fuse && L.vdw.bytes) {
+    const bool early_u = conc && unet::g_wgrad_early_u;
+    if (p->prec == UNET_PREC_FP32 && ((unet::g_bnb_fuse && L.vdw.bytes) || early_u)) {
       WgradArgs q = w;
       prep_wgrad(cw, q);
-      fused_vd = wgrad_winograd_mt(q, choose_wgrad(cw, q)) == 6 &&
-                 L.vdw.bytes >= bnb_wino6_vd_bytes(n, L.ho, L.wo, L.co);
+      const int wmt = wgrad_winograd_mt(q, choose_wgrad(cw, q));
+      fused_vd = unet::g_bnb_fuse && wmt == 6 && L.vdw.bytes >= bnb_wino6_vd_bytes(n, L.ho, L.wo, L.co);
+      if (early_u && wmt) {  // side stream, FIFO after the previous layer's point GEMMs
+        CK(launch_wino_wgrad_u(q, sw, wmt));
+        w.u_ready = 1;
+      }
     }
     if (fused_vd) {
       Timer t(p, s, UNET_KC_ELEMWISE, 0,
@@ -1378,6 +1397,7 @@ void unet_plan_destroy(unet_plan* p) {
     for (auto ev : p->ev_du) (void)hipEventDestroy(ev);
     for (auto ev : p->ev_seg) (void)hipEventDestroy(ev);
     (void)hipEventDestroy(p->ev_join);
+    (void)hipEventDestroy(p->ev_bwd0);
     (void)hipStreamDestroy(p->side);
   }
   for (auto& e : p->evs) {

@@ -114,7 +114,8 @@ extern std::atomic<long long> g_slab_fallbacks;
 // deterministic mode (unet_set_tuning("deterministic", 1), plan.hip): no fp32
 // atomics in any weight gradient; sites that had no such variant are counted
 extern int g_deterministic;
-extern int g_bnb_fuse;  // plan.hip: fp32 BN-backward apply fused with the F(6x6) dY transform
+extern int g_bnb_fuse;
+extern int g_wgrad_early_u;  // plan.hip: Winograd weight gradients' U issued before the layer's dY  // plan.hip: fp32 BN-backward apply fused with the F(6x6) dY transform
 extern std::atomic<long long> g_nondet_sites;
 
 struct WgradArgs {
@@ -150,6 +151,9 @@ struct WgradArgs {
   // already written here by k_bnb_wino6_dy (fused with the BatchNorm-backward
   // apply); launch_wino_wgrad then skips k_wino6_dy
   const float* vd_pre = nullptr;
+  // 1: the Winograd weight gradient's input transform U is already in wino_ws
+  // (launch_wino_wgrad_u, issued ahead of the layer's dY)
+  int u_ready = 0;
   // timing ablations of k_wgrad3_bf (UNET_WG_ABL; results wrong with any bit):
   // 1 = plain stores instead of the output atomics, 2 = no MFMA, 4 = no operand
   // loads after the first tile
@@ -186,7 +190,8 @@ hipError_t launch_wino_fused2(const IgemmArgs& a, hipStream_t s, int nc);
 double igemm_exec_flops(const IgemmArgs& a, GemmChoice c);
 double wgrad_exec_flops(const WgradArgs& a, GemmChoice c);
 hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int mt);
-int wgrad_winograd_mt(const WgradArgs& a, GemmChoice c);  // 4 / 6: the launch is Winograd F(mt x mt); else 0
+int wgrad_winograd_mt(const WgradArgs& a, GemmChoice c);
+hipError_t launch_wino_wgrad_u(const WgradArgs& a, hipStream_t s, int mt);  // 4 / 6: the launch is Winograd F(mt x mt); else 0
 // fp32 BatchNorm-backward apply fused with the F(6x6) weight gradient's dY
 // transform: dYpad (pad 2, border zeroed) and Vd[64][T][c] in one pass
 size_t bnb_wino6_vd_bytes(int n, int h, int w, int c);

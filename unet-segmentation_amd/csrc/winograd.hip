@@ -2413,6 +2413,19 @@ bool wino_wgrad_applies(const WgradArgs& a, int mt) {
   return wino_bytes((mt + 2) * (mt + 2), T, gb.Cg, a.Mo) <= a.wino_ws_bytes;
 }
 
+// The input transform U = B^T X B alone (into the head of a.wino_ws, where
+// launch_wino_wgrad with u_ready reads it): it needs only forward tensors, so
+// the plan can issue it before the layer's dY exists (UNET_WGRAD_EARLY_U)
+hipError_t launch_wino_wgrad_u(const WgradArgs& a, hipStream_t s, int mt) {
+  if ((mt != 4 && mt != 6) || !wino_wgrad_applies(a, mt)) return hipErrorInvalidValue;
+  const Gather& gb = a.gb;
+  const int Th = (gb.Hg + mt - 1) / mt, Tw = (gb.Wg + mt - 1) / mt;
+  const long long T = wino_wgrad_tiles(a, mt);
+  if (mt == 4) launch_wino4_in(gb, Th, Tw, T, a.wino_ws, s);
+  else launch_wino6_in(gb, Th, Tw, T, a.wino_ws, s);
+  return hipGetLastError();
+}
+
 // mt = 4 (wgrad tile 71) or 6 (tile 74).  per_cu: workgroups per CU of the point
 // GEMMs' pixel split, + 100 * (1 + k_wgrad tile id) to force their tile
 // (autotuner candidates)
@@ -2437,11 +2450,11 @@ hipError_t launch_wino_wgrad(const WgradArgs& a, hipStream_t s, int per_cu, int 
   float* Mw = reinterpret_cast<float*>(w + al((size_t)P * T * Ci * 4) + al((size_t)P * T * Co * 4));
   const long long nd = T * Co;
   if (mt == 4) {
-    launch_wino4_in(gb, Th, Tw, T, U, s);
+    if (!a.u_ready) launch_wino4_in(gb, Th, Tw, T, U, s);
     hipLaunchKernelGGL(k_wino4_dy, dim3((unsigned)((nd + 255) / 256)), dim3(256), 0, s, a.ga.s[0], gb.Hg, gb.Wg, Th,
                        Tw, T, Co, Vd);
   } else {
-    launch_wino6_in(gb, Th, Tw, T, U, s);
+    if (!a.u_ready) launch_wino6_in(gb, Th, Tw, T, U, s);
     if (a.vd_pre)  // written by k_bnb_wino6_dy beside dYpad (same tiles, same layout)
       Vd = const_cast<float*>(a.vd_pre);
     else
