@@ -13,7 +13,7 @@ kernels keep atomics under the heuristic (the ConvTranspose2d weight gradients
 and inc.c0's weight gradient): those are held to the run-to-run noise of a
 repeated unfused step.  The fused pass is on by default, together with the
 early input transforms of the Winograd weight gradients; the
-oracle case checks a step under the tuned choices against fp64.
+oracle case checks a step under the tuned choices against fp64."""
 import numpy as np
 import pytest
 
