@@ -159,3 +159,40 @@ def test_wgrad_early_u_bit_identical(n, h, seed):
         else:
             assert torch.equal(g0[k], g0b[k]), f"{k}: the default step is not reproducible"
             assert torch.equal(g0[k], g1[k]), f"{k}: early-U and default gradients differ"
+
+
+@pytest.mark.parametrize("n,h,seed", [(2, 188, 47), (1, 204, 48)])
+def test_wgrad_fwd_u_bit_identical(n, h, seed):
+    """unet_set_tuning("wgrad_fwd_u", 1) (read at plan creation): the Winograd
+    weight gradients' input transform U is issued during the forward on the
+    side stream, into a per-layer buffer the backward's point GEMMs read.  The
+    second (concurrent) step is bit-identical to the default schedule on every
+    reproducible tensor, with F(6x6) forced in slab mode."""
+    from unet_amd import _lib
+    lib = _lib.load()
+    params = O.hash_init(1, 2, seed=seed, bn_random=True)
+    x, tgt, wmap = F.make_inputs(seed, n, 1, h)
+    runs = []
+    lib.unet_tuning_reset()
+    lib.unet_set_tuning(b"autotune", 0)
+    lib.unet_set_tuning(b"wgrad_variant", 1074)
+    try:
+        for fwd_u in (0, 0, 1):
+            lib.unet_set_tuning(b"wgrad_fwd_u", fwd_u)
+            runs.append(_two_steps(params, x, tgt, wmap))
+    finally:
+        lib.unet_set_tuning(b"wgrad_fwd_u", 0)
+        lib.unet_set_tuning(b"wgrad_variant", -1)
+        lib.unet_set_tuning(b"autotune", 1)
+        lib.unet_tuning_reset()
+    (l0, s0, g0), (_, _, g0b), (l1, s1, g1) = runs
+    assert torch.equal(l0, l1) and torch.equal(s0, s1)
+    for k in g0:
+        if _atomic_leaf(k):
+            a, b, c = (t.double() for t in (g0[k], g0b[k], g1[k]))
+            nrm = a.norm().item() + 1e-30
+            noise, diff = (b - a).norm().item() / nrm, (c - a).norm().item() / nrm
+            assert diff <= 2 * noise + 1e-6, (k, diff, noise)
+        else:
+            assert torch.equal(g0[k], g0b[k]), f"{k}: the default step is not reproducible"
+            assert torch.equal(g0[k], g1[k]), f"{k}: forward-U and default gradients differ"

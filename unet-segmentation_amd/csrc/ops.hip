@@ -14,7 +14,7 @@ using namespace unet;
 namespace unet {
 extern int g_tune_igemm, g_tune_wgrad, g_autotune, g_force_split, g_force_tile, g_concurrent, g_wino_max,
     g_wino_dgrad_max, g_wino_wgrad_max, g_bf16_norm, g_bn_fold, g_wino4_fwd_min_cg, g_wino4_fwd_small_cg,
-    g_maxpool_vec8;
+    g_maxpool_vec8, g_wgrad_fwd_u;
 hipError_t launch_fill(float* p, size_t n, float v, hipStream_t s);
 hipError_t launch_pair_sum(const double* st, int g, int c, float* out, hipStream_t s);
 }  // namespace unet
@@ -547,6 +547,7 @@ int unet_set_tuning(const char* key, int value) {
   else if (k == "maxpool_vec8") g_maxpool_vec8 = value;
   else if (k == "bnb_fuse") g_bnb_fuse = value;
   else if (k == "wgrad_early_u") g_wgrad_early_u = value;
+  else if (k == "wgrad_fwd_u") g_wgrad_fwd_u = value;
   else if (k == "deterministic") g_deterministic = value != 0;  // 0: bf16 plans pool with the 4-channel kernel (A/B tests)
   else if (k == "op_precision") {
     if (value != UNET_PREC_FP32 && value != UNET_PREC_BF16 && value != UNET_PREC_BF16X3) return -EINVAL;

@@ -78,6 +78,11 @@ std::atomic<long long> g_fused_bnb_sites{0};
 // dY, so it runs beside the main stream's BN-backward finalize / apply (or
 // fused pass) of that layer instead of after it
 int g_wgrad_early_u = getenv("UNET_WGRAD_EARLY_U") ? atoi(getenv("UNET_WGRAD_EARLY_U")) : 1;
+// unet_set_tuning("wgrad_fwd_u", v) or UNET_WGRAD_FWD_U (default off): fp32
+// training plans issue each Winograd weight gradient's input transform U
+// during the FORWARD, on the side stream (idle there), into a per-layer buffer
+// the backward's point GEMMs read; read for the workspace layout at plan creation
+int g_wgrad_fwd_u = getenv("UNET_WGRAD_FWD_U") ? atoi(getenv("UNET_WGRAD_FWD_U")) : 0;
 }  // namespace unet
 
 namespace {
@@ -107,6 +112,8 @@ struct Conv {
   int pw = 0, gw = 0;  // param / grad table base (conv w, b, bn w, bn b, rm, rv, nbt)
   Buf y, mean, invstd, scale, shift, wf, wd, dwp, dz, dyp, coef, stats, bstats;
   Buf vdw;  // fp32 plans: the F(6x6) weight gradient's dY transform (k_bnb_wino6_dy), one per layer
+  Buf uws;  // fp32 plans with wgrad_fwd_u: this layer's Winograd weight-gradient scratch (U | Vd | Mw)
+  bool u_fwd = false;  // U of this step already issued by the forward (side stream)
   Buf a;  // bf16 plans: relu(bn(y)) in bf16, the operand its GEMM consumers read
 };
 struct ConvT {
@@ -146,6 +153,7 @@ struct unet_plan {
   hipStream_t side = nullptr;
   hipEvent_t ev_dy[18] = {}, ev_du[4] = {}, ev_join = nullptr;
   hipEvent_t ev_bwd0 = nullptr;  // main stream at a backward call's start (early U transforms wait on it)
+  hipEvent_t ev_fwdu = nullptr;  // main stream before a forward layer whose U the side stream computes
   // per backward segment: recorded on the side stream after the segment's
   // weight gradients (UNET_BWD_DEFER_JOIN calls), waited on by the caller's
   // collective stream (unet_plan_wait_segment)
@@ -619,8 +627,8 @@ hipError_t run_igemm(const Ctx& c, IgemmArgs a) {
 void prep_wgrad(const Ctx& c, WgradArgs& a) {
   a.bf16 = c.p->prec != UNET_PREC_FP32;
   a.split = c.p->prec == UNET_PREC_BF16X3;
-  if (c.p->wino_w.bytes) {  // fp32 training plans: the Winograd weight-gradient scratch (side stream)
-    a.wino_ws = c.f(c.p->wino_w);
+  if (c.p->wino_w.bytes && !a.wino_ws) {  // fp32 training plans: the Winograd weight-gradient scratch
+    a.wino_ws = c.f(c.p->wino_w);           // (side stream; a layer's own with wgrad_fwd_u)
     a.wino_ws_bytes = c.p->wino_w.bytes;
   }
   if (c.p->wslab.bytes) {  // partial planes of the slab-mode weight gradients (side stream)
@@ -711,6 +719,34 @@ Gather input_gather(const Ctx& c, int l) {
   }
   if (g.s[1].ptr == nullptr) g.s[1] = g.s[0];
   return g;
+}
+
+hipError_t ensure_side_stream(unet_plan* p);
+
+// Weight gradient of 3x3 layer l >= 1: dW(l) = dY(l)^T x im2col(input of l),
+// dY read from the interior of the padded buffer
+WgradArgs conv_wgrad_args(const Ctx& c, int l) {
+  const Conv& L = c.p->L[l];
+  Src dy;
+  dy.ptr = c.f(L.dyp);
+  dy.H = L.ho + 4;
+  dy.W = L.wo + 4;
+  dy.C = L.co;
+  dy.oy = dy.ox = 2;
+  dy.h16 = c.p->prec == UNET_PREC_BF16;
+  WgradArgs w;
+  w.ga.s[0] = dy;
+  w.ga.s[1] = dy;
+  w.ga.Cg = w.ga.c_split = L.co;
+  w.ga.Hg = L.ho;
+  w.ga.Wg = L.wo;
+  w.ga.nimg = c.p->n;
+  w.gb = input_gather(c, l);
+  w.Mo = L.co;
+  w.No = 9 * L.ci;
+  w.P = c.p->n * L.ho * L.wo;
+  w.out = c.f(L.dwp);
+  return w;
 }
 
 int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, char* ws, int train, hipStream_t s) {
@@ -811,6 +847,24 @@ int run_forward(unet_plan* p, void* const* prm, const float* x, float* logits, c
       Timer tb(p, s, UNET_KC_BOTTLENECK, 2.0 * a.M * a.N * a.K, 0, k == 0);
       CK(run_igemm(c, a));
     }
+    L.u_fwd = false;
+    if (train && unet::g_wgrad_fwd_u && L.uws.bytes && unet::g_concurrent && !p->timing && p->bwd_full > 0) {
+      // this layer's weight-gradient input transform U on the (idle) side
+      // stream, beside the forward GEMMs: its inputs are final at this point
+      CK(ensure_side_stream(p));
+      Ctx cs{p, ws, p->side};
+      WgradArgs q = conv_wgrad_args(c, l);
+      prep_wgrad(cs, q);
+      const int mt = wgrad_winograd_mt(q, choose_wgrad(cs, q));
+      q.wino_ws = c.f(L.uws);
+      q.wino_ws_bytes = L.uws.bytes;
+      if (mt && wino_wgrad_applies(q, mt)) {
+        CK(hipEventRecord(p->ev_fwdu, s));
+        CK(hipStreamWaitEvent(p->side, p->ev_fwdu, 0));
+        CK(launch_wino_wgrad_u(q, p->side, mt));
+        L.u_fwd = true;
+      }
+    }
     IgemmArgs a;
     a.a = input_gather(c, l);
     a.b = c.f(L.wf);
@@ -866,6 +920,7 @@ hipError_t ensure_side_stream(unet_plan* p) {
   for (auto& ev : p->ev_seg)
     if ((e = hipEventCreateWithFlags(&ev, hipEventDisableTiming)) != hipSuccess) return e;
   if ((e = hipEventCreateWithFlags(&p->ev_bwd0, hipEventDisableTiming)) != hipSuccess) return e;
+  if ((e = hipEventCreateWithFlags(&p->ev_fwdu, hipEventDisableTiming)) != hipSuccess) return e;
   return hipEventCreateWithFlags(&p->ev_join, hipEventDisableTiming);
 }
 
@@ -928,29 +983,18 @@ int run_backward(unet_plan* p, void* const* prm, void* const* grd, const float* 
     }
     CK(launch_bnb_finalize(c.d(L.bstats), L.co, M, P<float>(prm, L.pw + 2), c.f(L.mean), c.f(L.invstd),
                            P<float>(grd, L.gw + 2), P<float>(grd, L.gw + 3), P<float>(grd, L.gw + 1), c.f(L.coef), s));
-    Src dy;  // dY interior of the padded buffer
-    dy.ptr = c.f(L.dyp);
-    dy.H = L.ho + 4;
-    dy.W = L.wo + 4;
-    dy.C = L.co;
-    dy.oy = dy.ox = 2;
-    dy.h16 = dy16;
-    WgradArgs w;  // weight gradient dW(l) = dY(l)^T x im2col(input of l)
-    w.ga.s[0] = dy;
-    w.ga.s[1] = dy;
-    w.ga.Cg = w.ga.c_split = L.co;
-    w.ga.Hg = L.ho;
-    w.ga.Wg = L.wo;
-    w.ga.nimg = n;
-    w.gb = input_gather(c, l);
-    w.Mo = L.co;
-    w.No = 9 * L.ci;
-    w.P = n * L.ho * L.wo;
-    w.out = c.f(L.dwp);
+    WgradArgs w = conv_wgrad_args(c, l);  // weight gradient dW(l) = dY(l)^T x im2col(input of l)
+    const Src dy = w.ga.s[0];             // dY interior of the padded buffer
+    if (L.u_fwd && conc) {  // U issued by this step's forward on the side stream (FIFO before this wgrad)
+      w.wino_ws = c.f(L.uws);
+      w.wino_ws_bytes = L.uws.bytes;
+      w.u_ready = 1;
+    }
+    L.u_fwd = false;
     // fp32: when this weight gradient runs Winograd F(6x6), dY and its transform
     // Vd come out of one pass over dz and y (k_bnb_wino6_dy)
     bool fused_vd = false;
-    const bool early_u = conc && unet::g_wgrad_early_u;
+    const bool early_u = conc && unet::g_wgrad_early_u && !w.u_ready;
     if (p->prec == UNET_PREC_FP32 && ((unet::g_bnb_fuse && L.vdw.bytes) || early_u)) {
       WgradArgs q = w;
       prep_wgrad(cw, q);
@@ -1379,6 +1423,10 @@ unet_plan* unet_plan_create_ex(int n, int c_in, int h, int w, int n_classes, int
       Conv& L = p->L[l];
       if (L.co % 64 == 0) L.vdw = al.take(bnb_wino6_vd_bytes(n, L.ho, L.wo, L.co));
     }
+    for (int l = 1; l < 18 && unet::g_wgrad_fwd_u; ++l) {
+      Conv& L = p->L[l];
+      L.uws = al.take(wino_ws_bytes_grid(n, L.ho, L.wo, L.ci, L.co));
+    }
   }
   // slab-mode weight gradients (ring tiles 26-33 with per_cu codes 11 / 12,
   // pixel-column tiles with codes 101-104): one [Mo][No] fp32 plane per pixel
@@ -1398,6 +1446,7 @@ void unet_plan_destroy(unet_plan* p) {
     for (auto ev : p->ev_seg) (void)hipEventDestroy(ev);
     (void)hipEventDestroy(p->ev_join);
     (void)hipEventDestroy(p->ev_bwd0);
+    (void)hipEventDestroy(p->ev_fwdu);
     (void)hipStreamDestroy(p->side);
   }
   for (auto& e : p->evs) {
